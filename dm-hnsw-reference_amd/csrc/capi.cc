@@ -1,0 +1,468 @@
+// C ABI (include/shine_gpu.h): the HBM shard manager and the batched query entry points.
+//
+// Replaces, on the query side: MemoryNode (src/memory_node.hh:40-209: buffer allocation + dump load),
+// the remote-access token / entry-point distribution (compute_node.cc:258-268, rdma_reads.hh:74-99),
+// WorkerPool::process_queries + hnsw::schedule (worker_pool.hh:78-89, scheduler.hh:19-102) and the per-query
+// HNSW::knn coroutine (hnsw.hh:253-307).  One query per wavefront replaces one query per coroutine; the device
+// work queue replaces the lock-free query queue (query_router.hh:393 / scheduler.hh:64-77).
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/shine_gpu.h"
+#include "graph.h"
+#include "kernels.h"
+
+using namespace shine;
+
+namespace {
+
+constexpr uint32_t kLogCap = 32768;          // visited ids remembered per slot for O(visited) clearing
+constexpr uint32_t kLdsPerCu = 160 * 1024;   // gfx950
+constexpr uint32_t kCus = 256;
+
+#define HIP_TRY(expr)                                                                              \
+  do {                                                                                             \
+    hipError_t _e = (expr);                                                                        \
+    if (_e != hipSuccess)                                                                          \
+      return set_error(_e == hipErrorOutOfMemory ? SHINE_ERR_NOMEM : SHINE_ERR_HIP,                \
+                       std::string(#expr) + ": " + hipGetErrorString(_e));                         \
+  } while (0)
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  int grow(size_t want) {
+    if (want <= n) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(want, 1) * sizeof(T));
+    if (e != hipSuccess)
+      return set_error(e == hipErrorOutOfMemory ? SHINE_ERR_NOMEM : SHINE_ERR_HIP,
+                       std::string("hipMalloc: ") + hipGetErrorString(e));
+    n = want;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+struct Replica {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  DevBuf<uint8_t> vec;
+  DevBuf<uint32_t> adj0, uid, up_base, adjU, inv_uid;
+  // search scratch
+  DevBuf<uint32_t> visited, vlog, counter;
+  uint32_t slots = 0;
+  // staging for the host-pointer API
+  DevBuf<float> q, d;
+  DevBuf<uint32_t> ids, qs, qmap;
+};
+
+}  // namespace
+
+struct shine_index {
+  uint32_t dim = 0, M = 0, M0 = 0;
+  int metric = 0, elem = 0;
+  uint64_t N = 0, upper_rows = 0;
+  uint32_t ep = 0, ep_level = 0, ep_uid = 0, n_shards = 0, lists_unique = 1;
+  uint32_t inv_size = 0;
+  uint64_t words_per_slot = 0;
+  uint64_t device_bytes = 0;
+  std::vector<Replica> reps;
+  std::mutex mu;
+};
+
+namespace {
+
+DevGraph dev_graph(const shine_index* h, const Replica& r) {
+  DevGraph g{};
+  g.vec = r.vec.p;
+  g.adj0 = r.adj0.p;
+  g.uid = r.uid.p;
+  g.up_base = r.up_base.p;
+  g.adjU = r.adjU.p;
+  g.inv_uid = r.inv_uid.p;
+  g.inv_size = h->inv_size;
+  g.N = static_cast<uint32_t>(h->N);
+  g.M0 = h->M0;
+  g.MU = h->M;
+  g.ep = h->ep;
+  g.ep_level = h->ep_level;
+  g.lists_unique = h->lists_unique;
+  return g;
+}
+
+template <class T>
+int upload(DevBuf<T>& dst, const T* src, size_t n, hipStream_t s) {
+  if (int rc = dst.grow(std::max<size_t>(n, 1))) return rc;
+  if (n) HIP_TRY(hipMemcpyAsync(dst.p, src, n * sizeof(T), hipMemcpyHostToDevice, s));
+  return 0;
+}
+
+int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus, shine_index_t* out) {
+  if (!out) return set_error(SHINE_ERR_ARG, "out is NULL");
+  if (elem != SHINE_ELEM_F32 && elem != SHINE_ELEM_F16) return set_error(SHINE_ERR_ARG, "elem must be 0 (f32) or 1 (f16)");
+  if (!dim_supported(G.L.dim, elem))
+    return set_error(SHINE_ERR_ARG, "dim " + std::to_string(G.L.dim) + " has no compiled kernel for this element type");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (ndev <= 0) return set_error(SHINE_ERR_HIP, "no HIP device");
+  std::vector<int> devs;
+  if (!gpu_ids || n_gpus == 0) devs.push_back(0);
+  else devs.assign(gpu_ids, gpu_ids + n_gpus);
+  for (int d : devs)
+    if (d < 0 || d >= ndev) return set_error(SHINE_ERR_ARG, "gpu id " + std::to_string(d) + " out of range");
+
+  auto h = std::make_unique<shine_index>();
+  h->dim = G.L.dim;
+  h->M = G.L.M;
+  h->M0 = 2 * G.L.M;
+  h->metric = G.metric;
+  h->elem = elem;
+  h->N = G.N;
+  h->upper_rows = G.adjU.size() / G.L.M;
+  h->ep = G.ep;
+  h->ep_level = G.ep_level;
+  h->ep_uid = G.uid[G.ep];
+  h->n_shards = G.n_shards;
+  h->lists_unique = G.lists_unique ? 1 : 0;
+  h->words_per_slot = (G.N + 31) / 32;
+
+  // uid → dense id (for the distance-batch API); uids are the base-file positions, so dense-ish
+  uint32_t max_uid = 0;
+  for (uint32_t u : G.uid) max_uid = std::max(max_uid, u);
+  h->inv_size = max_uid + 1;
+  std::vector<uint32_t> inv(h->inv_size, kInvalid);
+  for (uint64_t g = 0; g < G.N; ++g) inv[G.uid[g]] = static_cast<uint32_t>(g);
+
+  std::vector<uint8_t> vbytes;
+  const uint8_t* vsrc = reinterpret_cast<const uint8_t*>(G.vec.data());
+  size_t vlen = G.vec.size() * sizeof(float);
+  if (elem == SHINE_ELEM_F16) {  // config 5: records converted to fp16 at load
+    vbytes.resize(G.vec.size() * sizeof(__half));
+    __half* hp = reinterpret_cast<__half*>(vbytes.data());
+    for (size_t i = 0; i < G.vec.size(); ++i) hp[i] = __float2half(G.vec[i]);
+    vsrc = vbytes.data();
+    vlen = vbytes.size();
+  }
+
+  h->reps.resize(devs.size());
+  for (size_t r = 0; r < devs.size(); ++r) {
+    Replica& R = h->reps[r];
+    R.device = devs[r];
+    HIP_TRY(hipSetDevice(R.device));
+    HIP_TRY(hipStreamCreateWithFlags(&R.stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&R.ev0));
+    HIP_TRY(hipEventCreate(&R.ev1));
+    if (int rc = upload(R.vec, vsrc, vlen, R.stream)) return rc;
+    if (int rc = upload(R.adj0, G.adj0.data(), G.adj0.size(), R.stream)) return rc;
+    if (int rc = upload(R.uid, G.uid.data(), G.uid.size(), R.stream)) return rc;
+    if (int rc = upload(R.up_base, G.up_base.data(), G.up_base.size(), R.stream)) return rc;
+    if (int rc = upload(R.adjU, G.adjU.data(), G.adjU.size(), R.stream)) return rc;
+    if (int rc = upload(R.inv_uid, inv.data(), inv.size(), R.stream)) return rc;
+    if (int rc = R.counter.grow(1)) return rc;
+    HIP_TRY(hipStreamSynchronize(R.stream));
+  }
+  h->device_bytes = vlen + 4 * (G.adj0.size() + G.uid.size() + G.up_base.size() + G.adjU.size() + inv.size());
+  *out = h.release();
+  return SHINE_OK;
+}
+
+// Candidate-queue capacity and slot count for a launch: enough resident wavefronts for the batch, the rest of
+// the CU's 160 KiB of LDS given to next_candidates.
+struct LaunchShape {
+  uint32_t cap, grid;
+};
+LaunchShape pick_shape(uint32_t nq, uint32_t ef, bool big) {
+  uint32_t waves_per_cu = std::max<uint32_t>(1, std::min<uint32_t>(16, (nq + kCus - 1) / kCus));
+  if (big) waves_per_cu = 1;
+  uint32_t lds = std::min<uint32_t>(kLdsPerCu / waves_per_cu, big ? kLdsPerCu : 64 * 1024);
+  lds &= ~15u;
+  int64_t cap = (static_cast<int64_t>(lds) - 8ll * ef - 512) / 8;
+  cap = std::max<int64_t>(cap, 64);
+  if (!big) {  // test hook: force a small first-pass queue so the overflow re-run path is exercised
+    if (const char* env = std::getenv("SHINE_DEBUG_CAP")) cap = std::max<int64_t>(1, std::atoll(env));
+  }
+  const uint32_t per_cu = std::max<uint32_t>(1, kLdsPerCu / static_cast<uint32_t>(search_lds_bytes(ef, static_cast<uint32_t>(cap))));
+  const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(nq, kCus * std::min<uint32_t>(per_cu, 16)));
+  return {static_cast<uint32_t>(cap), grid};
+}
+
+int ensure_slots(shine_index* h, Replica& R, uint32_t slots) {
+  if (slots <= R.slots) return 0;
+  R.visited.release();
+  R.vlog.release();
+  R.slots = 0;
+  if (int rc = R.visited.grow(static_cast<size_t>(slots) * h->words_per_slot)) return rc;
+  if (int rc = R.vlog.grow(static_cast<size_t>(slots) * kLogCap)) return rc;
+  HIP_TRY(hipMemsetAsync(R.visited.p, 0, R.visited.n * sizeof(uint32_t), R.stream));
+  HIP_TRY(hipStreamSynchronize(R.stream));
+  R.slots = slots;
+  return 0;
+}
+
+int enqueue_search(shine_index* h, Replica& R, const float* d_q, const uint32_t* d_qmap, uint32_t nq, uint32_t k,
+                   uint32_t ef, uint32_t* d_ids, float* d_dists, uint32_t* d_qs, hipStream_t s, bool big,
+                   bool timed) {
+  const LaunchShape sh = pick_shape(nq, ef, big);
+  if (int rc = ensure_slots(h, R, sh.grid)) return rc;
+  SearchArgs a{};
+  a.g = dev_graph(h, R);
+  a.queries = d_q;
+  a.qmap = d_qmap;
+  a.nq = nq;
+  a.k = k;
+  a.ef = ef;
+  a.cap = sh.cap;
+  a.out_ids = d_ids;
+  a.out_dists = d_dists;
+  a.qstats = d_qs;
+  a.visited = R.visited.p;
+  a.words_per_slot = h->words_per_slot;
+  a.vlog = R.vlog.p;
+  a.log_cap = kLogCap;
+  a.counter = R.counter.p;
+  HIP_TRY(hipMemsetAsync(R.counter.p, 0, sizeof(uint32_t), s));
+  if (timed) HIP_TRY(hipEventRecord(R.ev0, s));
+  hipError_t e = launch_search(h->dim, h->metric, h->elem, sh.grid, a, s);
+  if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("search launch: ") + hipGetErrorString(e));
+  if (timed) HIP_TRY(hipEventRecord(R.ev1, s));
+  return 0;
+}
+
+int check_knn_args(shine_index* h, uint32_t k, uint32_t ef) {
+  if (!h) return set_error(SHINE_ERR_ARG, "index handle is NULL");
+  if (k == 0) return set_error(SHINE_ERR_ARG, "k must be > 0");
+  if (ef < k) return set_error(SHINE_ERR_ARG, "ef_search must be >= k");  // hnsw.hh:36
+  if (ef > 4096) return set_error(SHINE_ERR_ARG, "ef_search must be <= 4096");
+  return 0;
+}
+
+uint64_t bq_bytes(const shine_index* h, const uint32_t* qs) {  // B_q
+  const uint64_t e = h->elem == SHINE_ELEM_F16 ? 2 : 4;
+  return qs[SHINE_QS_DISTCOMPS] * h->dim * e + qs[SHINE_QS_LISTS_L0] * (4ull + 4ull * h->M0) +
+         qs[SHINE_QS_LISTS_UPPER] * (4ull + 4ull * h->M) + h->dim * e;
+}
+
+uint64_t ref_read_bytes(const shine_index* h, const uint32_t* qs) {  // rdma_reads.hh:12,46 accounting
+  const uint64_t node = 16 + 4ull * h->dim;
+  const uint64_t node_reads = qs[SHINE_QS_DISTCOMPS] > 0 ? qs[SHINE_QS_DISTCOMPS] - 1 : 0;
+  return node_reads * node + qs[SHINE_QS_LISTS_L0] * (4ull + 8ull * h->M0) + qs[SHINE_QS_LISTS_UPPER] * (4ull + 8ull * h->M);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* shine_last_error(void) { return last_error(); }
+
+int shine_open_buffers(const uint8_t* const* dumps, const uint64_t* sizes, uint32_t n_dumps, uint32_t dim,
+                       uint32_t M, int metric, int elem, const int* gpu_ids, uint32_t n_gpus, shine_index_t* out) {
+  if (!dumps || !sizes) return set_error(SHINE_ERR_ARG, "dumps / sizes is NULL");
+  if (metric != SHINE_METRIC_L2 && metric != SHINE_METRIC_IP) return set_error(SHINE_ERR_ARG, "metric must be 0 or 1");
+  HostGraph G;
+  if (int rc = parse_dumps(dumps, sizes, n_dumps, dim, M, metric, 0, G)) return rc;
+  return make_index(G, elem, gpu_ids, n_gpus, out);
+}
+
+int shine_open(const char* const* dump_paths, uint32_t n_dumps, uint32_t dim, uint32_t M, int metric, int elem,
+               const int* gpu_ids, uint32_t n_gpus, shine_index_t* out) {
+  if (!dump_paths || n_dumps == 0) return set_error(SHINE_ERR_ARG, "no dump paths");
+  std::vector<std::vector<uint8_t>> files(n_dumps);
+  std::vector<const uint8_t*> ptrs(n_dumps);
+  std::vector<uint64_t> sizes(n_dumps);
+  for (uint32_t i = 0; i < n_dumps; ++i) {
+    if (!dump_paths[i]) return set_error(SHINE_ERR_ARG, "dump path is NULL");
+    if (int rc = read_file(dump_paths[i], files[i])) return rc;
+    ptrs[i] = files[i].data();
+    sizes[i] = files[i].size();
+  }
+  return shine_open_buffers(ptrs.data(), sizes.data(), n_dumps, dim, M, metric, elem, gpu_ids, n_gpus, out);
+}
+
+int shine_index_get_info(shine_index_t h, shine_index_info* o) {
+  if (!h || !o) return set_error(SHINE_ERR_ARG, "NULL argument");
+  std::memset(o, 0, sizeof(*o));
+  o->num_nodes = h->N;
+  o->num_upper_rows = h->upper_rows;
+  o->device_bytes = h->device_bytes;
+  o->dim = h->dim;
+  o->M = h->M;
+  o->metric = static_cast<uint32_t>(h->metric);
+  o->elem = static_cast<uint32_t>(h->elem);
+  o->max_level = h->ep_level;
+  o->entry_uid = h->ep_uid;
+  o->n_shards = h->n_shards;
+  o->n_gpus = static_cast<uint32_t>(h->reps.size());
+  return SHINE_OK;
+}
+
+uint64_t shine_algorithmic_bytes(shine_index_t h, const uint32_t* qstats, uint32_t nq) {
+  if (!h || !qstats) return 0;
+  uint64_t t = 0;
+  for (uint32_t i = 0; i < nq; ++i) t += bq_bytes(h, qstats + static_cast<size_t>(i) * SHINE_QS_WORDS);
+  return t;
+}
+
+int shine_knn_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_queries, uint32_t nq, uint32_t k,
+                           uint32_t ef, uint32_t* d_out_ids, float* d_out_dists, uint32_t* d_qstats, void* stream) {
+  if (int rc = check_knn_args(h, k, ef)) return rc;
+  if (gpu_slot >= h->reps.size()) return set_error(SHINE_ERR_ARG, "gpu_slot out of range");
+  if (nq == 0) return SHINE_OK;
+  if (!d_queries || !d_out_ids) return set_error(SHINE_ERR_ARG, "NULL device pointer");
+  std::lock_guard<std::mutex> lk(h->mu);
+  Replica& R = h->reps[gpu_slot];
+  HIP_TRY(hipSetDevice(R.device));
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : R.stream;
+  return enqueue_search(h, R, d_queries, nullptr, nq, k, ef, d_out_ids, d_out_dists, d_qstats, s, false, false);
+}
+
+int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t k, uint32_t ef, uint32_t* out_ids,
+                    float* out_dists, uint32_t* qstats, shine_stats* stats) {
+  if (int rc = check_knn_args(h, k, ef)) return rc;
+  if (stats) std::memset(stats, 0, sizeof(*stats));
+  if (nq == 0) return SHINE_OK;
+  if (!queries || !out_ids) return set_error(SHINE_ERR_ARG, "NULL host pointer");
+  std::lock_guard<std::mutex> lk(h->mu);
+  const uint32_t G = static_cast<uint32_t>(h->reps.size());
+  const size_t d = h->dim;
+  // queries are split over the replicas round-robin by position, as compute nodes split them by id
+  // (read_data.hh:57-58: id % num_clients == client_id)
+  std::vector<std::vector<uint32_t>> part(G);
+  for (uint32_t i = 0; i < nq; ++i) part[i % G].push_back(i);
+  std::vector<std::vector<float>> qbuf(G);
+  std::vector<std::vector<uint32_t>> ibuf(G), sbuf(G);
+  std::vector<std::vector<float>> dbuf(G);
+  for (uint32_t r = 0; r < G; ++r) {
+    const uint32_t n = static_cast<uint32_t>(part[r].size());
+    if (n == 0) continue;
+    Replica& R = h->reps[r];
+    HIP_TRY(hipSetDevice(R.device));
+    qbuf[r].resize(n * d);
+    for (uint32_t j = 0; j < n; ++j) std::memcpy(&qbuf[r][j * d], queries + part[r][j] * d, d * sizeof(float));
+    if (int rc = upload(R.q, qbuf[r].data(), qbuf[r].size(), R.stream)) return rc;
+    if (int rc = R.ids.grow(static_cast<size_t>(n) * k)) return rc;
+    if (int rc = R.d.grow(static_cast<size_t>(n) * k)) return rc;
+    if (int rc = R.qs.grow(static_cast<size_t>(n) * SHINE_QS_WORDS)) return rc;
+    if (int rc = enqueue_search(h, R, R.q.p, nullptr, n, k, ef, R.ids.p, R.d.p, R.qs.p, R.stream, false, true))
+      return rc;
+  }
+  double kernel_ms = 0;
+  uint64_t retries = 0;
+  for (uint32_t r = 0; r < G; ++r) {
+    const uint32_t n = static_cast<uint32_t>(part[r].size());
+    if (n == 0) continue;
+    Replica& R = h->reps[r];
+    HIP_TRY(hipSetDevice(R.device));
+    sbuf[r].resize(static_cast<size_t>(n) * SHINE_QS_WORDS);
+    HIP_TRY(hipMemcpyAsync(sbuf[r].data(), R.qs.p, sbuf[r].size() * 4, hipMemcpyDeviceToHost, R.stream));
+    HIP_TRY(hipStreamSynchronize(R.stream));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, R.ev0, R.ev1));
+    kernel_ms = std::max(kernel_ms, static_cast<double>(ms));
+    // queries whose next_candidates outgrew the LDS queue: re-run them alone with the whole CU's LDS
+    std::vector<uint32_t> redo;
+    for (uint32_t j = 0; j < n; ++j)
+      if (sbuf[r][j * SHINE_QS_WORDS + SHINE_QS_STATUS] == SHINE_ERR_OVERFLOW) redo.push_back(j);
+    if (!redo.empty()) {
+      retries += redo.size();
+      if (int rc = upload(R.qmap, redo.data(), redo.size(), R.stream)) return rc;
+      if (int rc = enqueue_search(h, R, R.q.p, R.qmap.p, static_cast<uint32_t>(redo.size()), k, ef, R.ids.p, R.d.p,
+                                  R.qs.p, R.stream, true, true))
+        return rc;
+      HIP_TRY(hipMemcpyAsync(sbuf[r].data(), R.qs.p, sbuf[r].size() * 4, hipMemcpyDeviceToHost, R.stream));
+      HIP_TRY(hipStreamSynchronize(R.stream));
+      HIP_TRY(hipEventElapsedTime(&ms, R.ev0, R.ev1));
+      kernel_ms += ms;
+    }
+    ibuf[r].resize(static_cast<size_t>(n) * k);
+    dbuf[r].resize(static_cast<size_t>(n) * k);
+    HIP_TRY(hipMemcpyAsync(ibuf[r].data(), R.ids.p, ibuf[r].size() * 4, hipMemcpyDeviceToHost, R.stream));
+    HIP_TRY(hipMemcpyAsync(dbuf[r].data(), R.d.p, dbuf[r].size() * 4, hipMemcpyDeviceToHost, R.stream));
+    HIP_TRY(hipStreamSynchronize(R.stream));
+  }
+  int rc = SHINE_OK;
+  shine_stats agg{};
+  for (uint32_t r = 0; r < G; ++r) {
+    for (size_t j = 0; j < part[r].size(); ++j) {
+      const uint32_t qi = part[r][j];
+      std::memcpy(out_ids + static_cast<size_t>(qi) * k, &ibuf[r][j * k], k * 4);
+      if (out_dists) std::memcpy(out_dists + static_cast<size_t>(qi) * k, &dbuf[r][j * k], k * 4);
+      const uint32_t* qs = &sbuf[r][j * SHINE_QS_WORDS];
+      if (qstats) std::memcpy(qstats + static_cast<size_t>(qi) * SHINE_QS_WORDS, qs, SHINE_QS_WORDS * 4);
+      if (qs[SHINE_QS_STATUS] != 0 && rc == SHINE_OK)
+        rc = set_error(static_cast<int>(qs[SHINE_QS_STATUS]),
+                       "query " + std::to_string(qi) + " failed with status " + std::to_string(qs[SHINE_QS_STATUS]));
+      agg.processed += qs[SHINE_QS_STATUS] == 0 ? 1 : 0;
+      agg.distcomps += qs[SHINE_QS_DISTCOMPS];
+      agg.visited_nodes += qs[SHINE_QS_VISITED_UPPER];
+      agg.visited_nodes_l0 += qs[SHINE_QS_VISITED_L0];
+      agg.visited_neighborlists += qs[SHINE_QS_LISTS_L0] + qs[SHINE_QS_LISTS_UPPER];
+      agg.visited_neighborlists_l0 += qs[SHINE_QS_LISTS_L0];
+      agg.rdma_reads_in_bytes += ref_read_bytes(h, qs);
+      agg.algorithmic_bytes += bq_bytes(h, qs);
+    }
+  }
+  agg.overflow_retries = retries;
+  agg.kernel_ms = kernel_ms;
+  if (stats) *stats = agg;
+  return rc;
+}
+
+int shine_distance_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_queries, uint32_t nq,
+                                const uint32_t* d_node_uids, uint32_t n_per_query, float* d_out, void* stream) {
+  if (!h) return set_error(SHINE_ERR_ARG, "index handle is NULL");
+  if (gpu_slot >= h->reps.size()) return set_error(SHINE_ERR_ARG, "gpu_slot out of range");
+  if (nq == 0 || n_per_query == 0) return SHINE_OK;
+  if (!d_queries || !d_node_uids || !d_out) return set_error(SHINE_ERR_ARG, "NULL device pointer");
+  std::lock_guard<std::mutex> lk(h->mu);
+  Replica& R = h->reps[gpu_slot];
+  HIP_TRY(hipSetDevice(R.device));
+  DistArgs a{};
+  a.g = dev_graph(h, R);
+  a.queries = d_queries;
+  a.nq = nq;
+  a.node_uids = d_node_uids;
+  a.n_per = n_per_query;
+  a.out = d_out;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : R.stream;
+  hipError_t e = launch_distance(h->dim, h->metric, h->elem, a, s);
+  if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("distance launch: ") + hipGetErrorString(e));
+  return SHINE_OK;
+}
+
+int shine_close(shine_index_t h) {
+  if (!h) return SHINE_OK;
+  for (auto& R : h->reps) {
+    (void)hipSetDevice(R.device);
+    if (R.stream) (void)hipStreamSynchronize(R.stream);
+    for (auto* b : {&R.adj0, &R.uid, &R.up_base, &R.adjU, &R.inv_uid, &R.visited, &R.vlog, &R.counter, &R.ids, &R.qs,
+                    &R.qmap})
+      b->release();
+    R.vec.release();
+    R.q.release();
+    R.d.release();
+    if (R.ev0) (void)hipEventDestroy(R.ev0);
+    if (R.ev1) (void)hipEventDestroy(R.ev1);
+    if (R.stream) (void)hipStreamDestroy(R.stream);
+  }
+  delete h;
+  return SHINE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,119 @@
+"""ctypes binding of libshine_gpu.so (include/shine_gpu.h).
+
+The library is the product: there is no fallback.  If it is missing or fails to load, every entry point
+raises ShineError — a GPU box without the HIP extension must fail loudly, never run something else.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+PKG_ROOT = Path(__file__).resolve().parent.parent          # dm-hnsw-reference_amd/
+REPO_ROOT = PKG_ROOT.parent
+LIB_PATH = Path(os.environ.get("SHINE_GPU_LIB", PKG_ROOT / "libshine_gpu.so"))
+HEADER = REPO_ROOT / "include" / "shine_gpu.h"
+
+OK, ERR_ARG, ERR_IO, ERR_FORMAT, ERR_HIP, ERR_NOMEM, ERR_OVERFLOW = range(7)
+METRIC_L2, METRIC_IP = 0, 1
+ELEM_F32, ELEM_F16 = 0, 1
+QS_DISTCOMPS, QS_VISITED_UPPER, QS_VISITED_L0, QS_LISTS_UPPER, QS_LISTS_L0, QS_MAX_NEXT, QS_STATUS, QS_NRESULT = range(8)
+QS_WORDS = 8
+
+
+class ShineError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"shine error {code}: {msg}")
+        self.code = code
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("processed", C.c_uint64),
+        ("distcomps", C.c_uint64),
+        ("visited_nodes", C.c_uint64),
+        ("visited_nodes_l0", C.c_uint64),
+        ("visited_neighborlists", C.c_uint64),
+        ("visited_neighborlists_l0", C.c_uint64),
+        ("rdma_reads_in_bytes", C.c_uint64),
+        ("algorithmic_bytes", C.c_uint64),
+        ("overflow_retries", C.c_uint64),
+        ("kernel_ms", C.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class IndexInfo(C.Structure):
+    _fields_ = [
+        ("num_nodes", C.c_uint64),
+        ("num_upper_rows", C.c_uint64),
+        ("device_bytes", C.c_uint64),
+        ("dim", C.c_uint32),
+        ("M", C.c_uint32),
+        ("metric", C.c_uint32),
+        ("elem", C.c_uint32),
+        ("max_level", C.c_uint32),
+        ("entry_uid", C.c_uint32),
+        ("n_shards", C.c_uint32),
+        ("n_gpus", C.c_uint32),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+P = C.c_void_p
+U32, U64, I32 = C.c_uint32, C.c_uint64, C.c_int
+PU8 = C.POINTER(C.c_uint8)
+
+# name -> (restype, argtypes); must cover every function include/shine_gpu.h declares
+PROTOTYPES = {
+    "shine_open": (I32, [C.POINTER(C.c_char_p), U32, U32, U32, I32, I32, C.POINTER(I32), U32, C.POINTER(P)]),
+    "shine_open_buffers": (I32, [C.POINTER(PU8), C.POINTER(U64), U32, U32, U32, I32, I32, C.POINTER(I32), U32,
+                                 C.POINTER(P)]),
+    "shine_knn_batch": (I32, [P, P, U32, U32, U32, P, P, P, C.POINTER(Stats)]),
+    "shine_knn_batch_device": (I32, [P, U32, P, U32, U32, U32, P, P, P, P]),
+    "shine_distance_batch_device": (I32, [P, U32, P, U32, P, U32, P, P]),
+    "shine_index_get_info": (I32, [P, C.POINTER(IndexInfo)]),
+    "shine_algorithmic_bytes": (U64, [P, P, U32]),
+    "shine_close": (I32, [P]),
+    "shine_last_error": (C.c_char_p, []),
+    "shine_build": (I32, [P, U64, U32, U32, U32, I32, U32, U32, U32, C.POINTER(P)]),
+    "shine_build_dump_size": (U64, [P, U32]),
+    "shine_build_dump_data": (P, [P, U32]),
+    "shine_build_distcomps": (U64, [P]),
+    "shine_build_write": (I32, [P, C.c_char_p, U32, U32]),
+    "shine_build_free": (I32, [P]),
+}
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libshine_gpu.so once; raise ShineError if it is absent (no fallback path exists)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise ShineError(ERR_HIP, f"{LIB_PATH} not built: run __graft_entry__.build() (make -C "
+                                      f"dm-hnsw-reference_amd/csrc)")
+        L = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in PROTOTYPES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != OK:
+        raise ShineError(rc, lib().shine_last_error().decode(errors="replace"))
+
+
+def declared_symbols() -> list[str]:
+    """Function names declared in include/shine_gpu.h (parsed from the header text)."""
+    import re
+    text = HEADER.read_text()
+    return sorted(set(re.findall(r"\b(shine_[a-z_0-9]+)\s*\(", text)))

@@ -1,0 +1,110 @@
+"""Synthetic workloads shaped like the reference's datasets (no datasets can be fetched here).
+
+* `sift_like`  — SIFT-shaped: integer-valued f32 in [0, 255], d = 128 (SURVEY §8d cfg 1/2).  A Gaussian mixture
+  in a low-dimensional latent space with a power-law spectrum, projected to d and quantised.  Integer values
+  make every L2 partial sum exact in f32 (< 2^24), as for real SIFT / BIGANN u8 data.
+* `deep_like`  — DEEP-shaped: L2-normalised f32, d = 96 (cfg 3/4).
+* `tti_like`   — Text-to-Image-shaped: f32, d = 200, inner product (cfg 5).
+* `zipf_query_mix` — scripts/data/skew.py:80-172 query replay (Zipf α, warm-up split).
+Model parameters come from a fixed seed, sample draws from `seed`, so base and queries share a distribution.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+_MODEL_SEED = 0x5EED
+
+
+def _latent_mixture(n, d, seed, latent, centres, spectrum, model_key):
+    rm = np.random.default_rng([_MODEL_SEED, model_key, d, latent, centres])
+    C = rm.normal(0.0, 1.0, (centres, latent)).astype(np.float32) * 2.5
+    scale = (np.arange(1, latent + 1, dtype=np.float32) ** -spectrum)
+    P = rm.normal(0.0, 1.0, (d, latent)).astype(np.float32) / np.float32(math.sqrt(latent))
+    rng = np.random.default_rng(seed)
+    out = np.empty((n, d), dtype=np.float32)
+    step = 1 << 16
+    for s in range(0, n, step):
+        m = min(step, n - s)
+        lab = rng.integers(0, centres, m)
+        z = (C[lab] + rng.normal(0.0, 1.0, (m, latent)).astype(np.float32)) * scale
+        out[s:s + m] = z @ P.T
+    return out
+
+
+def sift_like(n: int, seed: int = 1, d: int = 128) -> np.ndarray:
+    x = _latent_mixture(n, d, seed, latent=32, centres=256, spectrum=0.6, model_key=1)
+    x = np.rint(x * 24.0 + 40.0)
+    np.clip(x, 0.0, 255.0, out=x)
+    return x.astype(np.float32)
+
+
+def deep_like(n: int, seed: int = 1, d: int = 96) -> np.ndarray:
+    x = _latent_mixture(n, d, seed, latent=32, centres=512, spectrum=0.5, model_key=2)
+    x /= np.maximum(np.linalg.norm(x, axis=1, keepdims=True), 1e-12)
+    return x.astype(np.float32)
+
+
+def tti_like(n: int, seed: int = 1, d: int = 200) -> np.ndarray:
+    x = _latent_mixture(n, d, seed, latent=48, centres=512, spectrum=0.5, model_key=3)
+    x /= np.maximum(np.linalg.norm(x, axis=1, keepdims=True), 1e-12)
+    return (x * np.float32(0.8)).astype(np.float32)
+
+
+def brute_force_knn(base: np.ndarray, queries: np.ndarray, k: int, metric: int = 0, chunk: int = 256):
+    """Exact top-k (ties by id), distances in f64.  metric 0 = squared L2, 1 = 1 - <q, x>."""
+    b = base.astype(np.float64)
+    bn = (b * b).sum(1)
+    ids = np.empty((queries.shape[0], k), dtype=np.uint32)
+    dd = np.empty((queries.shape[0], k), dtype=np.float64)
+    for s in range(0, queries.shape[0], chunk):
+        q = queries[s:s + chunk].astype(np.float64)
+        ip = q @ b.T
+        dist = (q * q).sum(1)[:, None] + bn[None, :] - 2.0 * ip if metric == 0 else 1.0 - ip
+        part = np.argpartition(dist, k - 1, axis=1)[:, :k] if k < dist.shape[1] else \
+            np.tile(np.arange(dist.shape[1]), (dist.shape[0], 1))
+        # widen to include ties at the k-th distance, then order by (distance, id)
+        for r in range(dist.shape[0]):
+            kth = dist[r, part[r]].max()
+            cand = np.nonzero(dist[r] <= kth)[0]
+            order = np.lexsort((cand, dist[r, cand]))[:k]
+            ids[s + r] = cand[order]
+            dd[s + r] = dist[r, cand[order]]
+    return ids, dd
+
+
+def recall_at_k(results: np.ndarray, gt: np.ndarray, k: int) -> float:
+    """compute_node.cc:579-600 — Σ_q |result_q ∩ GT_q[0:k]| / (nq·k), set semantics."""
+    hits = 0
+    for r, g in zip(results, gt):
+        hits += len(set(r[:k].tolist()) & set(g[:k].tolist()))
+    return hits / (results.shape[0] * k)
+
+
+def harmonic_number(n: int, alpha: float) -> float:  # skew.py:14-19
+    return float(np.sum(1.0 / np.arange(1, n + 1, dtype=np.float64) ** alpha))
+
+
+def zipf_query_mix(pool: np.ndarray, num_queries: int, alpha: float, split: int = 0, seed: int = 0):
+    """skew.py:114-164: query i of the pool is repeated ceil(num_queries * pmf(i+1)) times (until num_queries
+    are drawn), the multiset is shuffled, and the last `split` become the warm-up set.  Returns
+    (queries, warmup, pool_index_of_each_query)."""
+    n = pool.shape[0]
+    h = harmonic_number(n, alpha)
+    counts = []
+    drawn = 0
+    for idx in range(n):
+        if drawn >= num_queries:
+            break
+        occ = math.ceil(num_queries * ((1.0 / (idx + 1) ** alpha) / h))
+        counts.append(occ)
+        drawn += occ
+    if drawn > num_queries:  # skew.py:141 TODO: trim the last count instead of asserting
+        counts[-1] -= drawn - num_queries
+    src = np.repeat(np.arange(len(counts)), counts)
+    perm = np.random.default_rng(seed).permutation(num_queries)
+    src = src[perm]
+    q = pool[src]
+    nq = num_queries - split
+    return q[:nq], q[nq:], src

@@ -1,0 +1,141 @@
+"""Host-side API over the C ABI, shaped after the reference's query interface.
+
+`Index` plays the memory-node tier plus `HNSW<Distance>` (src/memory_node.hh, src/hnsw/hnsw.hh): it is opened
+from the memory nodes' dumps and answers `knn` for a batch.  `build()` runs the parallel restatement of
+`HNSW::insert` and returns the dump images.  Device-pointer entry points take raw integers (e.g.
+`tensor.data_ptr()`) so that torch stays plumbing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _gpus(gpus):
+    if not gpus:
+        return None, 0
+    arr = (C.c_int * len(gpus))(*gpus)
+    return arr, len(gpus)
+
+
+@dataclass
+class KnnResult:
+    ids: np.ndarray      # (nq, k) uint32 uids, reference result order (heap-array order)
+    dists: np.ndarray    # (nq, k) float32
+    qstats: np.ndarray   # (nq, 8) uint32, SHINE_QS_* layout
+    stats: dict          # aggregates (statistics.hh names)
+
+
+class Index:
+    def __init__(self, handle: int, dim: int, metric: int):
+        self._h = C.c_void_p(handle)
+        self.dim = dim
+        self.metric = metric
+
+    # ---- construction ----------------------------------------------------------------------------------
+    @classmethod
+    def open(cls, dump_paths, dim: int, M: int, metric: int = L.METRIC_L2, elem: int = L.ELEM_F32, gpus=None):
+        arr = (C.c_char_p * len(dump_paths))(*[str(p).encode() for p in dump_paths])
+        g, ng = _gpus(gpus)
+        h = C.c_void_p()
+        L.check(L.lib().shine_open(arr, len(dump_paths), dim, M, metric, elem, g, ng, C.byref(h)))
+        return cls(h.value, dim, metric)
+
+    @classmethod
+    def from_buffers(cls, dumps, dim: int, M: int, metric: int = L.METRIC_L2, elem: int = L.ELEM_F32, gpus=None):
+        dumps = [np.ascontiguousarray(np.frombuffer(d, dtype=np.uint8) if not isinstance(d, np.ndarray) else d,
+                                      dtype=np.uint8) for d in dumps]
+        ptrs = (C.POINTER(C.c_uint8) * len(dumps))(*[d.ctypes.data_as(C.POINTER(C.c_uint8)) for d in dumps])
+        sizes = (C.c_uint64 * len(dumps))(*[d.size for d in dumps])
+        g, ng = _gpus(gpus)
+        h = C.c_void_p()
+        L.check(L.lib().shine_open_buffers(ptrs, sizes, len(dumps), dim, M, metric, elem, g, ng, C.byref(h)))
+        return cls(h.value, dim, metric)
+
+    def close(self):
+        if self._h is not None and self._h.value:
+            L.check(L.lib().shine_close(self._h))
+        self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def info(self) -> dict:
+        inf = L.IndexInfo()
+        L.check(L.lib().shine_index_get_info(self._h, C.byref(inf)))
+        return inf.as_dict()
+
+    # ---- queries -----------------------------------------------------------------------------------------
+    def knn(self, queries: np.ndarray, k: int, ef: int) -> KnnResult:
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        if q.ndim != 2 or q.shape[1] != self.dim:
+            raise ValueError(f"queries must be (nq, {self.dim})")
+        nq = q.shape[0]
+        ids = np.empty((nq, k), dtype=np.uint32)
+        dists = np.empty((nq, k), dtype=np.float32)
+        qs = np.empty((nq, L.QS_WORDS), dtype=np.uint32)
+        st = L.Stats()
+        L.check(L.lib().shine_knn_batch(self._h, _ptr(q), nq, k, ef, _ptr(ids), _ptr(dists), _ptr(qs), C.byref(st)))
+        return KnnResult(ids, dists, qs, st.as_dict())
+
+    def knn_device(self, q_ptr: int, nq: int, k: int, ef: int, ids_ptr: int, dists_ptr: int | None,
+                   qstats_ptr: int | None, stream: int | None = None, gpu_slot: int = 0) -> None:
+        L.check(L.lib().shine_knn_batch_device(self._h, gpu_slot, C.c_void_p(q_ptr), nq, k, ef, C.c_void_p(ids_ptr),
+                                               C.c_void_p(dists_ptr) if dists_ptr else None,
+                                               C.c_void_p(qstats_ptr) if qstats_ptr else None,
+                                               C.c_void_p(stream) if stream else None))
+
+    def distance_device(self, q_ptr: int, nq: int, uids_ptr: int, n_per: int, out_ptr: int,
+                        stream: int | None = None, gpu_slot: int = 0) -> None:
+        L.check(L.lib().shine_distance_batch_device(self._h, gpu_slot, C.c_void_p(q_ptr), nq, C.c_void_p(uids_ptr),
+                                                    n_per, C.c_void_p(out_ptr),
+                                                    C.c_void_p(stream) if stream else None))
+
+    def algorithmic_bytes(self, qstats: np.ndarray) -> int:
+        qs = np.ascontiguousarray(qstats, dtype=np.uint32)
+        return int(L.lib().shine_algorithmic_bytes(self._h, _ptr(qs), qs.shape[0]))
+
+
+def build(base: np.ndarray, M: int, ef_construction: int, metric: int = L.METRIC_L2, n_shards: int = 1,
+          seed: int = 1234, threads: int = 0) -> tuple[list[np.ndarray], int]:
+    """Parallel HNSW::insert over base[0..n) (ids = positions).  Returns (dump images, build distcomps)."""
+    b = np.ascontiguousarray(base, dtype=np.float32)
+    h = C.c_void_p()
+    L.check(L.lib().shine_build(_ptr(b), b.shape[0], b.shape[1], M, ef_construction, metric, n_shards, seed,
+                                threads, C.byref(h)))
+    try:
+        dumps = []
+        for s in range(n_shards):
+            n = L.lib().shine_build_dump_size(h, s)
+            p = L.lib().shine_build_dump_data(h, s)
+            dumps.append(np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(n,)).copy())
+        dc = int(L.lib().shine_build_distcomps(h))
+    finally:
+        L.lib().shine_build_free(h)
+    return dumps, dc
+
+
+def dump_name(M: int, efc: int, i: int, n: int) -> str:
+    """compute_node.cc:428-430"""
+    return f"index_m{M}_efc{efc}_node{i + 1}_of{n}.dat"

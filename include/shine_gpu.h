@@ -1,0 +1,134 @@
+/*
+ * shine_gpu.h — C ABI of the MI355X-native SHINE compute-node query engine.
+ *
+ * This is the drop-in boundary for the reference's query path.  The reference has no FFI: its seam is the
+ * C++ template call `HNSW<Distance>::knn(q_id, span<f32>, thread)` (src/hnsw/hnsw.hh:253) reading remote
+ * memory through `rdma::read_node / read_neighborlist / read_entry_point_ptr` (src/rdma/rdma_reads.hh:9-99)
+ * from memory nodes that hold the dump `[free_ptr | ep_ptr | records...]` (src/memory_node.hh:15-27).
+ * Each entry point below names the reference interface it replaces.
+ *
+ * Conventions: every function returns SHINE_OK (0) or a positive error code; nothing calls exit().  The
+ * message for the last error on the calling thread is available from shine_last_error().  A handle may be
+ * used by one host thread at a time; distinct handles are independent.  No torch / HIP C++ types cross the
+ * boundary: streams are passed as `void*` (a hipStream_t, or NULL for the handle's own stream).
+ */
+#ifndef SHINE_GPU_H
+#define SHINE_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SHINE_OK 0
+#define SHINE_ERR_ARG 1      /* invalid argument (also: ef < k, hnsw.hh:36) */
+#define SHINE_ERR_IO 2       /* dump / file could not be read */
+#define SHINE_ERR_FORMAT 3   /* malformed dump (record walks past free_ptr, dangling RemotePtr, ...) */
+#define SHINE_ERR_HIP 4      /* HIP runtime error, or no usable gfx950 device */
+#define SHINE_ERR_NOMEM 5    /* device memory exhausted */
+#define SHINE_ERR_OVERFLOW 6 /* a query's candidate queue exceeded the largest supported capacity */
+
+#define SHINE_METRIC_L2 0 /* L2Distance (src/hnsw/distance.hh:153-155), squared L2 */
+#define SHINE_METRIC_IP 1 /* IPDistance (src/hnsw/distance.hh:157-161), 1 - <a,b> */
+
+#define SHINE_ELEM_F32 0 /* element_t = f32 (src/common/types.hh:9) */
+#define SHINE_ELEM_F16 1 /* vectors converted to fp16 at load (config 5); distances still accumulate in f32 */
+
+/* Per-query counter layout (u32 words), identical in the oracle and on the GPU. */
+#define SHINE_QS_DISTCOMPS 0     /* stats.distcomps                         (hnsw.hh:272,286,376,459) */
+#define SHINE_QS_VISITED_UPPER 1 /* stats.visited_nodes, level > 0          (statistics.hh:164-170) */
+#define SHINE_QS_VISITED_L0 2    /* stats.visited_nodes_l0                  (statistics.hh:164-170) */
+#define SHINE_QS_LISTS_UPPER 3   /* stats.visited_neighborlists, level > 0  (hnsw.hh:359) */
+#define SHINE_QS_LISTS_L0 4      /* stats.visited_neighborlists, level 0    (hnsw.hh:438) */
+#define SHINE_QS_MAX_NEXT 5      /* peak size of next_candidates (diagnostic) */
+#define SHINE_QS_STATUS 6        /* 0 = ok, otherwise the SHINE_ERR_* that stopped this query */
+#define SHINE_QS_NRESULT 7       /* number of ids written (< k only if the graph has fewer nodes) */
+#define SHINE_QS_WORDS 8
+
+typedef struct shine_index* shine_index_t;
+
+/* Aggregates, named after the reference's CNStatistics / ThreadStatistics (statistics.hh:68-175). */
+typedef struct shine_stats {
+  uint64_t processed;             /* queries.processed */
+  uint64_t distcomps;             /* queries.dist_comps */
+  uint64_t visited_nodes;         /* queries.visited_nodes (levels > 0) */
+  uint64_t visited_nodes_l0;      /* queries.visited_nodes_l0 */
+  uint64_t visited_neighborlists; /* queries.visited_neighborlists (all levels) */
+  uint64_t visited_neighborlists_l0;
+  uint64_t rdma_reads_in_bytes;   /* bytes the reference would READ from memory nodes for the same search */
+  uint64_t algorithmic_bytes;     /* roofline basis B_q summed over the batch */
+  uint64_t overflow_retries;      /* queries re-run with a larger candidate-queue capacity */
+  double kernel_ms;               /* device time of the search launch(es), HIP events */
+} shine_stats;
+
+typedef struct shine_index_info {
+  uint64_t num_nodes;      /* records found in all dumps */
+  uint64_t num_upper_rows; /* neighbour lists at levels >= 1 */
+  uint64_t device_bytes;   /* HBM held by the index on each GPU */
+  uint32_t dim, M, metric, elem;
+  uint32_t max_level;      /* level of the entry point */
+  uint32_t entry_uid;      /* uid of the entry point (ep_ptr in node1's dump, bytes 8..15) */
+  uint32_t n_shards;       /* dump files (memory nodes) */
+  uint32_t n_gpus;
+} shine_index_info;
+
+/* Open the index from the memory nodes' dumps `index_m{M}_efc{efC}_node{i}_of{N}.dat`, i = 1..N, in that
+ * order (replaces MemoryNode::store_or_load_index, memory_node.hh:130-209, plus the token/EP distribution,
+ * compute_node.cc:258-268 and rdma_reads.hh:74-99).  dim / M / metric are not stored in the dump; they come
+ * from the base file header and the file name, exactly as in the reference.  gpu_ids / n_gpus select the
+ * device(s); NULL / 0 means device 0.  With n_gpus > 1 every GPU holds a full replica. */
+int shine_open(const char* const* dump_paths, uint32_t n_dumps, uint32_t dim, uint32_t M, int metric, int elem,
+               const int* gpu_ids, uint32_t n_gpus, shine_index_t* out);
+
+/* Same, from dump images already in host memory (e.g. produced by shine_build). */
+int shine_open_buffers(const uint8_t* const* dumps, const uint64_t* sizes, uint32_t n_dumps, uint32_t dim,
+                       uint32_t M, int metric, int elem, const int* gpu_ids, uint32_t n_gpus, shine_index_t* out);
+
+/* knn over a batch of host-resident queries (replaces the WorkerPool::process_queries → hnsw::schedule →
+ * HNSW::knn loop, worker_pool.hh:78-89, scheduler.hh:19-102, hnsw.hh:253-307).  queries: nq × dim row-major.
+ * out_ids: nq × k uids, in the reference's result order (top_candidates heap-array order, hnsw.hh:300-303).
+ * out_dists (nullable): nq × k.  qstats (nullable): nq × SHINE_QS_WORDS.  stats (nullable): aggregates.
+ * Requires ef >= k (hnsw.hh:36).  Synchronous. */
+int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t k, uint32_t ef,
+                    uint32_t* out_ids, float* out_dists, uint32_t* qstats, shine_stats* stats);
+
+/* Same with device-resident inputs/outputs on GPU `gpu_slot` of the handle, enqueued on `stream`
+ * (hipStream_t; NULL = the handle's stream).  Asynchronous: returns after enqueue.  qstats (device,
+ * nullable).  Queries whose candidate queue overflowed are flagged in qstats[SHINE_QS_STATUS]; use
+ * shine_knn_batch (or check qstats) when exactness under overflow must be guaranteed. */
+int shine_knn_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_queries, uint32_t nq, uint32_t k,
+                           uint32_t ef, uint32_t* d_out_ids, float* d_out_dists, uint32_t* d_qstats, void* stream);
+
+/* Batched distance kernel: for query i and its n_per_query node uids node_uids[i*n_per_query + j], write
+ * out[i*n_per_query + j] = Distance::dist(q_i, x_uid) (distance.hh:153-161).  Device pointers, async. */
+int shine_distance_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_queries, uint32_t nq,
+                                const uint32_t* d_node_uids, uint32_t n_per_query, float* d_out, void* stream);
+
+int shine_index_get_info(shine_index_t h, shine_index_info* out);
+
+/* Total algorithmic bytes (roofline basis) for per-query counters produced by a search with this index. */
+uint64_t shine_algorithmic_bytes(shine_index_t h, const uint32_t* qstats, uint32_t nq);
+
+int shine_close(shine_index_t h);
+
+const char* shine_last_error(void);
+
+/* ----------------------------------------------------------------------------------------------------------
+ * Build path: a parallel CPU restatement of HNSW::insert (hnsw.hh:40-251) writing the
+ * reference's dump layout.  threads == 1 reproduces the single-threaded insert order exactly.
+ * -------------------------------------------------------------------------------------------------------- */
+typedef struct shine_build* shine_build_t;
+int shine_build(const float* base, uint64_t n, uint32_t dim, uint32_t M, uint32_t ef_construction, int metric,
+                uint32_t n_shards, uint32_t seed, uint32_t threads, shine_build_t* out);
+uint64_t shine_build_dump_size(shine_build_t b, uint32_t shard);
+const uint8_t* shine_build_dump_data(shine_build_t b, uint32_t shard);
+uint64_t shine_build_distcomps(shine_build_t b);
+int shine_build_write(shine_build_t b, const char* dir, uint32_t M, uint32_t ef_construction); /* dump/ files */
+int shine_build_free(shine_build_t b);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SHINE_GPU_H */

@@ -1,0 +1,118 @@
+"""ctypes wrapper of liboracle.so — TEST INFRASTRUCTURE ONLY (the checker).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+ORACLE_DIR = Path(__file__).resolve().parent
+LIB_PATH = ORACLE_DIR / "liboracle.so"
+QS_WORDS = 8
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"{LIB_PATH} missing: run `make -C oracle`")
+        L = C.CDLL(str(LIB_PATH))
+        P, U32, I32 = C.c_void_p, C.c_uint32, C.c_int
+        L.oracle_draw_levels.argtypes = [U32, U32, U32, U32, P, P]
+        L.oracle_build.restype = P
+        L.oracle_build.argtypes = [P, U32, U32, U32, U32, I32, U32, U32]
+        L.oracle_dump_size.restype = C.c_uint64
+        L.oracle_dump_size.argtypes = [P, U32]
+        L.oracle_dump_data.restype = P
+        L.oracle_dump_data.argtypes = [P, U32]
+        L.oracle_build_distcomps.restype = C.c_uint64
+        L.oracle_build_distcomps.argtypes = [P]
+        L.oracle_max_level.restype = U32
+        L.oracle_max_level.argtypes = [P]
+        L.oracle_open.restype = P
+        L.oracle_open.argtypes = [P, P, U32, U32, U32, I32]
+        L.oracle_free.argtypes = [P]
+        L.oracle_knn.restype = I32
+        L.oracle_knn.argtypes = [P, P, U32, U32, U32, P, P, P, U32]
+        L.oracle_distance.restype = C.c_float
+        L.oracle_distance.argtypes = [I32, P, P, U32]
+        L.oracle_selftest_heap.restype = I32
+        L.oracle_selftest_heap.argtypes = [I32, P, P, P, U32, U32, P, P, P]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def draw_levels(n, M, seed, n_shards=1):
+    lv = np.empty(n, np.uint32)
+    sh = np.empty(n, np.uint32)
+    lib().oracle_draw_levels(n, M, seed, n_shards, _p(lv), _p(sh))
+    return lv, sh
+
+
+def build(base: np.ndarray, M: int, efc: int, metric: int = 0, n_shards: int = 1, seed: int = 1234):
+    """Single-threaded HNSW::insert in slot order.  Returns (dumps, build_distcomps, max_level)."""
+    b = np.ascontiguousarray(base, dtype=np.float32)
+    h = lib().oracle_build(_p(b), b.shape[0], b.shape[1], M, efc, metric, n_shards, seed)
+    try:
+        dumps = []
+        for s in range(n_shards):
+            n = lib().oracle_dump_size(h, s)
+            p = lib().oracle_dump_data(h, s)
+            dumps.append(np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(n,)).copy())
+        return dumps, int(lib().oracle_build_distcomps(h)), int(lib().oracle_max_level(h))
+    finally:
+        lib().oracle_free(h)
+
+
+class OracleIndex:
+    def __init__(self, dumps, dim, M, metric=0):
+        self._dumps = [np.ascontiguousarray(d, dtype=np.uint8) for d in dumps]
+        ptrs = (C.c_void_p * len(dumps))(*[d.ctypes.data for d in self._dumps])
+        sizes = (C.c_uint64 * len(dumps))(*[d.size for d in self._dumps])
+        self._h = lib().oracle_open(ptrs, sizes, len(dumps), dim, M, metric)
+        self.dim = dim
+
+    def knn(self, queries, k, ef, threads=1):
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        nq = q.shape[0]
+        ids = np.empty((nq, k), np.uint32)
+        dd = np.empty((nq, k), np.float32)
+        qs = np.empty((nq, QS_WORDS), np.uint32)
+        rc = lib().oracle_knn(self._h, _p(q), nq, k, ef, _p(ids), _p(dd), _p(qs), threads)
+        if rc != 0:
+            raise RuntimeError(f"oracle_knn failed: {rc}")
+        return ids, dd, qs
+
+    def close(self):
+        if self._h:
+            lib().oracle_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+def distance(metric, a, b):
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    return float(lib().oracle_distance(metric, _p(a), _p(b), a.shape[0]))
+
+
+def heap_replay(is_max, ops, vals, ids, k=0):
+    ops = np.ascontiguousarray(ops, np.int32)
+    vals = np.ascontiguousarray(vals, np.float32)
+    ids = np.ascontiguousarray(ids, np.uint32)
+    od = np.empty(len(ops) + 1, np.float32)
+    oi = np.empty(len(ops) + 1, np.uint32)
+    on = np.zeros(1, np.uint32)
+    lib().oracle_selftest_heap(int(is_max), _p(ops), _p(vals), _p(ids), len(ops), k, _p(od), _p(oi), _p(on))
+    n = int(on[0])
+    return od[:n].copy(), oi[:n].copy()

@@ -1,0 +1,187 @@
+"""GPU parity: the HIP search / distance kernels through the C ABI vs the CPU oracle, on identical dumps.
+
+Bar (north star): identical neighbour ids.  Here the bar is stricter — the kernels reproduce the oracle's FP
+order and libstdc++'s heap algorithms, so ids (in heap-array order), distances (bitwise) and every per-query
+counter must be identical, ties included.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+import shine_amd
+from shine_amd import datasets as D
+
+pytestmark = pytest.mark.gpu
+
+
+def _check_same(r, ref_ids, ref_d, ref_qs):
+    assert (r.qstats[:, shine_amd.QS_STATUS] == 0).all()
+    np.testing.assert_array_equal(r.ids, ref_ids)
+    np.testing.assert_array_equal(r.dists.view(np.uint32), ref_d.view(np.uint32))
+    # distcomps, visited (upper, L0), lists (upper, L0), peak next size, n results
+    np.testing.assert_array_equal(r.qstats[:, [0, 1, 2, 3, 4, 5, 7]], ref_qs[:, [0, 1, 2, 3, 4, 5, 7]])
+
+
+CASES = [
+    # name, generator, n, nq, dim, M, efc, metric, shards, k, ef
+    ("sift_l2_m16", D.sift_like, 6000, 200, 128, 16, 100, 0, 1, 10, 64),
+    ("sift_l2_m16_3shards", D.sift_like, 6000, 200, 128, 16, 100, 0, 3, 10, 128),
+    ("sift_l2_m8_ef256", D.sift_like, 4000, 100, 128, 8, 64, 0, 2, 10, 256),
+    ("deep_ip_d96", D.deep_like, 5000, 150, 96, 16, 100, 1, 1, 10, 100),
+    ("deep_l2_d96", D.deep_like, 4000, 100, 96, 12, 80, 0, 4, 5, 40),
+    ("tti_ip_d200_tail", D.tti_like, 3000, 100, 200, 16, 80, 1, 2, 10, 64),
+    ("m32_lists64", D.sift_like, 3000, 100, 128, 32, 100, 0, 1, 10, 64),
+    ("k_eq_ef", D.sift_like, 2000, 64, 128, 16, 64, 0, 1, 20, 20),
+]
+
+
+@pytest.fixture(scope="module", params=CASES, ids=[c[0] for c in CASES])
+def case(request):
+    name, gen, n, nq, dim, M, efc, metric, shards, k, ef = request.param
+    base = gen(n, seed=101, d=dim)
+    q = gen(nq, seed=202, d=dim)
+    dumps, _, _ = O.build(base, M, efc, metric, shards, seed=5)
+    ref = O.OracleIndex(dumps, dim, M, metric).knn(q, k, ef)
+    return dict(base=base, q=q, dumps=dumps, dim=dim, M=M, metric=metric, k=k, ef=ef, ref=ref)
+
+
+def test_knn_parity(case, gpu_available):
+    with shine_amd.Index.from_buffers(case["dumps"], case["dim"], case["M"], case["metric"], gpus=[0]) as idx:
+        r = idx.knn(case["q"], case["k"], case["ef"])
+    _check_same(r, *case["ref"])
+
+
+def test_knn_device_entry(case, gpu_available):
+    import torch
+    q = torch.from_numpy(case["q"]).cuda()
+    nq, k = q.shape[0], case["k"]
+    ids = torch.empty((nq, k), dtype=torch.int32, device="cuda")
+    dd = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+    qs = torch.empty((nq, 8), dtype=torch.int32, device="cuda")
+    with shine_amd.Index.from_buffers(case["dumps"], case["dim"], case["M"], case["metric"], gpus=[0]) as idx:
+        idx.knn_device(q.data_ptr(), nq, k, case["ef"], ids.data_ptr(), dd.data_ptr(), qs.data_ptr(),
+                       stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    ref_ids, ref_d, ref_qs = case["ref"]
+    np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32), ref_ids)
+    np.testing.assert_array_equal(dd.cpu().numpy().view(np.uint32), ref_d.view(np.uint32))
+    np.testing.assert_array_equal(qs.cpu().numpy().view(np.uint32)[:, :5], ref_qs[:, :5])
+
+
+def test_overflow_rerun_path(gpu_available, monkeypatch):
+    """A first pass with a 24-entry next_candidates queue overflows; the re-run must give identical results."""
+    base = D.sift_like(4000, seed=7)
+    q = D.sift_like(64, seed=8)
+    dumps, _, _ = O.build(base, 16, 100, 0, 1, seed=3)
+    ref = O.OracleIndex(dumps, 128, 16, 0).knn(q, 10, 128)
+    assert ref[2][:, 5].max() > 24
+    monkeypatch.setenv("SHINE_DEBUG_CAP", "24")
+    with shine_amd.Index.from_buffers(dumps, 128, 16, 0, gpus=[0]) as idx:
+        r = idx.knn(q, 10, 128)
+    assert r.stats["overflow_retries"] > 0
+    _check_same(r, *ref)
+
+
+def test_repeated_batches_keep_visited_clean(gpu_available):
+    """The visited bitmaps are cleared per query from the visited log: re-running must not change anything."""
+    base = D.sift_like(5000, seed=21)
+    q = D.sift_like(300, seed=22)
+    dumps, _, _ = O.build(base, 16, 100, 0, 1, seed=4)
+    ref = O.OracleIndex(dumps, 128, 16, 0).knn(q, 10, 64)
+    with shine_amd.Index.from_buffers(dumps, 128, 16, 0, gpus=[0]) as idx:
+        for _ in range(3):
+            _check_same(idx.knn(q, 10, 64), *ref)
+        # a batch with fewer queries than slots, then a single query
+        r = idx.knn(q[:7], 10, 64)
+        np.testing.assert_array_equal(r.ids, ref[0][:7])
+        r = idx.knn(q[5:6], 10, 64)
+        np.testing.assert_array_equal(r.ids, ref[0][5:6])
+
+
+def test_duplicate_vectors_ties(gpu_available):
+    """Many exactly-equal distances (duplicated base vectors): tie order must follow libstdc++'s heaps."""
+    rng = np.random.default_rng(3)
+    uniq = np.rint(rng.uniform(0, 4, (300, 16))).astype(np.float32)
+    base = uniq[rng.integers(0, 300, 3000)]
+    q = np.rint(rng.uniform(0, 4, (100, 16))).astype(np.float32)
+    dumps, _, _ = O.build(base, 8, 40, 0, 2, seed=9)
+    ref = O.OracleIndex(dumps, 16, 8, 0).knn(q, 10, 50)
+    with shine_amd.Index.from_buffers(dumps, 16, 8, 0, gpus=[0]) as idx:
+        _check_same(idx.knn(q, 10, 50), *ref)
+
+
+@pytest.mark.parametrize("n", [1, 2, 17])
+def test_tiny_graphs(n, gpu_available):
+    base = D.sift_like(n, seed=31)
+    q = D.sift_like(9, seed=32)
+    dumps, _, _ = O.build(base, 4, 16, 0, 1, seed=1)
+    ref = O.OracleIndex(dumps, 128, 4, 0).knn(q, 10, 16)
+    with shine_amd.Index.from_buffers(dumps, 128, 4, 0, gpus=[0]) as idx:
+        r = idx.knn(q, 10, 16)
+    np.testing.assert_array_equal(r.ids, ref[0])
+    np.testing.assert_array_equal(r.qstats[:, 7], ref[2][:, 7])
+
+
+def test_distance_kernel_parity(gpu_available):
+    import torch
+    for dim, metric, gen in [(128, 0, D.sift_like), (96, 1, D.deep_like), (200, 1, D.tti_like), (100, 0, D.deep_like)]:
+        base = gen(500, seed=41, d=dim)
+        q = gen(33, seed=42, d=dim)
+        dumps, _, _ = O.build(base, 8, 32, metric, 1, seed=2)
+        rng = np.random.default_rng(dim)
+        uids = rng.integers(0, 500, (33, 77)).astype(np.uint32)
+        uids[0, 3] = 10_000  # unknown uid → NaN
+        with shine_amd.Index.from_buffers(dumps, dim, 8, metric, gpus=[0]) as idx:
+            qt = torch.from_numpy(q).cuda()
+            ut = torch.from_numpy(uids.view(np.int32)).cuda()
+            out = torch.empty((33, 77), dtype=torch.float32, device="cuda")
+            idx.distance_device(qt.data_ptr(), 33, ut.data_ptr(), 77, out.data_ptr(),
+                                stream=torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            got = out.cpu().numpy()
+        for i in range(33):
+            for j in range(77):
+                if i == 0 and j == 3:
+                    assert np.isnan(got[i, j])
+                    continue
+                ref = O.distance(metric, q[i], base[uids[i, j]])
+                assert np.float32(ref).view(np.uint32) == got[i, j].view(np.uint32), (dim, metric, i, j)
+
+
+def test_open_from_files_and_errors(tmp_path, gpu_available):
+    base = D.sift_like(1500, seed=51)
+    q = D.sift_like(20, seed=52)
+    dumps, _, _ = O.build(base, 16, 60, 0, 2, seed=6)
+    paths = []
+    for i, d in enumerate(dumps):
+        p = tmp_path / shine_amd.dump_name(16, 60, i, 2)
+        d.tofile(p)
+        paths.append(p)
+    ref = O.OracleIndex(dumps, 128, 16, 0).knn(q, 10, 32)
+    with shine_amd.Index.open(paths, 128, 16, 0, gpus=[0]) as idx:
+        info = idx.info()
+        assert info["num_nodes"] == 1500 and info["n_shards"] == 2
+        r = idx.knn(q, 10, 32)
+        np.testing.assert_array_equal(r.ids, ref[0])
+        with pytest.raises(shine_amd.ShineError) as e:
+            idx.knn(q, 10, 5)  # ef < k (hnsw.hh:36)
+        assert e.value.code == 1
+    with pytest.raises(shine_amd.ShineError) as e:
+        shine_amd.Index.open([tmp_path / "missing.dat"], 128, 16, 0, gpus=[0])
+    assert e.value.code == 2
+
+
+@pytest.mark.skipif(os.environ.get("SHINE_SKIP_F16") == "1", reason="disabled")
+def test_fp16_records_recall(gpu_available):
+    """Config 5 converts records to fp16 at load: ids cannot be bit-exact; recall must match the f32 path."""
+    base = D.tti_like(6000, seed=61)
+    q = D.tti_like(200, seed=62)
+    dumps, _, _ = O.build(base, 16, 100, 1, 2, seed=8)
+    gt, _ = D.brute_force_knn(base, q, 10, metric=1)
+    with shine_amd.Index.from_buffers(dumps, 200, 16, 1, elem=shine_amd.ELEM_F32, gpus=[0]) as i32, \
+            shine_amd.Index.from_buffers(dumps, 200, 16, 1, elem=shine_amd.ELEM_F16, gpus=[0]) as i16:
+        r32 = D.recall_at_k(i32.knn(q, 10, 128).ids, gt, 10)
+        r16 = D.recall_at_k(i16.knn(q, 10, 128).ids, gt, 10)
+    assert r16 >= r32 - 0.02, (r16, r32)
