@@ -1,0 +1,240 @@
+#!/usr/bin/env python3
+"""bench.py — QPS at recall@10 >= 0.95 on a SIFT1M-shaped index (BASELINE.json configs[1]).
+
+Workload (one "step" = one batch): 1,024 queries through HNSW::knn (k=10, ef=128) against a 1M x 128-d L2 index
+built with M=16, efC=200 by the parallel restatement of HNSW::insert, in the reference's dump layout.  Data are
+synthetic SIFT-shaped vectors (shine_amd.datasets.sift_like; no datasets can be fetched).  Queries and outputs
+are resident in HBM when the timed region starts; value = queries / wall time over exactly K steps.
+
+Multi-GPU (torchrun, one process per GPU): every rank holds a full replica of the 0.75 GiB index and answers its
+own batches (queries split id % G, read_data.hh:57-58) — weak scaling, no data-path collective.  Rank 0 builds
+the index once and shares the dump files; the max over ranks of the timed wall time gives `value`.
+
+Also reported: `roofline` for the search kernel (algorithmic bytes per launch / HIP-event kernel time vs 8 TB/s)
+and `cpu_baseline` (the CPU oracle — a C++ restatement of the reference's knn — on the host cores, bounded
+sample, rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "dm-hnsw-reference_amd"))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(msg):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def host_threads():
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except Exception:
+        return os.cpu_count() or 1
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--n", type=int, default=1_000_000)
+    p.add_argument("--dim", type=int, default=128)
+    p.add_argument("--batch", type=int, default=1024)
+    p.add_argument("--nbatches", type=int, default=10, help="distinct query batches per rank (cycled)")
+    p.add_argument("--k", type=int, default=10)
+    p.add_argument("--ef", type=int, default=128)
+    p.add_argument("--M", type=int, default=16)
+    p.add_argument("--efc", type=int, default=200)
+    p.add_argument("--shards", type=int, default=1, help="memory-node dumps the index is spread over")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of the CPU-baseline sample")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--cache", default=os.environ.get("SHINE_BENCH_CACHE", "/tmp/shine_bench"))
+    p.add_argument("--pmc-json", default=None, help="per-launch HBM bytes measured by rocprofv3 --pmc (tools/pmc.py)")
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import shine_amd
+    from shine_amd import datasets as D
+
+    key = hashlib.sha1(f"{a.n}-{a.dim}-{a.M}-{a.efc}-{a.shards}-sift_like-v2".encode()).hexdigest()[:12]
+    cache = Path(a.cache) / key
+    t0 = time.time()
+    base = D.sift_like(a.n, seed=1, d=a.dim)
+    log(f"rank {rank}: generated base {base.shape} in {time.time() - t0:.1f}s")
+    paths = [cache / "dump" / shine_amd.dump_name(a.M, a.efc, i, a.shards) for i in range(a.shards)]
+    if rank == 0 and not all(p.exists() for p in paths):
+        t0 = time.time()
+        dumps, bdc = shine_amd.build(base, a.M, a.efc, shine_amd.METRIC_L2, a.shards, seed=1234,
+                                     threads=host_threads())
+        log(f"built index: {sum(d.size for d in dumps) / 2**20:.0f} MiB in {time.time() - t0:.1f}s "
+            f"({host_threads()} threads, {bdc} distcomps)")
+        (cache / "dump").mkdir(parents=True, exist_ok=True)
+        for p, d in zip(paths, dumps):
+            tmp = p.with_suffix(".tmp")
+            d.tofile(tmp)
+            tmp.rename(p)
+        del dumps
+    if dist:
+        dist.barrier()
+    idx = shine_amd.Index.open(paths, a.dim, a.M, shine_amd.METRIC_L2, gpus=[local])
+    info = idx.info()
+    log(f"rank {rank}: index on GPU {local}: {info['num_nodes']} nodes, max level {info['max_level']}, "
+        f"{info['device_bytes'] / 2**20:.0f} MiB")
+
+    # queries: rank r takes ids ≡ r (mod G) of a common pool (read_data.hh:57-58)
+    nq_rank = a.batch * a.nbatches
+    pool = D.sift_like(nq_rank * world, seed=2, d=a.dim)
+    q = np.ascontiguousarray(pool[rank::world][:nq_rank])
+    qd = torch.from_numpy(q).cuda()
+    ids = torch.empty((a.nbatches, a.batch, a.k), dtype=torch.int32, device="cuda")
+    dists = torch.empty((a.nbatches, a.batch, a.k), dtype=torch.float32, device="cuda")
+    qs = torch.zeros((a.nbatches, a.batch, 8), dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def step(i, rec=None):
+        b = i % a.nbatches
+        if rec is not None:
+            rec[0].record(stream)
+        idx.knn_device(qd[b * a.batch:(b + 1) * a.batch].data_ptr(), a.batch, a.k, a.ef, ids[b].data_ptr(),
+                       dists[b].data_ptr(), qs[b].data_ptr(), stream=stream.cuda_stream)
+        if rec is not None:
+            rec[1].record(stream)
+
+    # one validation pass over every batch: status, recall, algorithmic bytes
+    for i in range(a.nbatches):
+        step(i)
+    torch.cuda.synchronize()
+    qs_h = qs.cpu().numpy().view(np.uint32).reshape(-1, 8)
+    n_bad = int((qs_h[:, 6] != 0).sum())
+    if n_bad:
+        raise SystemExit(f"{n_bad} queries did not complete (status {np.unique(qs_h[:, 6])})")
+    bq_batch = [idx.algorithmic_bytes(qs_h[b * a.batch:(b + 1) * a.batch]) for b in range(a.nbatches)]
+    # ground truth on the GPU (exact: integer-valued data keep every f32 partial sum < 2^24)
+    bt = torch.from_numpy(base).cuda()
+    bn = (bt * bt).sum(1)
+    gt = []
+    for s in range(0, nq_rank, 256):
+        qq = qd[s:s + 256]
+        dd = (qq * qq).sum(1)[:, None] + bn[None, :] - 2.0 * (qq @ bt.T)
+        gt.append(torch.topk(dd, a.k, largest=False).indices.cpu().numpy())
+    del bt, bn
+    gt = np.concatenate(gt)
+    res = ids.cpu().numpy().view(np.uint32).reshape(-1, a.k)
+    recall = D.recall_at_k(res, gt, a.k)
+    log(f"rank {rank}: recall@{a.k} = {recall:.4f} over {nq_rank} queries; mean distcomps "
+        f"{qs_h[:, 0].mean():.0f}, lists L0 {qs_h[:, 4].mean():.1f}")
+
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(a.warmup + i, evs[i])
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = t1 - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = [s.elapsed_time(e) for s, e in evs]
+    bytes_steps = [bq_batch[(a.warmup + i) % a.nbatches] for i in range(a.steps)]
+    achieved = sum(bytes_steps) / (sum(kern_ms) / 1e3) / 1e9  # GB/s
+    avg_launch_ms = float(np.mean(kern_ms))
+
+    traffic = None
+    if a.pmc_json and Path(a.pmc_json).exists():
+        traffic = json.loads(Path(a.pmc_json).read_text()).get("hbm_bytes_per_launch")
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu:
+        cpu = cpu_baseline(paths, q, a, recall)
+
+    if rank == 0:
+        total_q = a.steps * a.batch * world
+        out = {
+            "metric": "QPS at recall@10>=0.95, SIFT1M d=128 batch=1024",
+            "value": total_q / elapsed,
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed * 1e3 / a.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic SIFT-shaped (integer-valued f32, 1M x 128), random-seeded; index built in-run",
+            "recall_at_10": recall,
+            "config": {"workload": "SIFT1M-shaped L2 knn, M=16 efC=200 ef=128 k=10", "n": a.n, "dim": a.dim,
+                       "global_batch": a.batch * world, "batch_per_gpu": a.batch, "M": a.M, "efc": a.efc,
+                       "ef": a.ef, "k": a.k, "shards": a.shards, "parallelism": f"replica{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                         "kernel": "search_kernel<128,L2,f32>", "avg_launch_ms": avg_launch_ms,
+                         "algorithmic_bytes_per_launch": float(np.mean(bytes_steps)),
+                         "mean_distcomps_per_query": float(qs_h[:, 0].mean())},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    idx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(paths, q, a, gpu_recall):
+    """The oracle (C++ restatement of the reference's knn) on this host's cores, same dump, same queries."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as O
+    dumps = [np.fromfile(p, dtype=np.uint8) for p in paths]
+    I = O.OracleIndex(dumps, a.dim, a.M, 0)
+    th = host_threads()
+    n = min(q.shape[0], 512)
+    t0 = time.perf_counter()
+    I.knn(q[:n], a.k, a.ef, threads=th)
+    probe = time.perf_counter() - t0
+    reps = max(1, int(a.cpu_seconds / max(probe, 1e-3)))
+    t0 = time.perf_counter()
+    done = 0
+    for r in range(reps):
+        s = (r * n) % max(1, q.shape[0] - n + 1)
+        I.knn(q[s:s + n], a.k, a.ef, threads=th)
+        done += n
+    el = time.perf_counter() - t0
+    I.close()
+    log(f"cpu baseline: {done} queries in {el:.1f}s on {th} threads")
+    return {"value": done / el, "unit": "queries/s", "cores": th, "kind": "port",
+            "sample": f"{done} queries (batches of {n} from the bench's query set, k={a.k}, ef={a.ef}) on the "
+                      f"same dump, {th} threads, ~{a.cpu_seconds:.0f}s"}
+
+
+if __name__ == "__main__":
+    main()

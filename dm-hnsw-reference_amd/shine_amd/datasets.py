@@ -17,11 +17,16 @@ import numpy as np
 _MODEL_SEED = 0x5EED
 
 
-def _latent_mixture(n, d, seed, latent, centres, spectrum, model_key):
+def _model(d, latent, centres, spectrum, cs, model_key):
     rm = np.random.default_rng([_MODEL_SEED, model_key, d, latent, centres])
-    C = rm.normal(0.0, 1.0, (centres, latent)).astype(np.float32) * 2.5
-    scale = (np.arange(1, latent + 1, dtype=np.float32) ** -spectrum)
+    C = rm.normal(0.0, 1.0, (centres, latent)).astype(np.float32) * np.float32(cs)
+    scale = (np.arange(1, latent + 1, dtype=np.float32) ** -np.float32(spectrum))
     P = rm.normal(0.0, 1.0, (d, latent)).astype(np.float32) / np.float32(math.sqrt(latent))
+    return C, scale, P
+
+
+def _latent_mixture(n, d, seed, latent, centres, spectrum, model_key, cs=2.5):
+    C, scale, P = _model(d, latent, centres, spectrum, cs, model_key)
     rng = np.random.default_rng(seed)
     out = np.empty((n, d), dtype=np.float32)
     step = 1 << 16
@@ -33,9 +38,26 @@ def _latent_mixture(n, d, seed, latent, centres, spectrum, model_key):
     return out
 
 
+def _model_std(d, latent, centres, spectrum, model_key, cs):
+    """Fixed output scale of the model (from a fixed calibration draw), so base and queries quantise alike."""
+    x = _latent_mixture(1 << 15, d, 0xCA1, latent, centres, spectrum, model_key, cs)
+    return float(x.std())
+
+
+_SIFT = dict(latent=64, centres=1024, spectrum=0.35, model_key=1, cs=1.0)
+_sift_std = {}
+
+
 def sift_like(n: int, seed: int = 1, d: int = 128) -> np.ndarray:
-    x = _latent_mixture(n, d, seed, latent=32, centres=256, spectrum=0.6, model_key=1)
-    x = np.rint(x * 24.0 + 40.0)
+    """SIFT-shaped: ~10 % zeros, mean ~50, values quantised to integers in [0, 255].  At 1M points with M=16 /
+    efC=200 the reference's knn reaches recall@10 ~0.93 at ef=32 and ~0.98 at ef=128 with ~2,100 distance
+    computations per query at ef=128 (measured with the oracle), close to real SIFT1M's behaviour."""
+    if d not in _sift_std:
+        _sift_std[d] = _model_std(d, _SIFT["latent"], _SIFT["centres"], _SIFT["spectrum"], _SIFT["model_key"],
+                                  _SIFT["cs"])
+    x = _latent_mixture(n, d, seed, _SIFT["latent"], _SIFT["centres"], _SIFT["spectrum"], _SIFT["model_key"],
+                        _SIFT["cs"])
+    x = np.rint(x * np.float32(40.0 / _sift_std[d]) + np.float32(50.0))
     np.clip(x, 0.0, 255.0, out=x)
     return x.astype(np.float32)
 
