@@ -37,6 +37,11 @@ def log(msg):
 
 
 def host_threads():
+    """This process's CPU share: OMP_NUM_THREADS when the launcher sets it (the GPU box grants 16 CPUs per GPU
+    while sched_getaffinity lists the whole machine), else the affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
     try:
         return max(1, len(os.sched_getaffinity(0)))
     except Exception:
@@ -111,7 +116,8 @@ def main():
     ids = torch.empty((a.nbatches, a.batch, a.k), dtype=torch.int32, device="cuda")
     dists = torch.empty((a.nbatches, a.batch, a.k), dtype=torch.float32, device="cuda")
     qs = torch.zeros((a.nbatches, a.batch, 8), dtype=torch.int32, device="cuda")
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()  # a real stream: the C ABI reads a NULL stream as "the handle's own stream"
+    torch.cuda.set_stream(stream)
 
     def step(i, rec=None):
         b = i % a.nbatches
