@@ -70,7 +70,7 @@ struct Replica {
   uint32_t slots = 0;
   // staging for the host-pointer API
   DevBuf<float> q, d;
-  DevBuf<uint32_t> ids, qs, qmap;
+  DevBuf<uint32_t> ids, qs, ovf;
 };
 
 }  // namespace
@@ -175,7 +175,7 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
     if (int rc = upload(R.up_base, G.up_base.data(), G.up_base.size(), R.stream)) return rc;
     if (int rc = upload(R.adjU, G.adjU.data(), G.adjU.size(), R.stream)) return rc;
     if (int rc = upload(R.inv_uid, inv.data(), inv.size(), R.stream)) return rc;
-    if (int rc = R.counter.grow(1)) return rc;
+    if (int rc = R.counter.grow(8)) return rc;
     HIP_TRY(hipStreamSynchronize(R.stream));
   }
   h->device_bytes = vlen + 4 * (G.adj0.size() + G.uid.size() + G.up_base.size() + G.adjU.size() + inv.size());
@@ -183,27 +183,50 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
   return SHINE_OK;
 }
 
-// Candidate-queue capacity and slot count for a launch: enough resident wavefronts for the batch, the rest of
-// the CU's 160 KiB of LDS given to next_candidates.
+// Launch shapes.  Each query keeps top_candidates, next_candidates and its visited table in LDS; the batch is
+// spread so that enough wavefronts are resident (one per query up to 16 per CU) and the rest of the CU's
+// 160 KiB go to the queues.  A query that outgrows them is re-run alone per CU with the whole LDS (mode 1),
+// then with the visited set in HBM (mode 2); only then does it fail with SHINE_ERR_OVERFLOW.
 struct LaunchShape {
-  uint32_t cap, grid;
+  uint32_t cap, grid, vis_cap, vis_limit;
 };
-LaunchShape pick_shape(uint32_t nq, uint32_t ef, bool big) {
-  uint32_t waves_per_cu = std::max<uint32_t>(1, std::min<uint32_t>(16, (nq + kCus - 1) / kCus));
-  if (big) waves_per_cu = 1;
-  uint32_t lds = std::min<uint32_t>(kLdsPerCu / waves_per_cu, big ? kLdsPerCu : 64 * 1024);
-  lds &= ~15u;
-  int64_t cap = (static_cast<int64_t>(lds) - 8ll * ef - 512) / 8;
-  cap = std::max<int64_t>(cap, 64);
-  if (!big) {  // test hook: force a small first-pass queue so the overflow re-run path is exercised
-    if (const char* env = std::getenv("SHINE_DEBUG_CAP")) cap = std::max<int64_t>(1, std::atoll(env));
-  }
-  const uint32_t per_cu = std::max<uint32_t>(1, kLdsPerCu / static_cast<uint32_t>(search_lds_bytes(ef, static_cast<uint32_t>(cap))));
-  const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(nq, kCus * std::min<uint32_t>(per_cu, 16)));
-  return {static_cast<uint32_t>(cap), grid};
+
+uint32_t pow2_at_least(uint32_t x) {
+  uint32_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
 }
 
-int ensure_slots(shine_index* h, Replica& R, uint32_t slots) {
+int64_t env_int(const char* name, int64_t dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoll(e) : dflt;
+}
+
+LaunchShape pick_shape(uint32_t nq, uint32_t ef, int mode) {
+  LaunchShape sh{};
+  const uint64_t top_bytes = align16(8ull * ef);
+  uint32_t wpc = 1;
+  if (mode == 0) {
+    sh.vis_cap = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(48 * ef)));
+    sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
+    const uint64_t need = search_lds_bytes(ef, 4 * ef, sh.vis_cap);
+    const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(kLdsPerCu / need));
+    wpc = std::max<uint32_t>(1, std::min<uint32_t>({(nq + kCus - 1) / kCus, 16u, fit}));
+  } else if (mode == 1) {
+    sh.vis_cap = 16384;
+  } else {
+    sh.vis_cap = 0;  // visited bitmap in HBM
+  }
+  const uint64_t budget = (kLdsPerCu / wpc) & ~15u;
+  const int64_t cap = (static_cast<int64_t>(budget) - static_cast<int64_t>(top_bytes) - 4ll * sh.vis_cap - 512) / 8;
+  sh.cap = static_cast<uint32_t>(std::max<int64_t>(cap & ~1ll, 2));
+  if (mode == 0) sh.cap = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_DEBUG_CAP", sh.cap)));  // test hook
+  sh.vis_limit = sh.vis_cap / 8 * 7;  // linear probing stays short; >= 64 free slots for one expansion
+  sh.grid = std::max<uint32_t>(1, std::min<uint32_t>(nq, kCus * wpc));
+  return sh;
+}
+
+int ensure_bitmaps(shine_index* h, Replica& R, uint32_t slots) {
   if (slots <= R.slots) return 0;
   R.visited.release();
   R.vlog.release();
@@ -216,31 +239,48 @@ int ensure_slots(shine_index* h, Replica& R, uint32_t slots) {
   return 0;
 }
 
-int enqueue_search(shine_index* h, Replica& R, const float* d_q, const uint32_t* d_qmap, uint32_t nq, uint32_t k,
-                   uint32_t ef, uint32_t* d_ids, float* d_dists, uint32_t* d_qs, hipStream_t s, bool big,
-                   bool timed) {
-  const LaunchShape sh = pick_shape(nq, ef, big);
-  if (int rc = ensure_slots(h, R, sh.grid)) return rc;
-  SearchArgs a{};
-  a.g = dev_graph(h, R);
-  a.queries = d_q;
-  a.qmap = d_qmap;
-  a.nq = nq;
-  a.k = k;
-  a.ef = ef;
-  a.cap = sh.cap;
-  a.out_ids = d_ids;
-  a.out_dists = d_dists;
-  a.qstats = d_qs;
-  a.visited = R.visited.p;
-  a.words_per_slot = h->words_per_slot;
-  a.vlog = R.vlog.p;
-  a.log_cap = kLogCap;
-  a.counter = R.counter.p;
-  HIP_TRY(hipMemsetAsync(R.counter.p, 0, sizeof(uint32_t), s));
+// Enqueue the three search passes on stream s: pass 0 over the whole batch; passes 1 and 2 (more LDS per
+// wavefront, then the visited set in HBM) over the compact lists of queries the previous pass could not hold.
+// Everything stays on the device, so the call is asynchronous and still exact.
+int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, uint32_t k, uint32_t ef,
+                   uint32_t* d_ids, float* d_dists, uint32_t* d_qs, hipStream_t s, bool timed) {
+  if (int rc = R.ovf.grow(2ull * nq)) return rc;
+  HIP_TRY(hipMemsetAsync(R.counter.p, 0, 8 * sizeof(uint32_t), s));  // 3 queue heads + 2 list counts
   if (timed) HIP_TRY(hipEventRecord(R.ev0, s));
-  hipError_t e = launch_search(h->dim, h->metric, h->elem, sh.grid, a, s);
-  if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("search launch: ") + hipGetErrorString(e));
+  const int start = static_cast<int>(env_int("SHINE_DEBUG_START_MODE", 0));  // test hook: exercise modes 1, 2
+  for (int mode = start; mode <= 2; ++mode) {
+    const LaunchShape sh = pick_shape(nq, ef, mode);
+    if (mode == 2) {
+      if (int rc = ensure_bitmaps(h, R, sh.grid)) return rc;
+    }
+    SearchArgs a{};
+    a.g = dev_graph(h, R);
+    a.queries = d_q;
+    a.nq = nq;
+    a.k = k;
+    a.ef = ef;
+    a.cap = sh.cap;
+    a.vis_cap = sh.vis_cap;
+    a.vis_limit = sh.vis_limit;
+    a.out_ids = d_ids;
+    a.out_dists = d_dists;
+    a.qstats = d_qs;
+    a.visited = R.visited.p;
+    a.words_per_slot = h->words_per_slot;
+    a.vlog = R.vlog.p;
+    a.log_cap = kLogCap;
+    a.counter = R.counter.p + mode;
+    if (mode > start) {
+      a.in_list = R.ovf.p + static_cast<size_t>(mode - 1) * nq;
+      a.in_count = R.counter.p + 3 + (mode - 1);
+    }
+    if (mode < 2) {
+      a.out_list = R.ovf.p + static_cast<size_t>(mode) * nq;
+      a.out_count = R.counter.p + 3 + mode;
+    }
+    hipError_t e = launch_search(h->dim, h->metric, h->elem, sh.grid, a, s);
+    if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("search launch: ") + hipGetErrorString(e));
+  }
   if (timed) HIP_TRY(hipEventRecord(R.ev1, s));
   return 0;
 }
@@ -329,7 +369,12 @@ int shine_knn_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_qu
   Replica& R = h->reps[gpu_slot];
   HIP_TRY(hipSetDevice(R.device));
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : R.stream;
-  return enqueue_search(h, R, d_queries, nullptr, nq, k, ef, d_out_ids, d_out_dists, d_qstats, s, false, false);
+  uint32_t* qs = d_qstats;
+  if (!qs) {
+    if (int rc = R.qs.grow(static_cast<size_t>(nq) * SHINE_QS_WORDS)) return rc;
+    qs = R.qs.p;
+  }
+  return enqueue_search(h, R, d_queries, nq, k, ef, d_out_ids, d_out_dists, qs, s, false);
 }
 
 int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t k, uint32_t ef, uint32_t* out_ids,
@@ -359,8 +404,7 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
     if (int rc = R.ids.grow(static_cast<size_t>(n) * k)) return rc;
     if (int rc = R.d.grow(static_cast<size_t>(n) * k)) return rc;
     if (int rc = R.qs.grow(static_cast<size_t>(n) * SHINE_QS_WORDS)) return rc;
-    if (int rc = enqueue_search(h, R, R.q.p, nullptr, n, k, ef, R.ids.p, R.d.p, R.qs.p, R.stream, false, true))
-      return rc;
+    if (int rc = enqueue_search(h, R, R.q.p, n, k, ef, R.ids.p, R.d.p, R.qs.p, R.stream, true)) return rc;
   }
   double kernel_ms = 0;
   uint64_t retries = 0;
@@ -375,21 +419,9 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, R.ev0, R.ev1));
     kernel_ms = std::max(kernel_ms, static_cast<double>(ms));
-    // queries whose next_candidates outgrew the LDS queue: re-run them alone with the whole CU's LDS
-    std::vector<uint32_t> redo;
-    for (uint32_t j = 0; j < n; ++j)
-      if (sbuf[r][j * SHINE_QS_WORDS + SHINE_QS_STATUS] == SHINE_ERR_OVERFLOW) redo.push_back(j);
-    if (!redo.empty()) {
-      retries += redo.size();
-      if (int rc = upload(R.qmap, redo.data(), redo.size(), R.stream)) return rc;
-      if (int rc = enqueue_search(h, R, R.q.p, R.qmap.p, static_cast<uint32_t>(redo.size()), k, ef, R.ids.p, R.d.p,
-                                  R.qs.p, R.stream, true, true))
-        return rc;
-      HIP_TRY(hipMemcpyAsync(sbuf[r].data(), R.qs.p, sbuf[r].size() * 4, hipMemcpyDeviceToHost, R.stream));
-      HIP_TRY(hipStreamSynchronize(R.stream));
-      HIP_TRY(hipEventElapsedTime(&ms, R.ev0, R.ev1));
-      kernel_ms += ms;
-    }
+    uint32_t ovf_counts[2] = {0, 0};  // queries handed to the fixup passes
+    HIP_TRY(hipMemcpy(ovf_counts, R.counter.p + 3, sizeof(ovf_counts), hipMemcpyDeviceToHost));
+    retries += ovf_counts[0] + ovf_counts[1];
     ibuf[r].resize(static_cast<size_t>(n) * k);
     dbuf[r].resize(static_cast<size_t>(n) * k);
     HIP_TRY(hipMemcpyAsync(ibuf[r].data(), R.ids.p, ibuf[r].size() * 4, hipMemcpyDeviceToHost, R.stream));
@@ -446,13 +478,40 @@ int shine_distance_batch_device(shine_index_t h, uint32_t gpu_slot, const float*
   return SHINE_OK;
 }
 
+int shine_selftest_heap(int is_max, const int32_t* ops, const float* vals, const uint32_t* ids, uint32_t n_ops,
+                        uint32_t k, float* out_d, uint32_t* out_ids, uint32_t* out_n) {
+  if (!ops || !vals || !ids || !out_d || !out_ids || !out_n) return set_error(SHINE_ERR_ARG, "NULL argument");
+  if (n_ops == 0 || n_ops > 16384) return set_error(SHINE_ERR_ARG, "n_ops must be in [1, 16384]");
+  HIP_TRY(hipSetDevice(0));
+  DevBuf<int32_t> dops;
+  DevBuf<float> dvals, dd;
+  DevBuf<uint32_t> dids, di, dn;
+  auto cleanup = [&]() { dops.release(); dvals.release(); dd.release(); dids.release(); di.release(); dn.release(); };
+  int rc = 0;
+  if ((rc = dops.grow(n_ops)) || (rc = dvals.grow(n_ops)) || (rc = dids.grow(n_ops)) || (rc = dd.grow(n_ops + 1)) ||
+      (rc = di.grow(n_ops + 1)) || (rc = dn.grow(1))) {
+    cleanup();
+    return rc;
+  }
+  hipError_t e = hipMemcpy(dops.p, ops, 4ull * n_ops, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dvals.p, vals, 4ull * n_ops, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dids.p, ids, 4ull * n_ops, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = launch_heap_replay(is_max, dops.p, dvals.p, dids.p, n_ops, k, dd.p, di.p, dn.p, nullptr);
+  if (e == hipSuccess) e = hipMemcpy(out_n, dn.p, 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && *out_n) e = hipMemcpy(out_d, dd.p, 4ull * *out_n, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && *out_n) e = hipMemcpy(out_ids, di.p, 4ull * *out_n, hipMemcpyDeviceToHost);
+  cleanup();
+  if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("heap replay: ") + hipGetErrorString(e));
+  return SHINE_OK;
+}
+
 int shine_close(shine_index_t h) {
   if (!h) return SHINE_OK;
   for (auto& R : h->reps) {
     (void)hipSetDevice(R.device);
     if (R.stream) (void)hipStreamSynchronize(R.stream);
     for (auto* b : {&R.adj0, &R.uid, &R.up_base, &R.adjU, &R.inv_uid, &R.visited, &R.vlog, &R.counter, &R.ids, &R.qs,
-                    &R.qmap})
+                    &R.ovf})
       b->release();
     R.vec.release();
     R.q.release();

@@ -21,9 +21,10 @@ struct DevGraph {
 struct SearchArgs {
   DevGraph g;
   const float* queries;   // [nq_total][dim]
-  const uint32_t* qmap;   // work item → query index (nullptr: identity)
   uint32_t nq;            // work items
   uint32_t k, ef, cap;    // cap: next_candidates capacity held in LDS
+  uint32_t vis_cap;       // LDS visited hash-table entries (power of two; 0 = global bitmap variant)
+  uint32_t vis_limit;     // entries allowed in the LDS table before the query is re-run with more LDS
   uint32_t* out_ids;      // [nq_total][k]
   float* out_dists;       // [nq_total][k] (nullable)
   uint32_t* qstats;       // [nq_total][8] (nullable)
@@ -32,6 +33,10 @@ struct SearchArgs {
   uint32_t* vlog;         // [slots][log_cap] ids whose visited bit is set (for clearing)
   uint32_t log_cap;
   uint32_t* counter;      // work queue head (zeroed before every launch)
+  const uint32_t* in_list;   // fixup passes: work items are in_list[0 .. *in_count)
+  const uint32_t* in_count;
+  uint32_t* out_list;        // queries that overflow here are appended for the next pass (nullable)
+  uint32_t* out_count;
 };
 
 struct DistArgs {
@@ -43,13 +48,20 @@ struct DistArgs {
   float* out;                 // [nq][n_per]
 };
 
-// LDS bytes a search workgroup needs for (ef, cap).
-inline size_t search_lds_bytes(uint32_t ef, uint32_t cap) { return 8ull * (ef + cap) + 64 * 4 * 2; }
+// LDS layout of a search workgroup: top[ef] | next[cap] | visited table[vis_cap] | scratch ids[64], dists[64]
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+inline size_t search_lds_bytes(uint32_t ef, uint32_t cap, uint32_t vis_cap) {
+  return align16(8ull * ef) + align16(8ull * cap) + 4ull * vis_cap + 64 * 4 * 2;
+}
 
 bool dim_supported(uint32_t dim, int elem);
 
 // Returns hipSuccess or the launch error.  grid = number of persistent search slots (one wavefront each).
 hipError_t launch_search(uint32_t dim, int metric, int elem, uint32_t grid, const SearchArgs& a, hipStream_t s);
 hipError_t launch_distance(uint32_t dim, int metric, int elem, const DistArgs& a, hipStream_t s);
+
+// Diagnostics: replay push / pop / push_k sequences through the device heap routines (one wavefront).
+hipError_t launch_heap_replay(int is_max, const int32_t* ops, const float* vals, const uint32_t* ids, uint32_t n_ops,
+                              uint32_t k, float* out_d, uint32_t* out_ids, uint32_t* out_n, hipStream_t s);
 
 }  // namespace shine

@@ -4,21 +4,31 @@
 //                   level-0 best-first beam search search_level (:406-476), one query per wavefront,
 //                   persistent workgroups pulling queries from a device work queue.
 //   distance_kernel Distance::dist (src/hnsw/distance.hh:153-161) over gathered (query, node) pairs.
+//   heap_replay     diagnostics: the device heap routines driven by an op list (tests pin them to libstdc++).
 //
-// Exactness.  Both kernels evaluate L2 / IP in exactly the oracle's floating-point order (oracle/oracle.cc):
-// eight lanes of a wavefront play the eight AVX2 accumulators of L2SqrSIMD16ExtAVX / InnerProductSIMD16ExtAVX
+// Exactness.  Distances are evaluated in exactly the oracle's floating-point order (oracle/oracle.cc): eight
+// lanes of a wavefront play the eight AVX2 accumulators of L2SqrSIMD16ExtAVX / InnerProductSIMD16ExtAVX
 // (distance.hh:11-76) — lane a owns elements i ≡ a (mod 8) of the 16-aligned prefix and runs the same fmaf
 // chain — the eight partial sums are added left to right, then the scalar tail.  The two candidate queues are
-// the reference's std::vector heaps (heap.hh) held in LDS and updated by lane 0 with the exact libstdc++
-// push_heap / pop_heap algorithms (bits/stl_heap.h: __push_heap, __adjust_heap, __pop_heap), so ties between
-// equal distances are broken exactly as on the CPU and the returned ids come out in the same heap-array
-// order (hnsw.hh:300-303).
+// the reference's std::vector heaps (heap.hh) kept in LDS and updated with exactly the libstdc++ algorithms
+// (bits/stl_heap.h: __push_heap, __adjust_heap, __pop_heap), so ties between equal distances are broken as on
+// the CPU and results come out in the same heap-array order (hnsw.hh:300-303).
 //
-// Per expansion the wavefront: pops the closest candidate (lane 0), loads the 2M-entry adjacency row with
-// one coalesced 128-/256-byte load (one u32 per lane), test-and-sets the visited bitmap with one atomicOr per
-// lane (ballot + mbcnt give the fresh neighbours in list order), gathers the fresh neighbours' vectors
-// (8 vectors per wave-instruction, 8 lanes × 32 B each), reduces, and lane 0 replays the reference's
-// accept / push / push_k sequence over them in list order.
+// Wave-parallel heap operations (one query = one wavefront, all 64 lanes cooperate on each operation):
+//   push   the ancestors of the new slot are loaded in one LDS round, each lane compares its ancestor with the
+//          new key, and the length of the run of moves (a ballot + ctz) fixes the final slot; the moved
+//          ancestors are stored in one more round.  (std::__push_heap walks the same chain one level at a time.)
+//   pop    std::__adjust_heap's hole walks from the root to a leaf always taking the child the comparator
+//          prefers, independently of the value being re-inserted.  The walk is resolved five levels per LDS
+//          round: 62 lanes load the 5-level subtree under the hole, 31 lanes compare sibling pairs, and the
+//          ballot of "right child wins" bits is walked with scalar bit tests.  The final std::__push_heap of the
+//          last element climbs back up that same path, so its stopping point is one more ballot, and all moves
+//          are written in one round.
+// Expansion step (search_level): pop the closest candidate; its 2M-entry adjacency row is one coalesced
+// 128-/256-byte load (one u32 per lane), issued speculatively during the previous step's accept phase for the
+// predicted next candidate; the visited test-and-set is an exact open-addressing hash table in LDS (CAS per
+// lane); fresh neighbours' vectors are gathered 8 per wave-instruction group and reduced; the accept / push /
+// push_k sequence (:456-465) is replayed in list order with the parallel heap operations.
 #include "kernels.h"
 
 #include <hip/hip_fp16.h>
@@ -49,7 +59,7 @@ __device__ __forceinline__ float to_f32(float x) { return x; }
 __device__ __forceinline__ float to_f32(__half x) { return __half2float(x); }
 
 // ------------------------------------------------------------------------------------------------------------
-// libstdc++ heap algorithms on an LDS array of packed {dist, id} entries (executed by lane 0 only).
+// Heaps of packed {dist, id} entries in LDS.
 //   MAXH = true : heap::MaxHeapCompare (lhs.distance < rhs.distance), heap.hh:15-17
 //   MAXH = false: heap::MinHeapCompare (lhs.distance > rhs.distance), heap.hh:19-21
 // ------------------------------------------------------------------------------------------------------------
@@ -58,48 +68,78 @@ __device__ __forceinline__ bool hcmp(float a, float b) {
   return MAXH ? (a < b) : (a > b);
 }
 
-// std::push_heap(first, first + n + 1) with h[n] = v   (std::__push_heap(first, n, 0, v))
+// push_back(v) + std::push_heap on h[0..n]  ≡  std::__push_heap(h, n, 0, v)
 template <bool MAXH>
-__device__ __forceinline__ void heap_push(u64* h, int n, u64 v) {
+__device__ __forceinline__ void heap_push(u64* h, int n, u64 v, int lane) {
   const float vd = key(v);
-  int hole = n;
-  while (hole > 0) {
-    const int parent = (hole - 1) >> 1;
-    const u64 pe = h[parent];
-    if (!hcmp<MAXH>(key(pe), vd)) break;
-    h[hole] = pe;
-    hole = parent;
+  const int L = 31 - __clz(n + 1);  // ancestors of slot n
+  u64 ent = 0;
+  bool c = false;
+  if (lane < L) {  // lane t holds ancestor t+1
+    ent = h[((n + 1) >> (lane + 1)) - 1];
+    c = hcmp<MAXH>(key(ent), vd);  // parent moves down while comp(parent, value)
   }
-  h[hole] = v;
+  const u64 C = __ballot(c);
+  const int s = static_cast<int>(__builtin_ctzll(~C));  // moves happen for the first s ancestors
+  if (lane < s) h[lane == 0 ? n : ((n + 1) >> lane) - 1] = ent;
+  const int fin = s == 0 ? n : ((n + 1) >> s) - 1;
+  if (lane == 0) h[fin] = v;
+  wave_sync();
 }
 
-// std::pop_heap(first, first + n) followed by pop_back  (std::__pop_heap → std::__adjust_heap(first, 0, n-1, v))
+// std::pop_heap on h[0..n) followed by pop_back  ≡  std::__adjust_heap(h, 0, n-1, h[n-1])
 template <bool MAXH>
-__device__ __forceinline__ void heap_pop(u64* h, int n) {
+__device__ __forceinline__ void heap_pop(u64* h, int n, int lane) {
   if (n <= 1) return;
   const int len = n - 1;
   const u64 value = h[len];
-  int hole = 0, second = 0;
-  while (second < (len - 1) / 2) {
-    second = 2 * (second + 1);
-    if (hcmp<MAXH>(key(h[second]), key(h[second - 1]))) second--;
-    h[hole] = h[second];
-    hole = second;
+  const float vk = key(value);
+  const int lim = (len - 1) / 2;  // the hole has two children while hole < lim
+  // lane m holds node m+2 (1-based) of a 5-level subtree: levels 1..5 below its root
+  const int rel = lane + 2;
+  const int rl = 31 - __clz(rel);
+  const int ro = rel - (1 << rl);
+  int pos = 0, L = 0, my_child = 0;  // lane t: the path's (t+1)-th node
+  while (pos < lim) {
+    const int absn = ((pos + 1) << rl) - 1 + ro;
+    float kk = 0.f;
+    if (lane < 62 && absn < len) kk = key(h[absn]);
+    const float lk = __shfl(kk, 2 * lane);      // left child of subtree node lane+1
+    const float rk = __shfl(kk, 2 * lane + 1);  // right child
+    const bool right = !hcmp<MAXH>(rk, lk);     // libstdc++ takes the left child iff comp(right, left)
+    const u64 W = __ballot(lane < 31 && right);
+    int r1 = 1;
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+      if (pos >= lim) break;
+      const int b = static_cast<int>((W >> (r1 - 1)) & 1ull);
+      const int child = 2 * pos + 1 + b;
+      if (lane == L) my_child = child;
+      ++L;
+      pos = child;
+      r1 = 2 * r1 + b;
+    }
   }
-  if ((len & 1) == 0 && second == (len - 2) / 2) {
-    second = 2 * (second + 1);
-    h[hole] = h[second - 1];
-    hole = second - 1;
+  if ((len & 1) == 0 && pos == (len - 2) / 2) {  // lone left child
+    const int child = 2 * pos + 1;
+    if (lane == L) my_child = child;
+    ++L;
+    pos = child;
   }
-  const float vd = key(value);
-  while (hole > 0) {
-    const int parent = (hole - 1) >> 1;
-    const u64 pe = h[parent];
-    if (!hcmp<MAXH>(key(pe), vd)) break;
-    h[hole] = pe;
-    hole = parent;
+  // std::__push_heap(h, hole = path end, 0, value) climbs the same path
+  u64 ent = 0;
+  bool c = false;
+  if (lane < L) {
+    ent = h[my_child];
+    c = hcmp<MAXH>(key(ent), vk);
   }
-  h[hole] = value;
+  const u64 C = __ballot(c);
+  const u64 stay = ~C & (L >= 64 ? ~0ull : ((1ull << L) - 1));
+  const int j = stay ? 64 - __clzll(stay) : 0;  // value lands on the path's j-th node
+  const int pj = j == 0 ? 0 : __shfl(my_child, j - 1);
+  if (lane < j) h[(my_child - 1) >> 1] = ent;  // path nodes above the landing slot shift up
+  if (lane == 0) h[pj] = value;
+  wave_sync();
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -189,34 +229,46 @@ __device__ __forceinline__ void dist_list(const E* __restrict__ vec, const Query
   }
 }
 
+// Exact visited set (hashset_t<RemotePtr>, types.hh:14-15) on dense node ids.
+//   VIS = 0: open-addressing table of u32 keys in LDS, linear probing, LDS compare-and-swap per lane.
+//   VIS = 1: per-slot bitmap in HBM (atomicOr test-and-set) + a log of set ids for clearing (large-LDS fallback).
+__device__ __forceinline__ u32 vhash(u32 key, u32 shift) { return (key * 0x9E3779B1u) >> shift; }
+
 // ------------------------------------------------------------------------------------------------------------
 // search kernel: one wavefront (= one workgroup) per persistent slot
 // ------------------------------------------------------------------------------------------------------------
-template <int D, int METRIC, typename E>
+template <int D, int METRIC, typename E, int VIS>
 __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  u64* top = reinterpret_cast<u64*>(smem);      // MaxHeap top_candidates, capacity ef
-  u64* nxt = top + A.ef;                         // MinHeap next_candidates, capacity cap
-  u32* sc_ids = reinterpret_cast<u32*>(nxt + A.cap);  // fresh neighbours of the current expansion
+  const int ef = static_cast<int>(A.ef), cap = static_cast<int>(A.cap);
+  u64* top = reinterpret_cast<u64*>(smem);                                    // MaxHeap top_candidates
+  u64* nxt = reinterpret_cast<u64*>(smem + align16(8ull * ef));               // MinHeap next_candidates
+  u32* vtab = reinterpret_cast<u32*>(smem + align16(8ull * ef) + align16(8ull * cap));
+  u32* sc_ids = vtab + (VIS == 0 ? A.vis_cap : 0u);                           // fresh neighbours
   float* sc_d = reinterpret_cast<float*>(sc_ids + 64);
 
   const int lane = threadIdx.x;
   const E* __restrict__ vec = static_cast<const E*>(A.g.vec);
   const u32 M0 = A.g.M0, MU = A.g.MU;
-  const int ef = static_cast<int>(A.ef), cap = static_cast<int>(A.cap);
-  u32* __restrict__ vis = A.visited + static_cast<u64>(blockIdx.x) * A.words_per_slot;
-  u32* __restrict__ vlog = A.vlog + static_cast<u64>(blockIdx.x) * A.log_cap;
+  const u32 vmask = A.vis_cap - 1, vshift = 32 - (31 - __clz(static_cast<int>(A.vis_cap > 1 ? A.vis_cap : 2)));
+  u32* __restrict__ vis = A.visited + (VIS == 1 ? static_cast<u64>(blockIdx.x) * A.words_per_slot : 0ull);
+  u32* __restrict__ vlog = A.vlog + (VIS == 1 ? static_cast<u64>(blockIdx.x) * A.log_cap : 0ull);
   const u64 below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));  // lanes < this one
 
+  const u32 n_items = A.in_count ? *A.in_count : A.nq;
   for (;;) {
     u32 item = 0;
     if (lane == 0) item = atomicAdd(A.counter, 1u);
     item = bcast(item);
-    if (item >= A.nq) break;
-    const u32 qi = A.qmap ? A.qmap[item] : item;
+    if (item >= n_items) break;
+    const u32 qi = A.in_list ? A.in_list[item] : item;
 
     QueryRegs<D> Q;
     load_query<D>(A.queries + static_cast<u64>(qi) * D, lane, Q);
+    if (VIS == 0) {  // visited_nodes.clear()  (:475) — done up front for this query
+      uint4* t4 = reinterpret_cast<uint4*>(vtab);
+      for (u32 i = lane; i < A.vis_cap / 4; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
+    }
 
     u32 st_dist = 0, st_vup = 0, st_vl0 = 0, st_lup = 0, st_ll0 = 0, st_maxnext = 0, status = 0;
 
@@ -274,39 +326,44 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
     // ---- top_candidates.push({nn, dist(q, nn)}) (hnsw.hh:285-286) ---------------------------------------
     ++st_dist;
     int ntop = 1, nnext = 1;
-    u32 logpos = 0;
+    u32 logpos = 0, nvis = 1;
     bool log_overflow = false;
     if (status == 0) {
       const u64 e0 = mk(closest, nn);
       if (lane == 0) {
         top[0] = e0;
         nxt[0] = e0;  // search_level :412-415
-        const u32 old = atomicOr(&vis[nn >> 5], 1u << (nn & 31));
-        (void)old;
-        vlog[0] = nn;
+        if (VIS == 0) {
+          u32 h = vhash(nn, vshift);
+          vtab[h] = nn;  // table is empty: first probe slot is free
+        } else {
+          atomicOr(&vis[nn >> 5], 1u << (nn & 31));
+          vlog[0] = nn;
+        }
       }
       logpos = 1;
       st_maxnext = 1;
+      wave_sync();
+
+      u32 pre_id = INV;  // candidate whose adjacency row is in flight in pre_e
+      u32 pre_e = INV;
 
       // ---- search_level(q, ef, 0) (hnsw.hh:406-476) ---------------------------------------------------------
       while (nnext > 0) {
-        u64 c = 0;
-        int brk = 0;
-        if (lane == 0) {
-          c = nxt[0];  // next_candidates.top(); pop()  (:418-419)
-          heap_pop<false>(nxt, nnext);
-          brk = key(c) > key(top[0]);  // :421-426
-        }
-        c = bcast64(c);
-        brk = static_cast<int>(bcast(static_cast<u32>(brk)));
+        const u64 c = bcast64(nxt[0]);  // next_candidates.top(); pop()  (:418-419)
+        const float farthest0 = key(top[0]);
+        heap_pop<false>(nxt, nnext, lane);
         --nnext;
-        if (brk) break;
+        if (key(c) > farthest0) break;  // :421-426
 
         // neighbour list of the candidate at level 0 (:436-438)
         ++st_ll0;
-        const u32* row = A.g.adj0 + static_cast<u64>(eid(c)) * M0;
         u32 e = INV;
-        if (static_cast<u32>(lane) < M0) e = row[lane];
+        if (eid(c) == pre_id) {
+          e = pre_e;
+        } else if (static_cast<u32>(lane) < M0) {
+          e = A.g.adj0[static_cast<u64>(eid(c)) * M0 + lane];
+        }
         bool cand = e != INV;
         if (!A.g.lists_unique) {  // first occurrence in list order wins (visited.insert order, :443)
           for (u32 j = 0; j < M0; ++j) {
@@ -315,65 +372,96 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
           }
         }
         bool fresh = false;
-        if (cand) {  // visited.contains / insert (:441-443): one atomic test-and-set per lane
-          const u32 bit = 1u << (e & 31);
-          fresh = (atomicOr(&vis[e >> 5], bit) & bit) == 0;
+        if (cand) {  // visited.contains / insert (:441-443)
+          if (VIS == 0) {
+            u32 h = vhash(e, vshift);
+            for (;;) {
+              const u32 old = atomicCAS(&vtab[h], INV, e);
+              if (old == INV) { fresh = true; break; }
+              if (old == e) break;
+              h = (h + 1) & vmask;
+            }
+          } else {
+            const u32 bit = 1u << (e & 31);
+            fresh = (atomicOr(&vis[e >> 5], bit) & bit) == 0;
+          }
         }
         const u64 fm = __ballot(fresh);
         const int nf = __popcll(fm);
         if (fresh) {
           const int r = __popcll(fm & below);
           sc_ids[r] = e;
-          const u32 lp = logpos + r;
-          if (lp < A.log_cap) vlog[lp] = e;
+          if (VIS == 1) {
+            const u32 lp = logpos + r;
+            if (lp < A.log_cap) vlog[lp] = e;
+          }
         }
         logpos += nf;
-        if (logpos > A.log_cap) log_overflow = true;
+        nvis += nf;
+        if (VIS == 1 && logpos > A.log_cap) log_overflow = true;
         st_vl0 += nf;
         st_dist += nf;
+        if (VIS == 0 && nvis > A.vis_limit) { status = ST_OVERFLOW; break; }
         if (nf == 0) continue;
         wave_sync();
         dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, nf, lane);
         wave_sync();
 
+        // Speculative prefetch of the adjacency row of the candidate expected on top of next_candidates once
+        // this step's pushes are done: a min-heap root changes only for a strictly smaller key, so the root
+        // survives ties and, among the fresh keys, the first minimum in list order wins.
+        {
+          float pd = __builtin_inff();
+          u32 pidx = 64;
+          if (lane < nf) {
+            const float d = sc_d[lane];
+            if (d < farthest0 || ntop < ef) { pd = d; pidx = lane; }
+          }
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) {
+            const float od = __shfl_xor(pd, off);
+            const u32 oi = __shfl_xor(pidx, off);
+            if (od < pd || (od == pd && oi < pidx)) { pd = od; pidx = oi; }
+          }
+          pd = bcastf(pd);
+          pidx = bcast(pidx);
+          u32 pid = INV;
+          if (nnext > 0 && !(pd < key(nxt[0]))) pid = eid(nxt[0]);
+          else if (pidx < 64) pid = sc_ids[pidx];
+          pid = bcast(pid);
+          pre_id = pid;
+          if (pid != INV && static_cast<u32>(lane) < M0) pre_e = A.g.adj0[static_cast<u64>(pid) * M0 + lane];
+        }
+
         // accept / push / push_k in list order (:456-465)
-        int ovf = 0;
-        if (lane == 0) {
-          for (int j = 0; j < nf; ++j) {
-            const float d = sc_d[j];
-            const float farthest = key(top[0]);
-            if (d < farthest || ntop < ef) {
-              if (nnext >= cap) { ovf = 1; break; }
-              const u64 en = mk(d, sc_ids[j]);
-              heap_push<false>(nxt, nnext, en);
-              ++nnext;
-              if (ntop < ef) {  // heap.hh:34-41 push_k
-                heap_push<true>(top, ntop, en);
-                ++ntop;
-              } else if (d < key(top[0])) {
-                heap_pop<true>(top, ntop);
-                heap_push<true>(top, ntop - 1, en);
-              }
-              if (static_cast<u32>(nnext) > st_maxnext) st_maxnext = nnext;
+        for (int j = 0; j < nf; ++j) {
+          const float d = sc_d[j];
+          const float farthest = key(top[0]);
+          if (d < farthest || ntop < ef) {
+            if (nnext >= cap) { status = ST_OVERFLOW; break; }
+            const u64 en = mk(d, sc_ids[j]);
+            heap_push<false>(nxt, nnext, en, lane);
+            ++nnext;
+            if (ntop < ef) {  // heap.hh:34-41 push_k
+              heap_push<true>(top, ntop, en, lane);
+              ++ntop;
+            } else {  // d < top().distance holds: it is the accept test with the top full
+              heap_pop<true>(top, ntop, lane);
+              heap_push<true>(top, ntop - 1, en, lane);
             }
+            if (static_cast<u32>(nnext) > st_maxnext) st_maxnext = nnext;
           }
         }
-        ntop = static_cast<int>(bcast(static_cast<u32>(ntop)));
-        nnext = static_cast<int>(bcast(static_cast<u32>(nnext)));
-        st_maxnext = bcast(st_maxnext);
-        if (bcast(static_cast<u32>(ovf))) { status = ST_OVERFLOW; break; }
-        wave_sync();
+        if (status != 0) break;
       }
 
       // ---- trim to k and emit in heap-array order (:296-303) ------------------------------------------------
-      if (status == 0 && lane == 0) {
+      if (status == 0) {
         while (ntop > static_cast<int>(A.k)) {
-          heap_pop<true>(top, ntop);
+          heap_pop<true>(top, ntop, lane);
           --ntop;
         }
       }
-      ntop = static_cast<int>(bcast(static_cast<u32>(ntop)));
-      wave_sync();
     }
 
     const u64 obase = static_cast<u64>(qi) * A.k;
@@ -388,6 +476,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
       A.out_ids[obase + i] = id;
       if (A.out_dists) A.out_dists[obase + i] = d;
     }
+    if (status == ST_OVERFLOW && A.out_list && lane == 0) A.out_list[atomicAdd(A.out_count, 1u)] = qi;
     if (A.qstats && lane == 0) {
       u32* qs = A.qstats + static_cast<u64>(qi) * 8;
       qs[0] = st_dist;
@@ -400,17 +489,18 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
       qs[7] = status == 0 ? static_cast<u32>(ntop < static_cast<int>(A.k) ? ntop : A.k) : 0u;
     }
 
-    // ---- visited_nodes.clear() (:475): clear exactly the words this query touched -------------------------
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!log_overflow) {
-      for (u32 i = lane; i < logpos; i += 64) {
-        const u32 id = __hip_atomic_load(&vlog[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        vis[id >> 5] = 0u;
+    if (VIS == 1) {  // visited_nodes.clear() (:475): clear exactly the words this query touched
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!log_overflow) {
+        for (u32 i = lane; i < logpos; i += 64) {
+          const u32 id = __hip_atomic_load(&vlog[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          vis[id >> 5] = 0u;
+        }
+      } else {
+        for (u64 w = lane; w < A.words_per_slot; w += 64) vis[w] = 0u;
       }
-    } else {
-      for (u64 w = lane; w < A.words_per_slot; w += 64) vis[w] = 0u;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 }
 
@@ -446,16 +536,59 @@ __global__ __launch_bounds__(64) void distance_kernel(DistArgs A) {
   if (j < A.n_per) A.out[static_cast<u64>(qi) * A.n_per + j] = ok ? sc_d[r] : __builtin_nanf("");
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// heap replay (diagnostics): op 0 = push, 1 = pop, 2 = push_k(k)
+// ------------------------------------------------------------------------------------------------------------
+template <bool MAXH>
+__global__ __launch_bounds__(64) void heap_replay_kernel(const int32_t* ops, const float* vals, const uint32_t* ids,
+                                                         uint32_t n_ops, uint32_t k, float* out_d, uint32_t* out_ids,
+                                                         uint32_t* out_n) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  u64* h = reinterpret_cast<u64*>(smem);
+  const int lane = threadIdx.x;
+  int n = 0;
+  for (u32 i = 0; i < n_ops; ++i) {
+    const u64 e = mk(vals[i], ids[i]);
+    const int op = ops[i];
+    if (op == 0) {
+      heap_push<MAXH>(h, n, e, lane);
+      ++n;
+    } else if (op == 1) {
+      if (n > 0) {
+        heap_pop<MAXH>(h, n, lane);
+        --n;
+      }
+    } else {
+      if (n < static_cast<int>(k)) {
+        heap_push<MAXH>(h, n, e, lane);
+        ++n;
+      } else if (hcmp<MAXH>(vals[i], key(h[0]))) {
+        heap_pop<MAXH>(h, n, lane);
+        heap_push<MAXH>(h, n - 1, e, lane);
+      }
+    }
+  }
+  for (int i = lane; i < n; i += 64) {
+    out_d[i] = key(h[i]);
+    out_ids[i] = eid(h[i]);
+  }
+  if (lane == 0) *out_n = static_cast<u32>(n);
+}
+
 template <int D, int METRIC, typename E>
 hipError_t launch_search_t(uint32_t grid, const SearchArgs& a, hipStream_t s) {
-  const size_t lds = search_lds_bytes(a.ef, a.cap);
-  if (lds > 65536) {  // beyond the default dynamic-LDS limit: opt in (per device, so every launch)
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&search_kernel<D, METRIC, E>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL((search_kernel<D, METRIC, E>), dim3(grid), dim3(64), lds, s, a);
-  return hipGetLastError();
+  const size_t lds = search_lds_bytes(a.ef, a.cap, a.vis_cap);
+  auto run = [&](auto kern) -> hipError_t {
+    if (lds > 65536) {  // beyond the default dynamic-LDS limit: opt in (per device, so every launch)
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, s, a);
+    return hipGetLastError();
+  };
+  if (a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0>);
+  return run(search_kernel<D, METRIC, E, 1>);
 }
 
 template <int D, int METRIC, typename E>
@@ -526,6 +659,25 @@ hipError_t launch_distance(uint32_t dim, int metric, int elem, const DistArgs& a
   }
 #undef SHINE_CASE16
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_heap_replay(int is_max, const int32_t* ops, const float* vals, const uint32_t* ids, uint32_t n_ops,
+                              uint32_t k, float* out_d, uint32_t* out_ids, uint32_t* out_n, hipStream_t s) {
+  const size_t lds = 8ull * (n_ops + 1);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const void* kern = is_max ? reinterpret_cast<const void*>(&heap_replay_kernel<true>)
+                            : reinterpret_cast<const void*>(&heap_replay_kernel<false>);
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    if (e != hipSuccess) return e;
+  }
+  if (is_max)
+    hipLaunchKernelGGL(heap_replay_kernel<true>, dim3(1), dim3(64), lds, s, ops, vals, ids, n_ops, k, out_d, out_ids,
+                       out_n);
+  else
+    hipLaunchKernelGGL(heap_replay_kernel<false>, dim3(1), dim3(64), lds, s, ops, vals, ids, n_ops, k, out_d, out_ids,
+                       out_n);
+  return hipGetLastError();
 }
 
 }  // namespace shine

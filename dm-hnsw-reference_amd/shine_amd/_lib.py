@@ -79,6 +79,7 @@ PROTOTYPES = {
     "shine_index_get_info": (I32, [P, C.POINTER(IndexInfo)]),
     "shine_algorithmic_bytes": (U64, [P, P, U32]),
     "shine_close": (I32, [P]),
+    "shine_selftest_heap": (I32, [I32, P, P, P, U32, U32, P, P, P]),
     "shine_last_error": (C.c_char_p, []),
     "shine_build": (I32, [P, U64, U32, U32, U32, I32, U32, U32, U32, C.POINTER(P)]),
     "shine_build_dump_size": (U64, [P, U32]),

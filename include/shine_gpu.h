@@ -112,6 +112,13 @@ uint64_t shine_algorithmic_bytes(shine_index_t h, const uint32_t* qstats, uint32
 
 int shine_close(shine_index_t h);
 
+/* Diagnostics: replay a sequence of heap operations (0 = push, 1 = pop, 2 = push_k with capacity k) through the
+ * device heap routines the search kernel uses (on device 0) and return the final heap array.  is_max selects
+ * heap::MaxHeapCompare / MinHeapCompare (heap.hh:15-21).  Tests compare it with libstdc++'s std::push_heap /
+ * std::pop_heap on the same sequence. */
+int shine_selftest_heap(int is_max, const int32_t* ops, const float* vals, const uint32_t* ids, uint32_t n_ops,
+                        uint32_t k, float* out_d, uint32_t* out_ids, uint32_t* out_n);
+
 const char* shine_last_error(void);
 
 /* ----------------------------------------------------------------------------------------------------------

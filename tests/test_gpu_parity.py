@@ -185,3 +185,49 @@ def test_fp16_records_recall(gpu_available):
         r32 = D.recall_at_k(i32.knn(q, 10, 128).ids, gt, 10)
         r16 = D.recall_at_k(i16.knn(q, 10, 128).ids, gt, 10)
     assert r16 >= r32 - 0.02, (r16, r32)
+
+
+def _heap_ops(rng, n_ops, ties):
+    ops = rng.choice([0, 0, 0, 1, 2], n_ops).astype(np.int32)
+    vals = (rng.integers(0, 6, n_ops) if ties else rng.permutation(n_ops)).astype(np.float32)
+    ids = np.arange(n_ops, dtype=np.uint32)
+    return ops, vals, ids
+
+
+@pytest.mark.parametrize("is_max", [True, False])
+@pytest.mark.parametrize("ties", [True, False])
+def test_device_heaps_match_libstdcxx(is_max, ties, gpu_available):
+    """The wave-parallel push/pop the kernel uses must leave the exact heap array libstdc++ leaves."""
+    import ctypes as C
+    L = shine_amd._lib
+    rng = np.random.default_rng(17 + is_max + 2 * ties)
+    for n_ops, k in [(1, 1), (2, 1), (7, 3), (100, 8), (600, 40), (3000, 128), (5000, 5000)]:
+        ops, vals, ids = _heap_ops(rng, n_ops, ties)
+        ref_d, ref_i = O.heap_replay(is_max, ops, vals, ids, k)
+        od = np.empty(n_ops + 1, np.float32)
+        oi = np.empty(n_ops + 1, np.uint32)
+        on = np.zeros(1, np.uint32)
+        p = lambda a: a.ctypes.data_as(C.c_void_p)
+        L.check(L.lib().shine_selftest_heap(int(is_max), p(ops), p(vals), p(ids), n_ops, k, p(od), p(oi), p(on)))
+        n = int(on[0])
+        assert n == ref_d.size, (n_ops, k)
+        np.testing.assert_array_equal(oi[:n], ref_i)
+        np.testing.assert_array_equal(od[:n], ref_d)
+
+
+@pytest.mark.parametrize("env", [{"SHINE_DEBUG_VISCAP": "1024"}, {"SHINE_DEBUG_START_MODE": "1"},
+                                 {"SHINE_DEBUG_START_MODE": "2"}])
+def test_visited_modes(env, gpu_available, monkeypatch):
+    """Visited table overflow → re-run with the whole LDS; and the HBM-bitmap variant: identical results."""
+    base = D.sift_like(8000, seed=71)
+    q = D.sift_like(128, seed=72)
+    dumps, _, _ = O.build(base, 16, 100, 0, 1, seed=3)
+    ref = O.OracleIndex(dumps, 128, 16, 0).knn(q, 10, 200)
+    for k_, v in env.items():
+        monkeypatch.setenv(k_, v)
+    with shine_amd.Index.from_buffers(dumps, 128, 16, 0, gpus=[0]) as idx:
+        r = idx.knn(q, 10, 200)
+        if "SHINE_DEBUG_VISCAP" in env:
+            assert r.stats["overflow_retries"] > 0
+        _check_same(r, *ref)
+        _check_same(idx.knn(q, 10, 200), *ref)
