@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -71,6 +72,7 @@ struct Replica {
   // staging for the host-pointer API
   DevBuf<float> q, d;
   DevBuf<uint32_t> ids, qs, ovf;
+  DevBuf<unsigned long long> prof;  // SHINE_PHASE_PROFILE diagnostics
 };
 
 }  // namespace
@@ -246,6 +248,10 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
                    uint32_t* d_ids, float* d_dists, uint32_t* d_qs, hipStream_t s, bool timed) {
   if (int rc = R.ovf.grow(2ull * nq)) return rc;
   HIP_TRY(hipMemsetAsync(R.counter.p, 0, 8 * sizeof(uint32_t), s));  // 3 queue heads + 2 list counts
+  if (env_int("SHINE_PHASE_PROFILE", 0)) {
+    if (int rc = R.prof.grow(8)) return rc;
+    HIP_TRY(hipMemsetAsync(R.prof.p, 0, 8 * sizeof(unsigned long long), s));
+  }
   if (timed) HIP_TRY(hipEventRecord(R.ev0, s));
   const int start = static_cast<int>(env_int("SHINE_DEBUG_START_MODE", 0));  // test hook: exercise modes 1, 2
   for (int mode = start; mode <= 2; ++mode) {
@@ -273,6 +279,10 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     if (mode > start) {
       a.in_list = R.ovf.p + static_cast<size_t>(mode - 1) * nq;
       a.in_count = R.counter.p + 3 + (mode - 1);
+    }
+    if (mode == 0 && env_int("SHINE_PHASE_PROFILE", 0)) {
+      if (int rc = R.prof.grow(8)) return rc;
+      a.prof = R.prof.p;
     }
     if (mode < 2) {
       a.out_list = R.ovf.p + static_cast<size_t>(mode) * nq;
@@ -419,6 +429,13 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, R.ev0, R.ev1));
     kernel_ms = std::max(kernel_ms, static_cast<double>(ms));
+    if (env_int("SHINE_PHASE_PROFILE", 0) && R.prof.p) {
+      unsigned long long ph[8];
+      HIP_TRY(hipMemcpy(ph, R.prof.p, sizeof(ph), hipMemcpyDeviceToHost));
+      std::fprintf(stderr, "SHINE_PHASE_PROFILE cycles: setup %llu greedy %llu pop %llu adj+visited %llu dist %llu "
+                           "predict %llu accept %llu trim+out %llu\n",
+                   ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6], ph[7]);
+    }
     uint32_t ovf_counts[2] = {0, 0};  // queries handed to the fixup passes
     HIP_TRY(hipMemcpy(ovf_counts, R.counter.p + 3, sizeof(ovf_counts), hipMemcpyDeviceToHost));
     retries += ovf_counts[0] + ovf_counts[1];
@@ -513,6 +530,7 @@ int shine_close(shine_index_t h) {
     for (auto* b : {&R.adj0, &R.uid, &R.up_base, &R.adjU, &R.inv_uid, &R.visited, &R.vlog, &R.counter, &R.ids, &R.qs,
                     &R.ovf})
       b->release();
+    R.prof.release();
     R.vec.release();
     R.q.release();
     R.d.release();

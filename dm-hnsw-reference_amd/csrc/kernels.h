@@ -37,6 +37,7 @@ struct SearchArgs {
   const uint32_t* in_count;
   uint32_t* out_list;        // queries that overflow here are appended for the next pass (nullable)
   uint32_t* out_count;
+  unsigned long long* prof; // diagnostics (nullable): per-phase shader-clock totals, PROF kernel variant only
 };
 
 struct DistArgs {

@@ -33,6 +33,8 @@
 
 #include <hip/hip_fp16.h>
 
+#include <type_traits>
+
 namespace shine {
 namespace {
 
@@ -237,8 +239,28 @@ __device__ __forceinline__ u32 vhash(u32 key, u32 shift) { return (key * 0x9E377
 // ------------------------------------------------------------------------------------------------------------
 // search kernel: one wavefront (= one workgroup) per persistent slot
 // ------------------------------------------------------------------------------------------------------------
-template <int D, int METRIC, typename E, int VIS>
+// Phase stamps for the diagnostic (PROF) build: s_memtime with its lgkmcnt wait in one statement.
+__device__ __forceinline__ u64 stamp() {
+  u64 t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+#define PHASE(i)                                   \
+  if constexpr (PROF) {                            \
+    __builtin_amdgcn_sched_barrier(0);             \
+    const u64 _t = stamp();                        \
+    __builtin_amdgcn_sched_barrier(0);             \
+    ph[cur_ph] += _t - t_last;                     \
+    t_last = _t;                                   \
+    cur_ph = (i);                                  \
+  }
+
+template <int D, int METRIC, typename E, int VIS, bool PROF = false>
 __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
+  u64 ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  u64 t_last = 0;
+  int cur_ph = 0;
+  if constexpr (PROF) t_last = stamp();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int ef = static_cast<int>(A.ef), cap = static_cast<int>(A.cap);
   u64* top = reinterpret_cast<u64*>(smem);                                    // MaxHeap top_candidates
@@ -263,6 +285,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
     if (item >= n_items) break;
     const u32 qi = A.in_list ? A.in_list[item] : item;
 
+    PHASE(0)
     QueryRegs<D> Q;
     load_query<D>(A.queries + static_cast<u64>(qi) * D, lane, Q);
     if (VIS == 0) {  // visited_nodes.clear()  (:475) — done up front for this query
@@ -283,6 +306,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
     if (A.g.ep_level > 0) ++st_vup; else ++st_vl0;
 
     // ---- greedy descent search_for_one (hnsw.hh:331-393) ------------------------------------------------
+    PHASE(1)
     u32 nn = ep;
     for (u32 level = A.g.ep_level; level > 0 && status == 0; --level) {
       bool changed;
@@ -350,6 +374,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
 
       // ---- search_level(q, ef, 0) (hnsw.hh:406-476) ---------------------------------------------------------
       while (nnext > 0) {
+        PHASE(2)
         const u64 c = bcast64(nxt[0]);  // next_candidates.top(); pop()  (:418-419)
         const float farthest0 = key(top[0]);
         heap_pop<false>(nxt, nnext, lane);
@@ -357,6 +382,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         if (key(c) > farthest0) break;  // :421-426
 
         // neighbour list of the candidate at level 0 (:436-438)
+        PHASE(3)
         ++st_ll0;
         u32 e = INV;
         if (eid(c) == pre_id) {
@@ -403,9 +429,11 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         st_dist += nf;
         if (VIS == 0 && nvis > A.vis_limit) { status = ST_OVERFLOW; break; }
         if (nf == 0) continue;
+        PHASE(4)
         wave_sync();
         dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, nf, lane);
         wave_sync();
+        PHASE(5)
 
         // Speculative prefetch of the adjacency row of the candidate expected on top of next_candidates once
         // this step's pushes are done: a min-heap root changes only for a strictly smaller key, so the root
@@ -434,6 +462,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         }
 
         // accept / push / push_k in list order (:456-465)
+        PHASE(6)
         for (int j = 0; j < nf; ++j) {
           const float d = sc_d[j];
           const float farthest = key(top[0]);
@@ -456,6 +485,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
       }
 
       // ---- trim to k and emit in heap-array order (:296-303) ------------------------------------------------
+      PHASE(7)
       if (status == 0) {
         while (ntop > static_cast<int>(A.k)) {
           heap_pop<true>(top, ntop, lane);
@@ -501,6 +531,11 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+  }
+  if constexpr (PROF) {
+    PHASE(0)
+    if (lane == 0 && A.prof)
+      for (int i = 0; i < 8; ++i) atomicAdd(&A.prof[i], static_cast<unsigned long long>(ph[i]));
   }
 }
 
@@ -587,6 +622,9 @@ hipError_t launch_search_t(uint32_t grid, const SearchArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, s, a);
     return hipGetLastError();
   };
+  if constexpr (D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
+    if (a.prof && a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0, true>);
+  }
   if (a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0>);
   return run(search_kernel<D, METRIC, E, 1>);
 }
