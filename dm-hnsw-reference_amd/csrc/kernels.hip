@@ -49,7 +49,6 @@ __device__ __forceinline__ u32 eid(u64 e) { return static_cast<u32>(e >> 32); }
 __device__ __forceinline__ u64 mk(float d, u32 id) { return (static_cast<u64>(id) << 32) | __float_as_uint(d); }
 
 __device__ __forceinline__ u32 bcast(u32 v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ float bcastf(float v) { return __uint_as_float(bcast(__float_as_uint(v))); }
 __device__ __forceinline__ u64 bcast64(u64 v) {
   return (static_cast<u64>(bcast(static_cast<u32>(v >> 32))) << 32) | bcast(static_cast<u32>(v));
 }
@@ -237,7 +236,121 @@ __device__ __forceinline__ void dist_list(const E* __restrict__ vec, const Query
 __device__ __forceinline__ u32 vhash(u32 key, u32 shift) { return (key * 0x9E3779B1u) >> shift; }
 
 // ------------------------------------------------------------------------------------------------------------
+// Wave-wide minimum on DPP: row_shr 1/2/4/8 inside each 16-lane row, then row_bcast15 / row_bcast31 — six VALU
+// steps instead of a ds_bpermute butterfly.  Lanes that hold nothing must pass +inf; NaN never wins.
+// ------------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_min(float v) {
+  int x = __float_as_int(v);
+#define SHINE_DPP_MIN(CTRL, RM)                                                                        \
+  x = __float_as_int(fminf(__int_as_float(x),                                                          \
+                           __int_as_float(__builtin_amdgcn_update_dpp(0x7F800000, x, CTRL, RM, 0xF, false))));
+  SHINE_DPP_MIN(0x111, 0xF)
+  SHINE_DPP_MIN(0x112, 0xF)
+  SHINE_DPP_MIN(0x114, 0xF)
+  SHINE_DPP_MIN(0x118, 0xF)
+  SHINE_DPP_MIN(0x142, 0xA)
+  SHINE_DPP_MIN(0x143, 0xC)
+#undef SHINE_DPP_MIN
+  return __int_as_float(__builtin_amdgcn_readlane(x, 63));
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Register-resident heaps.  With the batch spread at one wavefront per SIMD a wave may own up to 512 VGPRs, so
+// a heap of NR*64 entries lives in 2*NR VGPRs: entry i in lane i % 64 of register i / 64.  The libstdc++
+// algorithms then run as scalar code over v_readlane / lane-select writes (uniform index, SGPR results) — no LDS
+// round trip per heap level.
+// ------------------------------------------------------------------------------------------------------------
+template <int NR>
+struct RHeap {  // vector values, not arrays: dynamic element access lowers to GPR-indexed moves, never scratch
+  using V = int __attribute__((ext_vector_type(NR < 2 ? 2 : NR)));
+  V k;  // key bits (float)
+  V v;  // dense node id
+};
+
+// Entry i: register i >> 6 (uniform, so the private arrays become VGPR vectors read and written with
+// GPR-indexed moves), lane i & 63 (v_readlane / a lane-select write).
+template <int NR>
+__device__ __forceinline__ void rget(const RHeap<NR>& H, int i, float& k, u32& v) {
+  const int r = i >> 6, l = i & 63;
+  k = __int_as_float(__builtin_amdgcn_readlane(H.k[r], l));
+  v = static_cast<u32>(__builtin_amdgcn_readlane(H.v[r], l));
+}
+template <int NR>
+__device__ __forceinline__ void rput(RHeap<NR>& H, int i, float k, u32 v) {
+  const int r = i >> 6, l = i & 63;
+  const bool mine = static_cast<int>(threadIdx.x) == l;
+  const int ck = H.k[r], cv = H.v[r];
+  H.k[r] = mine ? __float_as_int(k) : ck;
+  H.v[r] = mine ? static_cast<int>(v) : cv;
+}
+template <int NR>
+__device__ __forceinline__ float rkey0(const RHeap<NR>& H) {
+  return __int_as_float(__builtin_amdgcn_readlane(H.k[0], 0));
+}
+
+// std::__push_heap(first, n, 0, value)
+template <bool MAXH, int NR>
+__device__ __forceinline__ void rheap_push(RHeap<NR>& H, int n, float vk, u32 vv) {
+  int hole = n;
+  while (hole > 0) {
+    const int parent = (hole - 1) >> 1;
+    float pk;
+    u32 pv;
+    rget(H, parent, pk, pv);
+    if (!hcmp<MAXH>(pk, vk)) break;
+    rput(H, hole, pk, pv);
+    hole = parent;
+  }
+  rput(H, hole, vk, vv);
+}
+
+// std::pop_heap(first, first + n) + pop_back  ≡  std::__adjust_heap(first, 0, n - 1, first[n - 1])
+template <bool MAXH, int NR>
+__device__ __forceinline__ void rheap_pop(RHeap<NR>& H, int n) {
+  if (n <= 1) return;
+  const int len = n - 1;
+  float vk;
+  u32 vv;
+  rget(H, len, vk, vv);
+  int hole = 0, second = 0;
+  while (second < (len - 1) / 2) {
+    second = 2 * (second + 1);
+    float rk, lk;
+    u32 rv, lv;
+    rget(H, second, rk, rv);
+    rget(H, second - 1, lk, lv);
+    if (hcmp<MAXH>(rk, lk)) {
+      --second;
+      rput(H, hole, lk, lv);
+    } else {
+      rput(H, hole, rk, rv);
+    }
+    hole = second;
+  }
+  if ((len & 1) == 0 && second == (len - 2) / 2) {
+    second = 2 * (second + 1);
+    float lk;
+    u32 lv;
+    rget(H, second - 1, lk, lv);
+    rput(H, hole, lk, lv);
+    hole = second - 1;
+  }
+  while (hole > 0) {
+    const int parent = (hole - 1) >> 1;
+    float pk;
+    u32 pv;
+    rget(H, parent, pk, pv);
+    if (!hcmp<MAXH>(pk, vk)) break;
+    rput(H, hole, pk, pv);
+    hole = parent;
+  }
+  rput(H, hole, vk, vv);
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // search kernel: one wavefront (= one workgroup) per persistent slot
+//   VIS   0: visited table in LDS, 1: visited bitmap in HBM
+//   HEAPS 0: top / next in registers (NRT / NRN VGPRs per field), 1: in LDS with the wave-parallel routines
 // ------------------------------------------------------------------------------------------------------------
 // Phase stamps for the diagnostic (PROF) build: s_memtime with its lgkmcnt wait in one statement.
 __device__ __forceinline__ u64 stamp() {
@@ -245,28 +358,49 @@ __device__ __forceinline__ u64 stamp() {
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
   return t;
 }
-#define PHASE(i)                                   \
-  if constexpr (PROF) {                            \
-    __builtin_amdgcn_sched_barrier(0);             \
-    const u64 _t = stamp();                        \
-    __builtin_amdgcn_sched_barrier(0);             \
-    ph[cur_ph] += _t - t_last;                     \
-    t_last = _t;                                   \
-    cur_ph = (i);                                  \
-  }
-
-template <int D, int METRIC, typename E, int VIS, bool PROF = false>
-__global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
+template <bool PROF>
+struct PhaseClock {  // empty unless PROF
+  __device__ void start() {}
+  __device__ void mark(int) {}
+  __device__ void flush(unsigned long long*, int) {}
+};
+template <>
+struct PhaseClock<true> {
   u64 ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u64 t_last = 0;
-  int cur_ph = 0;
-  if constexpr (PROF) t_last = stamp();
+  int cur = 0;
+  __device__ void start() { t_last = stamp(); }
+  __device__ void mark(int i) {
+    __builtin_amdgcn_sched_barrier(0);
+    const u64 t = stamp();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j == cur) ph[j] += t - t_last;
+    t_last = t;
+    cur = i;
+  }
+  __device__ void flush(unsigned long long* out, int lane) {
+    mark(0);
+    if (lane == 0 && out)
+      for (int j = 0; j < 8; ++j) atomicAdd(&out[j], static_cast<unsigned long long>(ph[j]));
+  }
+};
+#define PHASE(i) clk.mark(i);
+
+// amdgpu_waves_per_eu(1, 2): a batch of B queries keeps B / 256 wavefronts per CU resident (4 at the bench's
+// 1,024), so each wave may spend up to 256 VGPRs — that is what keeps the register heaps out of scratch.
+template <int D, int METRIC, typename E, int VIS, int HEAPS, int NRT, int NRN, bool PROF = false>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void search_kernel(SearchArgs A) {
+  PhaseClock<PROF> clk;
+  clk.start();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int ef = static_cast<int>(A.ef), cap = static_cast<int>(A.cap);
-  u64* top = reinterpret_cast<u64*>(smem);                                    // MaxHeap top_candidates
-  u64* nxt = reinterpret_cast<u64*>(smem + align16(8ull * ef));               // MinHeap next_candidates
-  u32* vtab = reinterpret_cast<u32*>(smem + align16(8ull * ef) + align16(8ull * cap));
-  u32* sc_ids = vtab + (VIS == 0 ? A.vis_cap : 0u);                           // fresh neighbours
+  const size_t top_b = HEAPS == 1 ? align16(8ull * ef) : 0, next_b = HEAPS == 1 ? align16(8ull * cap) : 0;
+  u64* top = reinterpret_cast<u64*>(smem);                     // MaxHeap top_candidates   (HEAPS = 1)
+  u64* nxt = reinterpret_cast<u64*>(smem + top_b);             // MinHeap next_candidates  (HEAPS = 1)
+  u32* vtab = reinterpret_cast<u32*>(smem + top_b + next_b);   // visited table            (VIS = 0)
+  u32* sc_ids = vtab + (VIS == 0 ? A.vis_cap : 0u);            // fresh neighbours
   float* sc_d = reinterpret_cast<float*>(sc_ids + 64);
 
   const int lane = threadIdx.x;
@@ -292,6 +426,8 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
       uint4* t4 = reinterpret_cast<uint4*>(vtab);
       for (u32 i = lane; i < A.vis_cap / 4; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
     }
+    RHeap<NRT> TH;  // top_candidates  (HEAPS = 0)
+    RHeap<NRN> NH;  // next_candidates (HEAPS = 0)
 
     u32 st_dist = 0, st_vup = 0, st_vl0 = 0, st_lup = 0, st_ll0 = 0, st_maxnext = 0, status = 0;
 
@@ -329,17 +465,10 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         // first neighbour (list order) attaining the minimum; adopted only if strictly closer (:378)
         float bd = (lane < cnt) ? sc_d[lane] : __builtin_inff();
         if (bd != bd) bd = __builtin_inff();  // NaN never compares less
-        int bi = lane;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-          const float od = __shfl_xor(bd, off);
-          const int oi = __shfl_xor(bi, off);
-          if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
-        }
-        bd = bcastf(bd);
-        bi = static_cast<int>(bcast(static_cast<u32>(bi)));
-        if (bd < closest) {
-          closest = bd;
+        const float mn = wave_min(bd);
+        if (mn < closest) {
+          const int bi = static_cast<int>(__builtin_ctzll(__ballot(bd == mn)));
+          closest = mn;
           nn = sc_ids[bi];
           changed = true;
         }
@@ -353,13 +482,18 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
     u32 logpos = 0, nvis = 1;
     bool log_overflow = false;
     if (status == 0) {
-      const u64 e0 = mk(closest, nn);
+      if constexpr (HEAPS == 0) {
+        rput(TH, 0, closest, nn);
+        rput(NH, 0, closest, nn);  // search_level :412-415
+      }
       if (lane == 0) {
-        top[0] = e0;
-        nxt[0] = e0;  // search_level :412-415
+        if constexpr (HEAPS == 1) {
+          const u64 e0 = mk(closest, nn);
+          top[0] = e0;
+          nxt[0] = e0;
+        }
         if (VIS == 0) {
-          u32 h = vhash(nn, vshift);
-          vtab[h] = nn;  // table is empty: first probe slot is free
+          vtab[vhash(nn, vshift)] = nn;  // table is empty: the first probe slot is free
         } else {
           atomicOr(&vis[nn >> 5], 1u << (nn & 31));
           vlog[0] = nn;
@@ -375,20 +509,30 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
       // ---- search_level(q, ef, 0) (hnsw.hh:406-476) ---------------------------------------------------------
       while (nnext > 0) {
         PHASE(2)
-        const u64 c = bcast64(nxt[0]);  // next_candidates.top(); pop()  (:418-419)
-        const float farthest0 = key(top[0]);
-        heap_pop<false>(nxt, nnext, lane);
+        float ck, farthest0;
+        u32 cid;
+        if constexpr (HEAPS == 0) {  // next_candidates.top(); pop()  (:418-419)
+          rget(NH, 0, ck, cid);
+          farthest0 = rkey0(TH);
+          rheap_pop<false>(NH, nnext);
+        } else {
+          const u64 c = bcast64(nxt[0]);
+          ck = key(c);
+          cid = eid(c);
+          farthest0 = key(top[0]);
+          heap_pop<false>(nxt, nnext, lane);
+        }
         --nnext;
-        if (key(c) > farthest0) break;  // :421-426
+        if (ck > farthest0) break;  // :421-426
 
         // neighbour list of the candidate at level 0 (:436-438)
         PHASE(3)
         ++st_ll0;
         u32 e = INV;
-        if (eid(c) == pre_id) {
+        if (cid == pre_id) {
           e = pre_e;
         } else if (static_cast<u32>(lane) < M0) {
-          e = A.g.adj0[static_cast<u64>(eid(c)) * M0 + lane];
+          e = A.g.adj0[static_cast<u64>(cid) * M0 + lane];
         }
         bool cand = e != INV;
         if (!A.g.lists_unique) {  // first occurrence in list order wins (visited.insert order, :443)
@@ -434,29 +578,34 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, nf, lane);
         wave_sync();
         PHASE(5)
+        // lane j < nf holds fresh neighbour j (list order)
+        const float my_d = lane < nf ? sc_d[lane] : __builtin_inff();
+        const u32 my_id = lane < nf ? sc_ids[lane] : INV;
 
         // Speculative prefetch of the adjacency row of the candidate expected on top of next_candidates once
         // this step's pushes are done: a min-heap root changes only for a strictly smaller key, so the root
         // survives ties and, among the fresh keys, the first minimum in list order wins.
         {
-          float pd = __builtin_inff();
-          u32 pidx = 64;
-          if (lane < nf) {
-            const float d = sc_d[lane];
-            if (d < farthest0 || ntop < ef) { pd = d; pidx = lane; }
-          }
-#pragma unroll
-          for (int off = 32; off > 0; off >>= 1) {
-            const float od = __shfl_xor(pd, off);
-            const u32 oi = __shfl_xor(pidx, off);
-            if (od < pd || (od == pd && oi < pidx)) { pd = od; pidx = oi; }
-          }
-          pd = bcastf(pd);
-          pidx = bcast(pidx);
+          const float pd_l = (lane < nf && (my_d < farthest0 || ntop < ef) && my_d == my_d) ? my_d : __builtin_inff();
+          const float pd = wave_min(pd_l);
           u32 pid = INV;
-          if (nnext > 0 && !(pd < key(nxt[0]))) pid = eid(nxt[0]);
-          else if (pidx < 64) pid = sc_ids[pidx];
-          pid = bcast(pid);
+          float rk0 = __builtin_inff();
+          u32 rid0 = INV;
+          if (nnext > 0) {
+            if constexpr (HEAPS == 0) {
+              rget(NH, 0, rk0, rid0);
+            } else {
+              const u64 r0 = bcast64(nxt[0]);
+              rk0 = key(r0);
+              rid0 = eid(r0);
+            }
+          }
+          if (nnext > 0 && !(pd < rk0)) {
+            pid = rid0;
+          } else if (pd < __builtin_inff()) {
+            const u64 hit = __ballot(pd_l == pd);
+            pid = __builtin_amdgcn_readlane(static_cast<int>(my_id), static_cast<int>(__builtin_ctzll(hit)));
+          }
           pre_id = pid;
           if (pid != INV && static_cast<u32>(lane) < M0) pre_e = A.g.adj0[static_cast<u64>(pid) * M0 + lane];
         }
@@ -464,20 +613,32 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         // accept / push / push_k in list order (:456-465)
         PHASE(6)
         for (int j = 0; j < nf; ++j) {
-          const float d = sc_d[j];
-          const float farthest = key(top[0]);
+          const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_d), j));
+          const float farthest = HEAPS == 0 ? rkey0(TH) : key(top[0]);
           if (d < farthest || ntop < ef) {
             if (nnext >= cap) { status = ST_OVERFLOW; break; }
-            const u64 en = mk(d, sc_ids[j]);
-            heap_push<false>(nxt, nnext, en, lane);
-            ++nnext;
-            if (ntop < ef) {  // heap.hh:34-41 push_k
-              heap_push<true>(top, ntop, en, lane);
-              ++ntop;
-            } else {  // d < top().distance holds: it is the accept test with the top full
-              heap_pop<true>(top, ntop, lane);
-              heap_push<true>(top, ntop - 1, en, lane);
+            const u32 id = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(my_id), j));
+            if constexpr (HEAPS == 0) {
+              rheap_push<false>(NH, nnext, d, id);
+              if (ntop < ef) {  // heap.hh:34-41 push_k
+                rheap_push<true>(TH, ntop, d, id);
+                ++ntop;
+              } else {  // d < top().distance holds: it is the accept test with the top full
+                rheap_pop<true>(TH, ntop);
+                rheap_push<true>(TH, ntop - 1, d, id);
+              }
+            } else {
+              const u64 en = mk(d, id);
+              heap_push<false>(nxt, nnext, en, lane);
+              if (ntop < ef) {
+                heap_push<true>(top, ntop, en, lane);
+                ++ntop;
+              } else {
+                heap_pop<true>(top, ntop, lane);
+                heap_push<true>(top, ntop - 1, en, lane);
+              }
             }
+            ++nnext;
             if (static_cast<u32>(nnext) > st_maxnext) st_maxnext = nnext;
           }
         }
@@ -488,23 +649,36 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
       PHASE(7)
       if (status == 0) {
         while (ntop > static_cast<int>(A.k)) {
-          heap_pop<true>(top, ntop, lane);
+          if constexpr (HEAPS == 0) rheap_pop<true>(TH, ntop);
+          else heap_pop<true>(top, ntop, lane);
           --ntop;
         }
       }
     }
 
     const u64 obase = static_cast<u64>(qi) * A.k;
-    for (u32 i = lane; i < A.k; i += 64) {
-      u32 id = INV;
-      float d = 0.f;
-      if (status == 0 && static_cast<int>(i) < ntop) {
-        const u64 en = top[i];
-        id = A.g.uid[eid(en)];
-        d = key(en);
+    if constexpr (HEAPS == 0) {
+#pragma unroll
+      for (int r = 0; r < NRT; ++r) {
+        const u32 i = static_cast<u32>(r * 64 + lane);
+        if (i < A.k) {
+          const bool ok = status == 0 && static_cast<int>(i) < ntop;
+          A.out_ids[obase + i] = ok ? A.g.uid[static_cast<u32>(TH.v[r])] : INV;
+          if (A.out_dists) A.out_dists[obase + i] = ok ? __int_as_float(TH.k[r]) : 0.f;
+        }
       }
-      A.out_ids[obase + i] = id;
-      if (A.out_dists) A.out_dists[obase + i] = d;
+    } else {
+      for (u32 i = lane; i < A.k; i += 64) {
+        u32 id = INV;
+        float d = 0.f;
+        if (status == 0 && static_cast<int>(i) < ntop) {
+          const u64 en = top[i];
+          id = A.g.uid[eid(en)];
+          d = key(en);
+        }
+        A.out_ids[obase + i] = id;
+        if (A.out_dists) A.out_dists[obase + i] = d;
+      }
     }
     if (status == ST_OVERFLOW && A.out_list && lane == 0) A.out_list[atomicAdd(A.out_count, 1u)] = qi;
     if (A.qstats && lane == 0) {
@@ -532,11 +706,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
-  if constexpr (PROF) {
-    PHASE(0)
-    if (lane == 0 && A.prof)
-      for (int i = 0; i < 8; ++i) atomicAdd(&A.prof[i], static_cast<unsigned long long>(ph[i]));
-  }
+  clk.flush(A.prof, lane);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -612,7 +782,8 @@ __global__ __launch_bounds__(64) void heap_replay_kernel(const int32_t* ops, con
 
 template <int D, int METRIC, typename E>
 hipError_t launch_search_t(uint32_t grid, const SearchArgs& a, hipStream_t s) {
-  const size_t lds = search_lds_bytes(a.ef, a.cap, a.vis_cap);
+  const bool reg_heaps = a.heap_regs != 0;
+  const size_t lds = search_lds_bytes(reg_heaps ? 0 : a.ef, reg_heaps ? 0 : a.cap, a.vis_cap);
   auto run = [&](auto kern) -> hipError_t {
     if (lds > 65536) {  // beyond the default dynamic-LDS limit: opt in (per device, so every launch)
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -622,11 +793,21 @@ hipError_t launch_search_t(uint32_t grid, const SearchArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, s, a);
     return hipGetLastError();
   };
-  if constexpr (D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
-    if (a.prof && a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0, true>);
+  if (reg_heaps) {
+    if (a.vis_cap == 0 || a.cap > kRegNextCap) return hipErrorInvalidValue;
+    if constexpr (D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
+      if (a.prof) {
+        if (a.ef <= 64) return run(search_kernel<D, METRIC, E, 0, 0, 1, kRegNextCap / 64, true>);
+        if (a.ef <= 128) return run(search_kernel<D, METRIC, E, 0, 0, 2, kRegNextCap / 64, true>);
+      }
+    }
+    if (a.ef <= 64) return run(search_kernel<D, METRIC, E, 0, 0, 1, kRegNextCap / 64>);
+    if (a.ef <= 128) return run(search_kernel<D, METRIC, E, 0, 0, 2, kRegNextCap / 64>);
+    if (a.ef <= 256) return run(search_kernel<D, METRIC, E, 0, 0, 4, kRegNextCap / 64>);
+    return hipErrorInvalidValue;
   }
-  if (a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0>);
-  return run(search_kernel<D, METRIC, E, 1>);
+  if (a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0, 1, 1, 1>);
+  return run(search_kernel<D, METRIC, E, 1, 1, 1, 1>);
 }
 
 template <int D, int METRIC, typename E>
