@@ -190,7 +190,7 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
 // 160 KiB go to the queues.  A query that outgrows them is re-run alone per CU with the whole LDS (mode 1),
 // then with the visited set in HBM (mode 2); only then does it fail with SHINE_ERR_OVERFLOW.
 struct LaunchShape {
-  uint32_t cap, grid, vis_cap, vis_limit, heap_regs;
+  uint32_t cap, grid, vis_cap, vis_limit;
 };
 
 uint32_t pow2_at_least(uint32_t x) {
@@ -204,39 +204,26 @@ int64_t env_int(const char* name, int64_t dflt) {
   return e ? std::atoll(e) : dflt;
 }
 
-// mode 0: one wavefront per query up to 16 per CU; heaps in VGPRs when ef <= 256 (next_candidates <= 512
-//         entries), visited table in the LDS share.
-// mode 1: one wavefront per CU, heaps and a 16K-entry visited table in LDS (fixup pass).
-// mode 2: one wavefront per CU, heaps in LDS, visited bitmap in HBM (fixup pass).
+// mode 0: one wavefront per query up to 16 per CU; top / next / visited table in the wave's LDS share.
+// mode 1: one wavefront per CU with the whole 160 KiB: 16K-entry visited table, larger next queue (fixup).
+// mode 2: one wavefront per CU, visited bitmap in HBM, next queue takes the LDS (fixup).
 LaunchShape pick_shape(uint32_t nq, uint32_t ef, int mode) {
   LaunchShape sh{};
   const uint64_t top_bytes = align16(8ull * ef);
   uint32_t wpc = 1;
   if (mode == 0) {
-    const int64_t dbg_cap = env_int("SHINE_DEBUG_CAP", 0);  // test hook: a tiny queue forces the fixup passes
-    sh.heap_regs = ef <= 256 && (dbg_cap == 0 || dbg_cap <= static_cast<int64_t>(kRegNextCap)) ? 1u : 0u;
-    const uint32_t want_vis = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(48 * ef)));
-    const uint64_t heap_b = sh.heap_regs ? 0 : top_bytes + 8ull * 4 * ef;
-    const uint64_t need = heap_b + 4ull * want_vis + 512;
+    sh.vis_cap = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(48 * ef)));
+    const uint64_t need = search_lds_bytes(ef, 4 * ef, sh.vis_cap);
     const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(kLdsPerCu / need));
     wpc = std::max<uint32_t>(1, std::min<uint32_t>({(nq + kCus - 1) / kCus, 16u, fit}));
-    const uint64_t budget = (kLdsPerCu / wpc) & ~15u;
-    sh.vis_cap = want_vis;
-    while (sh.vis_cap < 16384 && heap_b + 8ull * sh.vis_cap + 512 <= budget) sh.vis_cap *= 2;  // spare LDS
-    sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));             // test hook
-    if (sh.heap_regs) {
-      sh.cap = kRegNextCap;
-    } else {
-      const int64_t cap = (static_cast<int64_t>(budget) - static_cast<int64_t>(top_bytes) - 4ll * sh.vis_cap - 512) / 8;
-      sh.cap = static_cast<uint32_t>(std::max<int64_t>(cap & ~1ll, 2));
-    }
-    if (dbg_cap > 0) sh.cap = static_cast<uint32_t>(dbg_cap);
+    sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
   } else {
     sh.vis_cap = mode == 1 ? 16384 : 0;  // mode 2: visited bitmap in HBM
-    const int64_t cap =
-        (static_cast<int64_t>(kLdsPerCu) - static_cast<int64_t>(top_bytes) - 4ll * sh.vis_cap - 512) / 8;
-    sh.cap = static_cast<uint32_t>(std::max<int64_t>(cap & ~1ll, 2));
   }
+  const uint64_t budget = (kLdsPerCu / wpc) & ~15u;
+  const int64_t cap = (static_cast<int64_t>(budget) - static_cast<int64_t>(top_bytes) - 4ll * sh.vis_cap - 512) / 8;
+  sh.cap = static_cast<uint32_t>(std::max<int64_t>(cap & ~1ll, 2));
+  if (mode == 0) sh.cap = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_DEBUG_CAP", sh.cap)));  // test hook
   sh.vis_limit = sh.vis_cap / 8 * 7;  // linear probing stays short; >= 64 free slots for one expansion
   sh.grid = std::max<uint32_t>(1, std::min<uint32_t>(nq, kCus * wpc));
   return sh;
@@ -282,7 +269,6 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     a.cap = sh.cap;
     a.vis_cap = sh.vis_cap;
     a.vis_limit = sh.vis_limit;
-    a.heap_regs = sh.heap_regs;
     a.out_ids = d_ids;
     a.out_dists = d_dists;
     a.qstats = d_qs;

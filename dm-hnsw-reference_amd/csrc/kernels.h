@@ -38,10 +38,7 @@ struct SearchArgs {
   uint32_t* out_list;        // queries that overflow here are appended for the next pass (nullable)
   uint32_t* out_count;
   unsigned long long* prof; // diagnostics (nullable): per-phase shader-clock totals, PROF kernel variant only
-  uint32_t heap_regs;       // 1: top / next kept in VGPRs (ef <= 256, cap <= kRegNextCap); 0: in LDS
 };
-
-constexpr uint32_t kRegNextCap = 512;  // next_candidates capacity of the register-resident variant
 
 struct DistArgs {
   DevGraph g;

@@ -69,9 +69,10 @@ __device__ __forceinline__ bool hcmp(float a, float b) {
   return MAXH ? (a < b) : (a > b);
 }
 
-// push_back(v) + std::push_heap on h[0..n]  ≡  std::__push_heap(h, n, 0, v)
+// push_back(v) + std::push_heap on h[0..n]  ≡  std::__push_heap(h, n, 0, v).  Returns the new root given the
+// old one (root0; ignored when n == 0).
 template <bool MAXH>
-__device__ __forceinline__ void heap_push(u64* h, int n, u64 v, int lane) {
+__device__ __forceinline__ u64 heap_push(u64* h, int n, u64 v, u64 root0, int lane) {
   const float vd = key(v);
   const int L = 31 - __clz(n + 1);  // ancestors of slot n
   u64 ent = 0;
@@ -86,32 +87,40 @@ __device__ __forceinline__ void heap_push(u64* h, int n, u64 v, int lane) {
   const int fin = s == 0 ? n : ((n + 1) >> s) - 1;
   if (lane == 0) h[fin] = v;
   wave_sync();
+  return fin == 0 ? v : root0;
 }
 
-// std::pop_heap on h[0..n) followed by pop_back  ≡  std::__adjust_heap(h, 0, n-1, h[n-1])
+// std::pop_heap on h[0..n) followed by pop_back  ≡  std::__adjust_heap(h, 0, n-1, h[n-1]).  Returns the new
+// root (meaningless when n <= 1).
+//
+// The hole's walk is resolved six levels per LDS round: lane i plays internal node i+1 (1-based) of the
+// 63-node window below the hole, reads both children's keys (adjacent slots: one ds_read2_b32) and votes
+// "right child wins"; the walk then follows the ballot with scalar bit tests.
 template <bool MAXH>
-__device__ __forceinline__ void heap_pop(u64* h, int n, int lane) {
-  if (n <= 1) return;
+__device__ __forceinline__ u64 heap_pop(u64* h, int n, int lane) {
+  if (n <= 1) return 0;
   const int len = n - 1;
   const u64 value = h[len];
   const float vk = key(value);
   const int lim = (len - 1) / 2;  // the hole has two children while hole < lim
-  // lane m holds node m+2 (1-based) of a 5-level subtree: levels 1..5 below its root
-  const int rel = lane + 2;
-  const int rl = 31 - __clz(rel);
-  const int ro = rel - (1 << rl);
+  const u32* hk = reinterpret_cast<const u32*>(h);
+  const int j1 = lane + 1;
+  const int lj = 31 - __clz(j1);
+  const int oj = j1 - (1 << lj);
   int pos = 0, L = 0, my_child = 0;  // lane t: the path's (t+1)-th node
   while (pos < lim) {
-    const int absn = ((pos + 1) << rl) - 1 + ro;
-    float kk = 0.f;
-    if (lane < 62 && absn < len) kk = key(h[absn]);
-    const float lk = __shfl(kk, 2 * lane);      // left child of subtree node lane+1
-    const float rk = __shfl(kk, 2 * lane + 1);  // right child
-    const bool right = !hcmp<MAXH>(rk, lk);     // libstdc++ takes the left child iff comp(right, left)
-    const u64 W = __ballot(lane < 31 && right);
+    const int a = ((pos + 1) << lj) - 1 + oj;  // this lane's node
+    const int c1 = 2 * a + 1;
+    bool right = false;
+    if (lane < 63 && c1 + 1 < len) {
+      const float lk = __uint_as_float(hk[2 * c1]);
+      const float rk = __uint_as_float(hk[2 * c1 + 2]);
+      right = !hcmp<MAXH>(rk, lk);  // libstdc++ takes the left child iff comp(right, left)
+    }
+    const u64 W = __ballot(right);
     int r1 = 1;
 #pragma unroll
-    for (int s = 0; s < 5; ++s) {
+    for (int s = 0; s < 6; ++s) {
       if (pos >= lim) break;
       const int b = static_cast<int>((W >> (r1 - 1)) & 1ull);
       const int child = 2 * pos + 1 + b;
@@ -141,6 +150,7 @@ __device__ __forceinline__ void heap_pop(u64* h, int n, int lane) {
   if (lane < j) h[(my_child - 1) >> 1] = ent;  // path nodes above the landing slot shift up
   if (lane == 0) h[pj] = value;
   wave_sync();
+  return j == 0 ? value : bcast64(ent);  // lane 0 holds the path's first node
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -255,102 +265,8 @@ __device__ __forceinline__ float wave_min(float v) {
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// Register-resident heaps.  With the batch spread at one wavefront per SIMD a wave may own up to 512 VGPRs, so
-// a heap of NR*64 entries lives in 2*NR VGPRs: entry i in lane i % 64 of register i / 64.  The libstdc++
-// algorithms then run as scalar code over v_readlane / lane-select writes (uniform index, SGPR results) — no LDS
-// round trip per heap level.
-// ------------------------------------------------------------------------------------------------------------
-template <int NR>
-struct RHeap {  // vector values, not arrays: dynamic element access lowers to GPR-indexed moves, never scratch
-  using V = int __attribute__((ext_vector_type(NR < 2 ? 2 : NR)));
-  V k;  // key bits (float)
-  V v;  // dense node id
-};
-
-// Entry i: register i >> 6 (uniform, so the private arrays become VGPR vectors read and written with
-// GPR-indexed moves), lane i & 63 (v_readlane / a lane-select write).
-template <int NR>
-__device__ __forceinline__ void rget(const RHeap<NR>& H, int i, float& k, u32& v) {
-  const int r = i >> 6, l = i & 63;
-  k = __int_as_float(__builtin_amdgcn_readlane(H.k[r], l));
-  v = static_cast<u32>(__builtin_amdgcn_readlane(H.v[r], l));
-}
-template <int NR>
-__device__ __forceinline__ void rput(RHeap<NR>& H, int i, float k, u32 v) {
-  const int r = i >> 6, l = i & 63;
-  const bool mine = static_cast<int>(threadIdx.x) == l;
-  const int ck = H.k[r], cv = H.v[r];
-  H.k[r] = mine ? __float_as_int(k) : ck;
-  H.v[r] = mine ? static_cast<int>(v) : cv;
-}
-template <int NR>
-__device__ __forceinline__ float rkey0(const RHeap<NR>& H) {
-  return __int_as_float(__builtin_amdgcn_readlane(H.k[0], 0));
-}
-
-// std::__push_heap(first, n, 0, value)
-template <bool MAXH, int NR>
-__device__ __forceinline__ void rheap_push(RHeap<NR>& H, int n, float vk, u32 vv) {
-  int hole = n;
-  while (hole > 0) {
-    const int parent = (hole - 1) >> 1;
-    float pk;
-    u32 pv;
-    rget(H, parent, pk, pv);
-    if (!hcmp<MAXH>(pk, vk)) break;
-    rput(H, hole, pk, pv);
-    hole = parent;
-  }
-  rput(H, hole, vk, vv);
-}
-
-// std::pop_heap(first, first + n) + pop_back  ≡  std::__adjust_heap(first, 0, n - 1, first[n - 1])
-template <bool MAXH, int NR>
-__device__ __forceinline__ void rheap_pop(RHeap<NR>& H, int n) {
-  if (n <= 1) return;
-  const int len = n - 1;
-  float vk;
-  u32 vv;
-  rget(H, len, vk, vv);
-  int hole = 0, second = 0;
-  while (second < (len - 1) / 2) {
-    second = 2 * (second + 1);
-    float rk, lk;
-    u32 rv, lv;
-    rget(H, second, rk, rv);
-    rget(H, second - 1, lk, lv);
-    if (hcmp<MAXH>(rk, lk)) {
-      --second;
-      rput(H, hole, lk, lv);
-    } else {
-      rput(H, hole, rk, rv);
-    }
-    hole = second;
-  }
-  if ((len & 1) == 0 && second == (len - 2) / 2) {
-    second = 2 * (second + 1);
-    float lk;
-    u32 lv;
-    rget(H, second - 1, lk, lv);
-    rput(H, hole, lk, lv);
-    hole = second - 1;
-  }
-  while (hole > 0) {
-    const int parent = (hole - 1) >> 1;
-    float pk;
-    u32 pv;
-    rget(H, parent, pk, pv);
-    if (!hcmp<MAXH>(pk, vk)) break;
-    rput(H, hole, pk, pv);
-    hole = parent;
-  }
-  rput(H, hole, vk, vv);
-}
-
-// ------------------------------------------------------------------------------------------------------------
 // search kernel: one wavefront (= one workgroup) per persistent slot
 //   VIS   0: visited table in LDS, 1: visited bitmap in HBM
-//   HEAPS 0: top / next in registers (NRT / NRN VGPRs per field), 1: in LDS with the wave-parallel routines
 // ------------------------------------------------------------------------------------------------------------
 // Phase stamps for the diagnostic (PROF) build: s_memtime with its lgkmcnt wait in one statement.
 __device__ __forceinline__ u64 stamp() {
@@ -388,17 +304,15 @@ struct PhaseClock<true> {
 };
 #define PHASE(i) clk.mark(i);
 
-// amdgpu_waves_per_eu(1, 2): a batch of B queries keeps B / 256 wavefronts per CU resident (4 at the bench's
-// 1,024), so each wave may spend up to 256 VGPRs — that is what keeps the register heaps out of scratch.
-template <int D, int METRIC, typename E, int VIS, int HEAPS, int NRT, int NRN, bool PROF = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void search_kernel(SearchArgs A) {
+template <int D, int METRIC, typename E, int VIS, bool PROF = false>
+__global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
   PhaseClock<PROF> clk;
   clk.start();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int ef = static_cast<int>(A.ef), cap = static_cast<int>(A.cap);
-  const size_t top_b = HEAPS == 1 ? align16(8ull * ef) : 0, next_b = HEAPS == 1 ? align16(8ull * cap) : 0;
-  u64* top = reinterpret_cast<u64*>(smem);                     // MaxHeap top_candidates   (HEAPS = 1)
-  u64* nxt = reinterpret_cast<u64*>(smem + top_b);             // MinHeap next_candidates  (HEAPS = 1)
+  const size_t top_b = align16(8ull * ef), next_b = align16(8ull * cap);
+  u64* top = reinterpret_cast<u64*>(smem);                     // MaxHeap top_candidates
+  u64* nxt = reinterpret_cast<u64*>(smem + top_b);             // MinHeap next_candidates
   u32* vtab = reinterpret_cast<u32*>(smem + top_b + next_b);   // visited table            (VIS = 0)
   u32* sc_ids = vtab + (VIS == 0 ? A.vis_cap : 0u);            // fresh neighbours
   float* sc_d = reinterpret_cast<float*>(sc_ids + 64);
@@ -426,8 +340,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       uint4* t4 = reinterpret_cast<uint4*>(vtab);
       for (u32 i = lane; i < A.vis_cap / 4; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
     }
-    RHeap<NRT> TH;  // top_candidates  (HEAPS = 0)
-    RHeap<NRN> NH;  // next_candidates (HEAPS = 0)
 
     u32 st_dist = 0, st_vup = 0, st_vl0 = 0, st_lup = 0, st_ll0 = 0, st_maxnext = 0, status = 0;
 
@@ -482,16 +394,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     u32 logpos = 0, nvis = 1;
     bool log_overflow = false;
     if (status == 0) {
-      if constexpr (HEAPS == 0) {
-        rput(TH, 0, closest, nn);
-        rput(NH, 0, closest, nn);  // search_level :412-415
-      }
+      u64 troot = mk(closest, nn), nroot = troot;  // roots of top / next, kept in SGPRs
       if (lane == 0) {
-        if constexpr (HEAPS == 1) {
-          const u64 e0 = mk(closest, nn);
-          top[0] = e0;
-          nxt[0] = e0;
-        }
+        top[0] = troot;
+        nxt[0] = troot;  // search_level :412-415
         if (VIS == 0) {
           vtab[vhash(nn, vshift)] = nn;  // table is empty: the first probe slot is free
         } else {
@@ -509,19 +415,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       // ---- search_level(q, ef, 0) (hnsw.hh:406-476) ---------------------------------------------------------
       while (nnext > 0) {
         PHASE(2)
-        float ck, farthest0;
-        u32 cid;
-        if constexpr (HEAPS == 0) {  // next_candidates.top(); pop()  (:418-419)
-          rget(NH, 0, ck, cid);
-          farthest0 = rkey0(TH);
-          rheap_pop<false>(NH, nnext);
-        } else {
-          const u64 c = bcast64(nxt[0]);
-          ck = key(c);
-          cid = eid(c);
-          farthest0 = key(top[0]);
-          heap_pop<false>(nxt, nnext, lane);
-        }
+        const float ck = key(nroot), farthest0 = key(troot);  // next_candidates.top(); pop()  (:418-421)
+        const u32 cid = eid(nroot);
+        nroot = heap_pop<false>(nxt, nnext, lane);
         --nnext;
         if (ck > farthest0) break;  // :421-426
 
@@ -589,19 +485,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
           const float pd_l = (lane < nf && (my_d < farthest0 || ntop < ef) && my_d == my_d) ? my_d : __builtin_inff();
           const float pd = wave_min(pd_l);
           u32 pid = INV;
-          float rk0 = __builtin_inff();
-          u32 rid0 = INV;
-          if (nnext > 0) {
-            if constexpr (HEAPS == 0) {
-              rget(NH, 0, rk0, rid0);
-            } else {
-              const u64 r0 = bcast64(nxt[0]);
-              rk0 = key(r0);
-              rid0 = eid(r0);
-            }
-          }
-          if (nnext > 0 && !(pd < rk0)) {
-            pid = rid0;
+          if (nnext > 0 && !(pd < key(nroot))) {
+            pid = eid(nroot);
           } else if (pd < __builtin_inff()) {
             const u64 hit = __ballot(pd_l == pd);
             pid = __builtin_amdgcn_readlane(static_cast<int>(my_id), static_cast<int>(__builtin_ctzll(hit)));
@@ -614,29 +499,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
         PHASE(6)
         for (int j = 0; j < nf; ++j) {
           const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_d), j));
-          const float farthest = HEAPS == 0 ? rkey0(TH) : key(top[0]);
-          if (d < farthest || ntop < ef) {
+          if (d < key(troot) || ntop < ef) {
             if (nnext >= cap) { status = ST_OVERFLOW; break; }
             const u32 id = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(my_id), j));
-            if constexpr (HEAPS == 0) {
-              rheap_push<false>(NH, nnext, d, id);
-              if (ntop < ef) {  // heap.hh:34-41 push_k
-                rheap_push<true>(TH, ntop, d, id);
-                ++ntop;
-              } else {  // d < top().distance holds: it is the accept test with the top full
-                rheap_pop<true>(TH, ntop);
-                rheap_push<true>(TH, ntop - 1, d, id);
-              }
-            } else {
-              const u64 en = mk(d, id);
-              heap_push<false>(nxt, nnext, en, lane);
-              if (ntop < ef) {
-                heap_push<true>(top, ntop, en, lane);
-                ++ntop;
-              } else {
-                heap_pop<true>(top, ntop, lane);
-                heap_push<true>(top, ntop - 1, en, lane);
-              }
+            const u64 en = mk(d, id);
+            nroot = heap_push<false>(nxt, nnext, en, nroot, lane);
+            if (ntop < ef) {  // heap.hh:34-41 push_k
+              troot = heap_push<true>(top, ntop, en, troot, lane);
+              ++ntop;
+            } else {  // d < top().distance holds: it is the accept test with the top full
+              troot = heap_pop<true>(top, ntop, lane);
+              troot = heap_push<true>(top, ntop - 1, en, troot, lane);
             }
             ++nnext;
             if (static_cast<u32>(nnext) > st_maxnext) st_maxnext = nnext;
@@ -649,25 +522,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       PHASE(7)
       if (status == 0) {
         while (ntop > static_cast<int>(A.k)) {
-          if constexpr (HEAPS == 0) rheap_pop<true>(TH, ntop);
-          else heap_pop<true>(top, ntop, lane);
+          heap_pop<true>(top, ntop, lane);
           --ntop;
         }
       }
     }
 
     const u64 obase = static_cast<u64>(qi) * A.k;
-    if constexpr (HEAPS == 0) {
-#pragma unroll
-      for (int r = 0; r < NRT; ++r) {
-        const u32 i = static_cast<u32>(r * 64 + lane);
-        if (i < A.k) {
-          const bool ok = status == 0 && static_cast<int>(i) < ntop;
-          A.out_ids[obase + i] = ok ? A.g.uid[static_cast<u32>(TH.v[r])] : INV;
-          if (A.out_dists) A.out_dists[obase + i] = ok ? __int_as_float(TH.k[r]) : 0.f;
-        }
-      }
-    } else {
+    {
       for (u32 i = lane; i < A.k; i += 64) {
         u32 id = INV;
         float d = 0.f;
@@ -752,38 +614,40 @@ __global__ __launch_bounds__(64) void heap_replay_kernel(const int32_t* ops, con
   u64* h = reinterpret_cast<u64*>(smem);
   const int lane = threadIdx.x;
   int n = 0;
+  u64 root = 0;  // tracked exactly as the search kernel tracks it; checked against h[0] after every op
+  bool root_ok = true;
   for (u32 i = 0; i < n_ops; ++i) {
     const u64 e = mk(vals[i], ids[i]);
     const int op = ops[i];
     if (op == 0) {
-      heap_push<MAXH>(h, n, e, lane);
+      root = heap_push<MAXH>(h, n, e, root, lane);
       ++n;
     } else if (op == 1) {
       if (n > 0) {
-        heap_pop<MAXH>(h, n, lane);
+        root = heap_pop<MAXH>(h, n, lane);
         --n;
       }
     } else {
       if (n < static_cast<int>(k)) {
-        heap_push<MAXH>(h, n, e, lane);
+        root = heap_push<MAXH>(h, n, e, root, lane);
         ++n;
-      } else if (hcmp<MAXH>(vals[i], key(h[0]))) {
-        heap_pop<MAXH>(h, n, lane);
-        heap_push<MAXH>(h, n - 1, e, lane);
+      } else if (hcmp<MAXH>(vals[i], key(root))) {
+        root = heap_pop<MAXH>(h, n, lane);
+        root = heap_push<MAXH>(h, n - 1, e, root, lane);
       }
     }
+    if (n > 0 && bcast64(h[0]) != root) root_ok = false;
   }
   for (int i = lane; i < n; i += 64) {
     out_d[i] = key(h[i]);
     out_ids[i] = eid(h[i]);
   }
-  if (lane == 0) *out_n = static_cast<u32>(n);
+  if (lane == 0) *out_n = root_ok ? static_cast<u32>(n) : 0xFFFFFFFFu;
 }
 
 template <int D, int METRIC, typename E>
 hipError_t launch_search_t(uint32_t grid, const SearchArgs& a, hipStream_t s) {
-  const bool reg_heaps = a.heap_regs != 0;
-  const size_t lds = search_lds_bytes(reg_heaps ? 0 : a.ef, reg_heaps ? 0 : a.cap, a.vis_cap);
+  const size_t lds = search_lds_bytes(a.ef, a.cap, a.vis_cap);
   auto run = [&](auto kern) -> hipError_t {
     if (lds > 65536) {  // beyond the default dynamic-LDS limit: opt in (per device, so every launch)
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -793,21 +657,11 @@ hipError_t launch_search_t(uint32_t grid, const SearchArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, s, a);
     return hipGetLastError();
   };
-  if (reg_heaps) {
-    if (a.vis_cap == 0 || a.cap > kRegNextCap) return hipErrorInvalidValue;
-    if constexpr (D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
-      if (a.prof) {
-        if (a.ef <= 64) return run(search_kernel<D, METRIC, E, 0, 0, 1, kRegNextCap / 64, true>);
-        if (a.ef <= 128) return run(search_kernel<D, METRIC, E, 0, 0, 2, kRegNextCap / 64, true>);
-      }
-    }
-    if (a.ef <= 64) return run(search_kernel<D, METRIC, E, 0, 0, 1, kRegNextCap / 64>);
-    if (a.ef <= 128) return run(search_kernel<D, METRIC, E, 0, 0, 2, kRegNextCap / 64>);
-    if (a.ef <= 256) return run(search_kernel<D, METRIC, E, 0, 0, 4, kRegNextCap / 64>);
-    return hipErrorInvalidValue;
+  if constexpr (D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
+    if (a.prof && a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0, true>);
   }
-  if (a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0, 1, 1, 1>);
-  return run(search_kernel<D, METRIC, E, 1, 1, 1, 1>);
+  if (a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0>);
+  return run(search_kernel<D, METRIC, E, 1>);
 }
 
 template <int D, int METRIC, typename E>
