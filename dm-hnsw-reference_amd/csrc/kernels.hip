@@ -90,6 +90,7 @@ __device__ __forceinline__ u64 heap_push(u64* h, int n, u64 v, u64 root0, int la
   return fin == 0 ? v : root0;
 }
 
+// General form (any keys, NaN included): the value's landing slot is found bottom-up like std::__push_heap.
 // std::pop_heap on h[0..n) followed by pop_back  ≡  std::__adjust_heap(h, 0, n-1, h[n-1]).  Returns the new
 // root (meaningless when n <= 1).
 //
@@ -97,7 +98,7 @@ __device__ __forceinline__ u64 heap_push(u64* h, int n, u64 v, u64 root0, int la
 // 63-node window below the hole, reads both children's keys (adjacent slots: one ds_read2_b32) and votes
 // "right child wins"; the walk then follows the ballot with scalar bit tests.
 template <bool MAXH>
-__device__ __forceinline__ u64 heap_pop(u64* h, int n, int lane) {
+__device__ __forceinline__ u64 heap_pop_any(u64* h, int n, int lane) {
   if (n <= 1) return 0;
   const int len = n - 1;
   const u64 value = h[len];
@@ -151,6 +152,68 @@ __device__ __forceinline__ u64 heap_pop(u64* h, int n, int lane) {
   if (lane == 0) h[pj] = value;
   wave_sync();
   return j == 0 ? value : bcast64(ent);  // lane 0 holds the path's first node
+}
+
+// Fast form for NaN-free heaps.  Along any root-to-leaf path of a heap the keys are monotone, so the
+// comparisons std::__push_heap makes on its way back up are false on a prefix of the path and true below it:
+// every path node whose winning child the comparator does not rank past the value shifts up, the first one
+// that does marks the landing slot.  Each 6-level window costs one LDS round trip: lane i plays window node
+// i+1 (1-based), reads both children entries (adjacent slots: one ds_read2_b64) and votes for the right
+// child; the walk follows the ballot on SGPRs; the on-path lanes then shift their winner up in place.
+template <bool MAXH>
+__device__ __forceinline__ u64 heap_pop(u64* h, int n, int lane) {
+  if (n <= 1) return 0;
+  const int len = n - 1;
+  const u64 value = h[len];
+  const float vk = key(value);
+  const int lim = (len - 1) / 2;  // the hole has two children while hole < lim
+  const int j1 = lane + 1;        // window node (1-based) of this lane
+  const int lj = 31 - __clz(j1);
+  const int oj = j1 - (1 << lj);
+  int P1 = 1;  // window root, 1-based heap index
+  u64 root = value;
+  for (int round = 0;; ++round) {
+    const int a1 = (P1 << lj) + oj;  // this lane's node, 1-based
+    const int c1 = 2 * a1 - 1;       // its left child, 0-based
+    u64 le = 0, re = 0;
+    if (lane < 63 && c1 < len) {
+      le = h[c1];
+      re = h[c1 + 1];
+    }
+    const bool right = lane < 63 && c1 + 1 < len && !hcmp<MAXH>(key(re), key(le));
+    const u64 we = right ? re : le;  // the child the hole would move into
+    const u64 W = __ballot(right);
+    int P = P1, r1 = 1, steps = 0;
+    while (steps < 6 && P - 1 < lim) {
+      const int b = static_cast<int>((W >> (r1 - 1)) & 1ull);
+      r1 = 2 * r1 + b;
+      P = 2 * P + b;
+      ++steps;
+    }
+    const bool lone = (len & 1) == 0 && P - 1 == (len - 2) / 2;  // a last node with only a left child
+    bool more = steps == 6 && (P - 1 < lim || lone);
+    if (!more && lone) {
+      r1 = 2 * r1;
+      P = 2 * P;
+      ++steps;
+    }
+    const bool onp = lane < 63 && lj < steps && (r1 >> (steps - lj)) == j1;
+    const bool up = onp && !hcmp<MAXH>(key(we), vk);  // no move back down: the winner stays shifted up
+    const int k = __popcll(__ballot(up));
+    if (up) h[a1 - 1] = we;
+    if (round == 0) root = k == 0 ? value : bcast64(we);  // lane 0 is the root
+    if (k < steps) {
+      if (lane == 0) h[(P >> (steps - k)) - 1] = value;
+      break;
+    }
+    if (!more) {
+      if (lane == 0) h[P - 1] = value;
+      break;
+    }
+    P1 = P;
+  }
+  wave_sync();
+  return root;
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -395,6 +458,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
     bool log_overflow = false;
     if (status == 0) {
       u64 troot = mk(closest, nn), nroot = troot;  // roots of top / next, kept in SGPRs
+      bool nan_keys = closest != closest;            // a NaN key in either heap: general pop from now on
       if (lane == 0) {
         top[0] = troot;
         nxt[0] = troot;  // search_level :412-415
@@ -417,7 +481,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         PHASE(2)
         const float ck = key(nroot), farthest0 = key(troot);  // next_candidates.top(); pop()  (:418-421)
         const u32 cid = eid(nroot);
-        nroot = heap_pop<false>(nxt, nnext, lane);
+        nroot = nan_keys ? heap_pop_any<false>(nxt, nnext, lane) : heap_pop<false>(nxt, nnext, lane);
         --nnext;
         if (ck > farthest0) break;  // :421-426
 
@@ -477,6 +541,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         // lane j < nf holds fresh neighbour j (list order)
         const float my_d = lane < nf ? sc_d[lane] : __builtin_inff();
         const u32 my_id = lane < nf ? sc_ids[lane] : INV;
+        if (__ballot(my_d != my_d)) nan_keys = true;
 
         // Speculative prefetch of the adjacency row of the candidate expected on top of next_candidates once
         // this step's pushes are done: a min-heap root changes only for a strictly smaller key, so the root
@@ -508,7 +573,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
               troot = heap_push<true>(top, ntop, en, troot, lane);
               ++ntop;
             } else {  // d < top().distance holds: it is the accept test with the top full
-              troot = heap_pop<true>(top, ntop, lane);
+              troot = nan_keys ? heap_pop_any<true>(top, ntop, lane) : heap_pop<true>(top, ntop, lane);
               troot = heap_push<true>(top, ntop - 1, en, troot, lane);
             }
             ++nnext;
@@ -522,7 +587,8 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
       PHASE(7)
       if (status == 0) {
         while (ntop > static_cast<int>(A.k)) {
-          heap_pop<true>(top, ntop, lane);
+          if (nan_keys) heap_pop_any<true>(top, ntop, lane);
+          else heap_pop<true>(top, ntop, lane);
           --ntop;
         }
       }
@@ -613,6 +679,8 @@ __global__ __launch_bounds__(64) void heap_replay_kernel(const int32_t* ops, con
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   u64* h = reinterpret_cast<u64*>(smem);
   const int lane = threadIdx.x;
+  const bool any = (k & 0x80000000u) != 0;  // exercise the general pop instead of the fast one
+  k &= 0x7FFFFFFFu;
   int n = 0;
   u64 root = 0;  // tracked exactly as the search kernel tracks it; checked against h[0] after every op
   bool root_ok = true;
@@ -624,7 +692,7 @@ __global__ __launch_bounds__(64) void heap_replay_kernel(const int32_t* ops, con
       ++n;
     } else if (op == 1) {
       if (n > 0) {
-        root = heap_pop<MAXH>(h, n, lane);
+        root = any ? heap_pop_any<MAXH>(h, n, lane) : heap_pop<MAXH>(h, n, lane);
         --n;
       }
     } else {
@@ -632,7 +700,7 @@ __global__ __launch_bounds__(64) void heap_replay_kernel(const int32_t* ops, con
         root = heap_push<MAXH>(h, n, e, root, lane);
         ++n;
       } else if (hcmp<MAXH>(vals[i], key(root))) {
-        root = heap_pop<MAXH>(h, n, lane);
+        root = any ? heap_pop_any<MAXH>(h, n, lane) : heap_pop<MAXH>(h, n, lane);
         root = heap_push<MAXH>(h, n - 1, e, root, lane);
       }
     }

@@ -194,9 +194,10 @@ def _heap_ops(rng, n_ops, ties):
     return ops, vals, ids
 
 
+@pytest.mark.parametrize("general", [False, True])
 @pytest.mark.parametrize("is_max", [True, False])
 @pytest.mark.parametrize("ties", [True, False])
-def test_device_heaps_match_libstdcxx(is_max, ties, gpu_available):
+def test_device_heaps_match_libstdcxx(is_max, ties, general, gpu_available):
     """The wave-parallel push/pop the kernel uses must leave the exact heap array libstdc++ leaves."""
     import ctypes as C
     L = shine_amd._lib
@@ -208,7 +209,8 @@ def test_device_heaps_match_libstdcxx(is_max, ties, gpu_available):
         oi = np.empty(n_ops + 1, np.uint32)
         on = np.zeros(1, np.uint32)
         p = lambda a: a.ctypes.data_as(C.c_void_p)
-        L.check(L.lib().shine_selftest_heap(int(is_max), p(ops), p(vals), p(ids), n_ops, k, p(od), p(oi), p(on)))
+        kk = k | (0x80000000 if general else 0)  # high bit: the general (NaN-safe) pop
+        L.check(L.lib().shine_selftest_heap(int(is_max), p(ops), p(vals), p(ids), n_ops, kk, p(od), p(oi), p(on)))
         n = int(on[0])
         assert n == ref_d.size, (n_ops, k)
         np.testing.assert_array_equal(oi[:n], ref_i)
@@ -231,3 +233,19 @@ def test_visited_modes(env, gpu_available, monkeypatch):
             assert r.stats["overflow_retries"] > 0
         _check_same(r, *ref)
         _check_same(idx.knn(q, 10, 200), *ref)
+
+
+def test_nan_distances_follow_reference(gpu_available):
+    """NaN components give NaN distances: comparisons with NaN are false in the reference too, so the search
+    still has one exact outcome; the kernel switches to its general heap routine and must reproduce it."""
+    base = D.sift_like(3000, seed=81)
+    base[::97, 5] = np.nan
+    q = D.sift_like(64, seed=82)
+    q[3, 7] = np.nan
+    dumps, _, _ = O.build(base, 8, 40, 0, 1, seed=2)
+    ref = O.OracleIndex(dumps, 128, 8, 0).knn(q, 10, 48)
+    with shine_amd.Index.from_buffers(dumps, 128, 8, 0, gpus=[0]) as idx:
+        r = idx.knn(q, 10, 48)
+    np.testing.assert_array_equal(r.ids, ref[0])
+    np.testing.assert_array_equal(r.dists.view(np.uint32), ref[1].view(np.uint32))
+    np.testing.assert_array_equal(r.qstats[:, :5], ref[2][:, :5])
