@@ -83,7 +83,7 @@ def main():
     import shine_amd
     from shine_amd import datasets as D
 
-    key = hashlib.sha1(f"{a.n}-{a.dim}-{a.M}-{a.efc}-{a.shards}-sift_like-v2".encode()).hexdigest()[:12]
+    key = hashlib.sha1(f"{a.n}-{a.dim}-{a.M}-{a.efc}-{a.shards}-sift_like-v3".encode()).hexdigest()[:12]
     cache = Path(a.cache) / key
     t0 = time.time()
     base = D.sift_like(a.n, seed=1, d=a.dim)

@@ -59,6 +59,7 @@ def sift_like(n: int, seed: int = 1, d: int = 128) -> np.ndarray:
                         _SIFT["cs"])
     x = np.rint(x * np.float32(40.0 / _sift_std[d]) + np.float32(50.0))
     np.clip(x, 0.0, 255.0, out=x)
+    x += np.float32(0.0)  # -0.0 → +0.0, so the vectors survive a u8 round trip bit for bit
     return x.astype(np.float32)
 
 
