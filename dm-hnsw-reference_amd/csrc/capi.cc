@@ -250,8 +250,8 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   if (int rc = R.ovf.grow(2ull * nq)) return rc;
   HIP_TRY(hipMemsetAsync(R.counter.p, 0, 8 * sizeof(uint32_t), s));  // 3 queue heads + 2 list counts
   if (env_int("SHINE_PHASE_PROFILE", 0)) {
-    if (int rc = R.prof.grow(8)) return rc;
-    HIP_TRY(hipMemsetAsync(R.prof.p, 0, 8 * sizeof(unsigned long long), s));
+    if (int rc = R.prof.grow(24)) return rc;
+    HIP_TRY(hipMemsetAsync(R.prof.p, 0, 24 * sizeof(unsigned long long), s));
   }
   if (timed) HIP_TRY(hipEventRecord(R.ev0, s));
   const int start = static_cast<int>(env_int("SHINE_DEBUG_START_MODE", 0));  // test hook: exercise modes 1, 2
@@ -282,7 +282,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
       a.in_count = R.counter.p + 3 + (mode - 1);
     }
     if (mode == 0 && env_int("SHINE_PHASE_PROFILE", 0)) {
-      if (int rc = R.prof.grow(8)) return rc;
+      if (int rc = R.prof.grow(24)) return rc;
       a.prof = R.prof.p;
     }
     if (mode < 2) {
@@ -431,11 +431,14 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
     HIP_TRY(hipEventElapsedTime(&ms, R.ev0, R.ev1));
     kernel_ms = std::max(kernel_ms, static_cast<double>(ms));
     if (env_int("SHINE_PHASE_PROFILE", 0) && R.prof.p) {
-      unsigned long long ph[8];
+      unsigned long long ph[24];
       HIP_TRY(hipMemcpy(ph, R.prof.p, sizeof(ph), hipMemcpyDeviceToHost));
+      std::fprintf(stderr, "SHINE_PHASE_PROFILE entries:");
+      for (int i = 12; i < 24; ++i) std::fprintf(stderr, " %llu", ph[i]);
+      std::fprintf(stderr, "\n");
       std::fprintf(stderr, "SHINE_PHASE_PROFILE cycles: setup %llu greedy %llu pop %llu adj+visited %llu dist %llu "
-                           "predict %llu accept %llu trim+out %llu\n",
-                   ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6], ph[7]);
+                           "predict %llu accept-loop %llu out %llu next-push %llu top-pop %llu top-push %llu trim %llu\n",
+                   ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6], ph[7], ph[8], ph[9], ph[10], ph[11]);
     }
     uint32_t ovf_counts[2] = {0, 0};  // queries handed to the fixup passes
     HIP_TRY(hipMemcpy(ovf_counts, R.counter.p + 3, sizeof(ovf_counts), hipMemcpyDeviceToHost));

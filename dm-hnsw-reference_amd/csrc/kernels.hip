@@ -345,7 +345,8 @@ struct PhaseClock {  // empty unless PROF
 };
 template <>
 struct PhaseClock<true> {
-  u64 ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  u64 ph[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  u32 cnt[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // entries into each phase
   u64 t_last = 0;
   int cur = 0;
   __device__ void start() { t_last = stamp(); }
@@ -354,15 +355,20 @@ struct PhaseClock<true> {
     const u64 t = stamp();
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
+    for (int j = 0; j < 12; ++j) {
       if (j == cur) ph[j] += t - t_last;
+      if (j == i) ++cnt[j];
+    }
     t_last = t;
     cur = i;
   }
   __device__ void flush(unsigned long long* out, int lane) {
     mark(0);
     if (lane == 0 && out)
-      for (int j = 0; j < 8; ++j) atomicAdd(&out[j], static_cast<unsigned long long>(ph[j]));
+      for (int j = 0; j < 12; ++j) {
+        atomicAdd(&out[j], static_cast<unsigned long long>(ph[j]));
+        atomicAdd(&out[12 + j], static_cast<unsigned long long>(cnt[j]));
+      }
   }
 };
 #define PHASE(i) clk.mark(i);
@@ -568,14 +574,19 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
             if (nnext >= cap) { status = ST_OVERFLOW; break; }
             const u32 id = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(my_id), j));
             const u64 en = mk(d, id);
+            PHASE(8)
             nroot = heap_push<false>(nxt, nnext, en, nroot, lane);
             if (ntop < ef) {  // heap.hh:34-41 push_k
+              PHASE(10)
               troot = heap_push<true>(top, ntop, en, troot, lane);
               ++ntop;
             } else {  // d < top().distance holds: it is the accept test with the top full
+              PHASE(9)
               troot = nan_keys ? heap_pop_any<true>(top, ntop, lane) : heap_pop<true>(top, ntop, lane);
+              PHASE(10)
               troot = heap_push<true>(top, ntop - 1, en, troot, lane);
             }
+            PHASE(6)
             ++nnext;
             if (static_cast<u32>(nnext) > st_maxnext) st_maxnext = nnext;
           }
@@ -586,6 +597,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
       // ---- trim to k and emit in heap-array order (:296-303) ------------------------------------------------
       PHASE(7)
       if (status == 0) {
+        PHASE(11)
         while (ntop > static_cast<int>(A.k)) {
           if (nan_keys) heap_pop_any<true>(top, ntop, lane);
           else heap_pop<true>(top, ntop, lane);

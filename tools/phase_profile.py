@@ -33,4 +33,4 @@ print("plain kernel_ms", r.stats["kernel_ms"], file=sys.stderr)
 os.environ["SHINE_PHASE_PROFILE"] = "1"
 r = idx.knn(q, 10, ef)
 print("profiled kernel_ms", r.stats["kernel_ms"], "mean distcomps", r.qstats[:, 0].mean(), "mean L0 lists",
-      r.qstats[:, 4].mean(), file=sys.stderr)
+      r.qstats[:, 4].mean(), "mean max next", r.qstats[:, 5].mean(), file=sys.stderr)
