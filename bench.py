@@ -64,6 +64,8 @@ def parse():
     p.add_argument("--shards", type=int, default=1, help="memory-node dumps the index is spread over")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of the CPU-baseline sample")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--mode", choices=["fast", "exact", "both"], default="both",
+                   help="search mode(s); the first one measured gives `value` (fast, then exact with 'both')")
     p.add_argument("--cache", default=os.environ.get("SHINE_BENCH_CACHE", "/tmp/shine_bench"))
     p.add_argument("--pmc-json", default=None, help="per-launch HBM bytes measured by rocprofv3 --pmc (tools/pmc.py)")
     return p.parse_args()
@@ -128,15 +130,6 @@ def main():
         if rec is not None:
             rec[1].record(stream)
 
-    # one validation pass over every batch: status, recall, algorithmic bytes
-    for i in range(a.nbatches):
-        step(i)
-    torch.cuda.synchronize()
-    qs_h = qs.cpu().numpy().view(np.uint32).reshape(-1, 8)
-    n_bad = int((qs_h[:, 6] != 0).sum())
-    if n_bad:
-        raise SystemExit(f"{n_bad} queries did not complete (status {np.unique(qs_h[:, 6])})")
-    bq_batch = [idx.algorithmic_bytes(qs_h[b * a.batch:(b + 1) * a.batch]) for b in range(a.nbatches)]
     # ground truth on the GPU (exact: integer-valued data keep every f32 partial sum < 2^24)
     bt = torch.from_numpy(base).cuda()
     bn = (bt * bt).sum(1)
@@ -147,34 +140,63 @@ def main():
         gt.append(torch.topk(dd, a.k, largest=False).indices.cpu().numpy())
     del bt, bn
     gt = np.concatenate(gt)
-    res = ids.cpu().numpy().view(np.uint32).reshape(-1, a.k)
-    recall = D.recall_at_k(res, gt, a.k)
-    log(f"rank {rank}: recall@{a.k} = {recall:.4f} over {nq_rank} queries; mean distcomps "
-        f"{qs_h[:, 0].mean():.0f}, lists L0 {qs_h[:, 4].mean():.1f}")
 
-    for i in range(a.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(a.warmup + i, evs[i])
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if dist:
-        dist.barrier()
-    elapsed = t1 - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    kern_ms = [s.elapsed_time(e) for s, e in evs]
-    bytes_steps = [bq_batch[(a.warmup + i) % a.nbatches] for i in range(a.steps)]
+    def run_mode(mode):
+        """Validation pass over every batch (status, recall, algorithmic bytes), warmup, then exactly K timed
+        steps between barriers; returns the measurements."""
+        idx.set_search_mode(mode)
+        for i in range(a.nbatches):
+            step(i)
+        torch.cuda.synchronize()
+        qs_h = qs.cpu().numpy().view(np.uint32).reshape(-1, 8).copy()
+        n_bad = int((qs_h[:, 6] != 0).sum())
+        if n_bad:
+            raise SystemExit(f"{n_bad} queries did not complete (status {np.unique(qs_h[:, 6])})")
+        bq_batch = [idx.algorithmic_bytes(qs_h[b * a.batch:(b + 1) * a.batch]) for b in range(a.nbatches)]
+        res = ids.cpu().numpy().view(np.uint32).reshape(-1, a.k).copy()
+        recall = D.recall_at_k(res, gt, a.k)
+        log(f"rank {rank}: mode {mode}: recall@{a.k} = {recall:.4f} over {nq_rank} queries; mean distcomps "
+            f"{qs_h[:, 0].mean():.0f}, lists L0 {qs_h[:, 4].mean():.1f}")
+        for i in range(a.warmup):
+            step(i)
+        torch.cuda.synchronize()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            step(a.warmup + i, evs[i])
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if dist:
+            dist.barrier()
+        elapsed = t1 - t0
+        if dist:
+            t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        kern_ms = [s.elapsed_time(e) for s, e in evs]
+        bytes_steps = [bq_batch[(a.warmup + i) % a.nbatches] for i in range(a.steps)]
+        return dict(elapsed=elapsed, kern_ms=kern_ms, bytes_steps=bytes_steps, recall=recall, qs=qs_h, ids=res)
+
+    modes = ["fast", "exact"] if a.mode == "both" else [a.mode]
+    runs = {m: run_mode(shine_amd.MODE_FAST if m == "fast" else shine_amd.MODE_EXACT) for m in modes}
+    head = runs[modes[0]]
+    elapsed, kern_ms, bytes_steps, recall, qs_h = (head[x] for x in ("elapsed", "kern_ms", "bytes_steps", "recall", "qs"))
     achieved = sum(bytes_steps) / (sum(kern_ms) / 1e3) / 1e9  # GB/s
     avg_launch_ms = float(np.mean(kern_ms))
+    mode_report = {}
+    for m, r in runs.items():
+        mode_report[m] = {"value": a.steps * a.batch * world / r["elapsed"], "ms_per_step": r["elapsed"] * 1e3 / a.steps,
+                          "avg_launch_ms": float(np.mean(r["kern_ms"])), "recall_at_10": r["recall"]}
+        if m == "fast":
+            mode_report[m]["queries_with_ties"] = float((r["qs"][:, 5] > 0).mean())
+    if "fast" in runs and "exact" in runs:
+        same = (np.sort(runs["fast"]["ids"], 1) == np.sort(runs["exact"]["ids"], 1)).all(1)
+        mode_report["fast"]["same_ids_as_exact"] = float(same.mean())
+        clean = runs["fast"]["qs"][:, 5] == 0
+        mode_report["fast"]["tie_free_same_ids_as_exact"] = float(same[clean].mean()) if clean.any() else None
 
     traffic = None
     if a.pmc_json and Path(a.pmc_json).exists():
@@ -200,12 +222,15 @@ def main():
             "dtype": "f32",
             "data": "synthetic SIFT-shaped (integer-valued f32, 1M x 128), random-seeded; index built in-run",
             "recall_at_10": recall,
+            "search_mode": modes[0],
+            "modes": mode_report,
             "config": {"workload": "SIFT1M-shaped L2 knn, M=16 efC=200 ef=128 k=10", "n": a.n, "dim": a.dim,
                        "global_batch": a.batch * world, "batch_per_gpu": a.batch, "M": a.M, "efc": a.efc,
                        "ef": a.ef, "k": a.k, "shards": a.shards, "parallelism": f"replica{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                         "kernel": "search_kernel<128,L2,f32>", "avg_launch_ms": avg_launch_ms,
+                         "kernel": ("search_fast_kernel<128,L2,f32,2>" if modes[0] == "fast"
+                                    else "search_kernel<128,L2,f32,0>"), "avg_launch_ms": avg_launch_ms,
                          "algorithmic_bytes_per_launch": float(np.mean(bytes_steps)),
                          "mean_distcomps_per_query": float(qs_h[:, 0].mean())},
             "cpu_baseline": cpu,

@@ -85,6 +85,7 @@ struct shine_index {
   uint32_t inv_size = 0;
   uint64_t words_per_slot = 0;
   uint64_t device_bytes = 0;
+  int search_mode = SHINE_MODE_EXACT;
   std::vector<Replica> reps;
   std::mutex mu;
 };
@@ -207,6 +208,20 @@ int64_t env_int(const char* name, int64_t dflt) {
 // mode 0: one wavefront per query up to 16 per CU; top / next / visited table in the wave's LDS share.
 // mode 1: one wavefront per CU with the whole 160 KiB: 16K-entry visited table, larger next queue (fixup).
 // mode 2: one wavefront per CU, visited bitmap in HBM, next queue takes the LDS (fixup).
+// fast (mode 0 of SHINE_MODE_FAST): the sorted list lives in VGPRs, LDS holds only the visited table.
+LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef) {
+  LaunchShape sh{};
+  sh.vis_cap = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(48 * ef)));
+  sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
+  const uint64_t need = search_fast_lds_bytes(sh.vis_cap);
+  const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(kLdsPerCu / need));
+  const uint32_t wpc = std::max<uint32_t>(1, std::min<uint32_t>({(nq + kCus - 1) / kCus, 16u, fit}));
+  sh.cap = 0;
+  sh.vis_limit = sh.vis_cap / 8 * 7;
+  sh.grid = std::max<uint32_t>(1, std::min<uint32_t>(nq, kCus * wpc));
+  return sh;
+}
+
 LaunchShape pick_shape(uint32_t nq, uint32_t ef, int mode) {
   LaunchShape sh{};
   const uint64_t top_bytes = align16(8ull * ef);
@@ -255,8 +270,10 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   }
   if (timed) HIP_TRY(hipEventRecord(R.ev0, s));
   const int start = static_cast<int>(env_int("SHINE_DEBUG_START_MODE", 0));  // test hook: exercise modes 1, 2
+  const bool fast_mode = h->search_mode == SHINE_MODE_FAST;
   for (int mode = start; mode <= 2; ++mode) {
-    const LaunchShape sh = pick_shape(nq, ef, mode);
+    const bool fast = fast_mode && mode == 0 && ef <= kFastMaxEf;
+    const LaunchShape sh = fast ? pick_fast_shape(nq, ef) : pick_shape(nq, ef, mode);
     if (mode == 2) {
       if (int rc = ensure_bitmaps(h, R, sh.grid)) return rc;
     }
@@ -277,6 +294,8 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     a.vlog = R.vlog.p;
     a.log_cap = kLogCap;
     a.counter = R.counter.p + mode;
+    a.fast = fast ? 1u : 0u;
+    a.sort_out = fast_mode ? 1u : 0u;
     if (mode > start) {
       a.in_list = R.ovf.p + static_cast<size_t>(mode - 1) * nq;
       a.in_count = R.counter.p + 3 + (mode - 1);
@@ -344,6 +363,16 @@ int shine_open(const char* const* dump_paths, uint32_t n_dumps, uint32_t dim, ui
     sizes[i] = files[i].size();
   }
   return shine_open_buffers(ptrs.data(), sizes.data(), n_dumps, dim, M, metric, elem, gpu_ids, n_gpus, out);
+}
+
+int shine_set_search_mode(shine_index_t h, int mode) {
+  if (!h) return set_error(SHINE_ERR_ARG, "index handle is NULL");
+  if (mode != SHINE_MODE_EXACT && mode != SHINE_MODE_FAST) return set_error(SHINE_ERR_ARG, "unknown search mode");
+  if (mode == SHINE_MODE_FAST && h->N >= 0x80000000ull)
+    return set_error(SHINE_ERR_ARG, "fast mode needs fewer than 2^31 nodes per GPU");
+  std::lock_guard<std::mutex> lk(h->mu);
+  h->search_mode = mode;
+  return SHINE_OK;
 }
 
 int shine_index_get_info(shine_index_t h, shine_index_info* o) {

@@ -38,6 +38,8 @@ struct SearchArgs {
   uint32_t* out_list;        // queries that overflow here are appended for the next pass (nullable)
   uint32_t* out_count;
   unsigned long long* prof; // diagnostics (nullable): per-phase shader-clock totals, PROF kernel variant only
+  uint32_t fast;            // 1: sorted-list kernel (SHINE_MODE_FAST; ef <= 256, vis_cap > 0)
+  uint32_t sort_out;        // heap kernel writes ascending order (fast-mode fixup passes)
 };
 
 struct DistArgs {
@@ -54,6 +56,10 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(
 inline size_t search_lds_bytes(uint32_t ef, uint32_t cap, uint32_t vis_cap) {
   return align16(8ull * ef) + align16(8ull * cap) + 4ull * vis_cap + 64 * 4 * 2;
 }
+
+// LDS of the fast kernel: visited table[vis_cap] | scratch ids[64], dists[64]
+inline size_t search_fast_lds_bytes(uint32_t vis_cap) { return 4ull * vis_cap + 64 * 4 * 2; }
+constexpr uint32_t kFastMaxEf = 256;
 
 bool dim_supported(uint32_t dim, int elem);
 

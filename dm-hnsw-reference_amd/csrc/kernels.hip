@@ -328,6 +328,64 @@ __device__ __forceinline__ float wave_min(float v) {
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// Entry point + greedy descent, shared by both search kernels: HNSW::knn's EP read and distance
+// (hnsw.hh:256-272) and search_for_one over levels ep_level..1 (hnsw.hh:331-393).  Counters: distcomps,
+// visited_nodes (upper / L0 for the EP), visited_neighborlists (upper).  status = ST_FORMAT on a broken index.
+// ------------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ u32 sortable(float f) {  // order-preserving u32 image of a float (total order)
+  const u32 b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+template <int D, int METRIC, typename E>
+__device__ __forceinline__ void entry_and_descent(const SearchArgs& A, const E* __restrict__ vec,
+                                                  const QueryRegs<D>& Q, u32* sc_ids, float* sc_d, int lane,
+                                                  u32& nn, float& closest, u32& st_dist, u32& st_vup, u32& st_vl0,
+                                                  u32& st_lup, u32& status) {
+  const u32 ep = A.g.ep;
+  if (lane == 0) sc_ids[0] = ep;
+  wave_sync();
+  dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, 1, lane);
+  wave_sync();
+  closest = sc_d[0];
+  ++st_dist;
+  if (A.g.ep_level > 0) ++st_vup; else ++st_vl0;
+  nn = ep;
+  const u32 MU = A.g.MU;
+  for (u32 level = A.g.ep_level; level > 0 && status == 0; --level) {
+    bool changed;
+    do {
+      changed = false;
+      const u32 ub = A.g.up_base[nn];
+      if (ub == INV) { status = ST_FORMAT; break; }
+      const u32* row = A.g.adjU + (static_cast<u64>(ub) + level - 1) * MU;
+      u32 e = INV;
+      if (static_cast<u32>(lane) < MU) e = row[lane];
+      const bool valid = e != INV;
+      const int cnt = __popcll(__ballot(valid));
+      ++st_lup;
+      st_vup += cnt;
+      st_dist += cnt;
+      if (valid) sc_ids[lane] = e;
+      wave_sync();
+      dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, cnt, lane);
+      wave_sync();
+      // first neighbour (list order) attaining the minimum; adopted only if strictly closer (:378)
+      float bd = (lane < cnt) ? sc_d[lane] : __builtin_inff();
+      if (bd != bd) bd = __builtin_inff();  // NaN never compares less
+      const float mn = wave_min(bd);
+      if (mn < closest) {
+        const int bi = static_cast<int>(__builtin_ctzll(__ballot(bd == mn)));
+        closest = mn;
+        nn = sc_ids[bi];
+        changed = true;
+      }
+      wave_sync();
+    } while (changed);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // search kernel: one wavefront (= one workgroup) per persistent slot
 //   VIS   0: visited table in LDS, 1: visited bitmap in HBM
 // ------------------------------------------------------------------------------------------------------------
@@ -388,7 +446,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
 
   const int lane = threadIdx.x;
   const E* __restrict__ vec = static_cast<const E*>(A.g.vec);
-  const u32 M0 = A.g.M0, MU = A.g.MU;
+  const u32 M0 = A.g.M0;
   const u32 vmask = A.vis_cap - 1, vshift = 32 - (31 - __clz(static_cast<int>(A.vis_cap > 1 ? A.vis_cap : 2)));
   u32* __restrict__ vis = A.visited + (VIS == 1 ? static_cast<u64>(blockIdx.x) * A.words_per_slot : 0ull);
   u32* __restrict__ vlog = A.vlog + (VIS == 1 ? static_cast<u64>(blockIdx.x) * A.log_cap : 0ull);
@@ -412,50 +470,11 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
 
     u32 st_dist = 0, st_vup = 0, st_vl0 = 0, st_lup = 0, st_ll0 = 0, st_maxnext = 0, status = 0;
 
-    // ---- entry point (hnsw.hh:256-272) -------------------------------------------------------------------
-    const u32 ep = A.g.ep;
-    if (lane == 0) sc_ids[0] = ep;
-    wave_sync();
-    dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, 1, lane);
-    wave_sync();
-    float closest = sc_d[0];
-    ++st_dist;
-    if (A.g.ep_level > 0) ++st_vup; else ++st_vl0;
-
-    // ---- greedy descent search_for_one (hnsw.hh:331-393) ------------------------------------------------
+    // ---- entry point + greedy descent (hnsw.hh:256-287) ---------------------------------------------------
     PHASE(1)
-    u32 nn = ep;
-    for (u32 level = A.g.ep_level; level > 0 && status == 0; --level) {
-      bool changed;
-      do {
-        changed = false;
-        const u32 ub = A.g.up_base[nn];
-        if (ub == INV) { status = ST_FORMAT; break; }
-        const u32* row = A.g.adjU + (static_cast<u64>(ub) + level - 1) * MU;
-        u32 e = INV;
-        if (static_cast<u32>(lane) < MU) e = row[lane];
-        const bool valid = e != INV;
-        const int cnt = __popcll(__ballot(valid));
-        ++st_lup;
-        st_vup += cnt;
-        st_dist += cnt;
-        if (valid) sc_ids[lane] = e;
-        wave_sync();
-        dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, cnt, lane);
-        wave_sync();
-        // first neighbour (list order) attaining the minimum; adopted only if strictly closer (:378)
-        float bd = (lane < cnt) ? sc_d[lane] : __builtin_inff();
-        if (bd != bd) bd = __builtin_inff();  // NaN never compares less
-        const float mn = wave_min(bd);
-        if (mn < closest) {
-          const int bi = static_cast<int>(__builtin_ctzll(__ballot(bd == mn)));
-          closest = mn;
-          nn = sc_ids[bi];
-          changed = true;
-        }
-        wave_sync();
-      } while (changed);
-    }
+    u32 nn;
+    float closest;
+    entry_and_descent<D, METRIC, E>(A, vec, Q, sc_ids, sc_d, lane, nn, closest, st_dist, st_vup, st_vl0, st_lup, status);
 
     // ---- top_candidates.push({nn, dist(q, nn)}) (hnsw.hh:285-286) ---------------------------------------
     ++st_dist;
@@ -607,18 +626,25 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
     }
 
     const u64 obase = static_cast<u64>(qi) * A.k;
-    {
-      for (u32 i = lane; i < A.k; i += 64) {
-        u32 id = INV;
-        float d = 0.f;
-        if (status == 0 && static_cast<int>(i) < ntop) {
-          const u64 en = top[i];
-          id = A.g.uid[eid(en)];
-          d = key(en);
+    for (u32 i = lane; i < A.k; i += 64) {
+      u32 id = INV;
+      float d = 0.f;
+      u32 slot = i;
+      if (status == 0 && static_cast<int>(i) < ntop) {
+        const u64 en = top[i];
+        id = A.g.uid[eid(en)];
+        d = key(en);
+        if (A.sort_out) {  // fast-mode fixup pass: ascending order (ties by heap position)
+          const u32 si = sortable(d);
+          slot = 0;
+          for (int j = 0; j < ntop; ++j) {
+            const u32 sj = sortable(key(top[j]));
+            slot += (sj < si || (sj == si && static_cast<u32>(j) < i)) ? 1u : 0u;
+          }
         }
-        A.out_ids[obase + i] = id;
-        if (A.out_dists) A.out_dists[obase + i] = d;
       }
+      A.out_ids[obase + slot] = id;
+      if (A.out_dists) A.out_dists[obase + slot] = d;
     }
     if (status == ST_OVERFLOW && A.out_list && lane == 0) A.out_list[atomicAdd(A.out_count, 1u)] = qi;
     if (A.qstats && lane == 0) {
@@ -628,7 +654,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
       qs[2] = st_vl0;
       qs[3] = st_lup;
       qs[4] = st_ll0;
-      qs[5] = st_maxnext;
+      qs[5] = A.sort_out ? 0u : st_maxnext;  // fast-mode fixup: exact, so no tie can have changed the set
       qs[6] = status;
       qs[7] = status == 0 ? static_cast<u32>(ntop < static_cast<int>(A.k) ? ntop : A.k) : 0u;
     }
@@ -647,6 +673,232 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
     }
   }
   clk.flush(A.prof, lane);
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Fast search kernel (SHINE_MODE_FAST).  The same traversal with a different candidate structure: one sorted
+// list of the best ef candidates (key, id, expanded bit) held in VGPRs — position p in lane p % 64 of register
+// p / 64 — instead of the two std::vector heaps.
+//
+// Equivalence: every entry pushed onto next_candidates is also pushed onto top_candidates (hnsw.hh:461-465), and
+// with pairwise distinct distances an entry evicted from top has a key above every later farthest distance, so
+// it is never expanded.  next_candidates' minimum is therefore the smallest unexpanded top entry, and the loop
+// ends when none is left (the break at :424).  One expansion's accept / push / push_k sequence leaves top equal to
+// the ef smallest of (top ∪ fresh).  Hence, when no two keys compare equal where the reference's tie-breaking
+// could decide, this kernel expands the same nodes in the same order and returns the same ids, distances and
+// counters; it counts the equal-key events it meets (qstats word 5) so a caller can tell.  Results are written
+// in ascending distance order.  Costs: an insertion is two ballots per register plus one DPP wave_shr per
+// register (no LDS), the next candidate is one ballot per register.
+// ------------------------------------------------------------------------------------------------------------
+constexpr u32 EXPANDED = 0x80000000u;  // id bit: this candidate has been expanded (ids < 2^31)
+
+__device__ __forceinline__ float dpp_shr1(float v, float fill) {  // lane l <- lane l-1, lane 0 <- fill
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(fill), __float_as_int(v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ u32 dpp_shr1(u32 v, u32 fill) {
+  return static_cast<u32>(__builtin_amdgcn_update_dpp(static_cast<int>(fill), static_cast<int>(v), 0x138, 0xF, 0xF, false));
+}
+
+template <int D, int METRIC, typename E, int R>
+__global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  u32* vtab = reinterpret_cast<u32*>(smem);  // visited table
+  u32* sc_ids = vtab + A.vis_cap;             // fresh neighbours
+  float* sc_d = reinterpret_cast<float*>(sc_ids + 64);
+  const int lane = threadIdx.x;
+  const E* __restrict__ vec = static_cast<const E*>(A.g.vec);
+  const u32 M0 = A.g.M0;
+  const int ef = static_cast<int>(A.ef);
+  const u32 vmask = A.vis_cap - 1, vshift = 32 - (31 - __clz(static_cast<int>(A.vis_cap)));
+  const u64 below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const float INF = __builtin_inff();
+
+  const u32 n_items = A.in_count ? *A.in_count : A.nq;
+  for (;;) {
+    u32 item = 0;
+    if (lane == 0) item = atomicAdd(A.counter, 1u);
+    item = bcast(item);
+    if (item >= n_items) break;
+    const u32 qi = A.in_list ? A.in_list[item] : item;
+
+    QueryRegs<D> Q;
+    load_query<D>(A.queries + static_cast<u64>(qi) * D, lane, Q);
+    {
+      uint4* t4 = reinterpret_cast<uint4*>(vtab);
+      for (u32 i = lane; i < A.vis_cap / 4; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
+    }
+    u32 st_dist = 0, st_vup = 0, st_vl0 = 0, st_lup = 0, st_ll0 = 0, ties = 0, status = 0;
+    u32 nn;
+    float closest;
+    entry_and_descent<D, METRIC, E>(A, vec, Q, sc_ids, sc_d, lane, nn, closest, st_dist, st_vup, st_vl0, st_lup, status);
+    ++st_dist;  // top_candidates.push({nn, dist(q, nn)}) (hnsw.hh:285-286)
+
+    float ck[R];  // candidate keys, ascending; +inf beyond the size
+    u32 ci[R];    // candidate ids | EXPANDED; INV beyond the size
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      ck[r] = INF;
+      ci[r] = INV;
+    }
+    int cs = 0;
+    if (status == 0) {
+      ck[0] = lane == 0 ? closest : INF;
+      ci[0] = lane == 0 ? nn : INV;
+      cs = 1;
+      if (closest != closest) ++ties;
+      if (lane == 0) vtab[vhash(nn, vshift)] = nn;
+      wave_sync();
+    }
+    u32 nvis = 1;
+    u32 pre_id = INV, pre_e = INV;
+    float cmax = INF;  // key at position ef - 1 once the list is full
+
+    while (status == 0) {
+      // smallest unexpanded candidate = next_candidates.top() (:418)
+      int p = -1;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const u64 m = __ballot(ci[r] != INV && (ci[r] & EXPANDED) == 0);
+        if (p < 0 && m) p = 64 * r + static_cast<int>(__builtin_ctzll(m));
+      }
+      if (p < 0) break;  // every candidate within the radius expanded: the break at :424
+      u32 cid = 0;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if ((p >> 6) == r) {
+          cid = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(ci[r]), p & 63));
+          ci[r] = lane == (p & 63) ? (ci[r] | EXPANDED) : ci[r];
+        }
+
+      ++st_ll0;  // read_neighborlist (:436-438)
+      u32 e = INV;
+      if (cid == pre_id) e = pre_e;
+      else if (static_cast<u32>(lane) < M0) e = A.g.adj0[static_cast<u64>(cid) * M0 + lane];
+      bool cand = e != INV;
+      if (!A.g.lists_unique) {
+        for (u32 j = 0; j < M0; ++j) {
+          const u32 ej = __shfl(e, static_cast<int>(j));
+          if (j < static_cast<u32>(lane) && ej == e) cand = false;
+        }
+      }
+      bool fresh = false;
+      if (cand) {  // visited.contains / insert (:441-443)
+        u32 h = vhash(e, vshift);
+        for (;;) {
+          const u32 old = atomicCAS(&vtab[h], INV, e);
+          if (old == INV) { fresh = true; break; }
+          if (old == e) break;
+          h = (h + 1) & vmask;
+        }
+      }
+      const u64 fm = __ballot(fresh);
+      const int nf = __popcll(fm);
+      if (fresh) sc_ids[__popcll(fm & below)] = e;
+      nvis += nf;
+      st_vl0 += nf;
+      st_dist += nf;
+      if (nvis > A.vis_limit) { status = ST_OVERFLOW; break; }
+      if (nf == 0) continue;
+      wave_sync();
+      dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, nf, lane);
+      wave_sync();
+      float my_d = lane < nf ? sc_d[lane] : INF;
+      const u32 my_id = lane < nf ? sc_ids[lane] : INV;
+      if (my_d != my_d) {  // NaN: the reference's comparisons are all false; no ordered slot exists here
+        my_d = INF;
+        ++ties;
+      }
+      // fresh keys that can enter (:461): below the current farthest, or the list not yet full
+      const u64 acc = __ballot(lane < nf && (cs < ef || my_d < cmax));
+
+      // prefetch the adjacency row of the candidate expected next: the smallest unexpanded key after insertion
+      {
+        const float fmin = wave_min(((acc >> lane) & 1ull) ? my_d : INF);
+        float emin = INF;
+        u32 eid_ = INV;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const u64 m = __ballot(ci[r] != INV && (ci[r] & EXPANDED) == 0);
+          if (emin == INF && m) {
+            const int l = static_cast<int>(__builtin_ctzll(m));
+            emin = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ck[r]), l));
+            eid_ = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(ci[r]), l));
+          }
+        }
+        u32 pid = eid_;
+        if (fmin < emin) {
+          const u64 hit = __ballot(((acc >> lane) & 1ull) && my_d == fmin);
+          pid = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(my_id), static_cast<int>(__builtin_ctzll(hit))));
+        }
+        pre_id = pid;
+        if (pid != INV && static_cast<u32>(lane) < M0) pre_e = A.g.adj0[static_cast<u64>(pid) * M0 + lane];
+      }
+
+      // insertion in list order (the set outcome is order-free; ties are what the order could decide)
+      u64 todo = acc;
+      while (todo) {
+        const int j = static_cast<int>(__builtin_ctzll(todo));
+        todo &= todo - 1;
+        const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_d), j));
+        if (cs == ef && !(d < cmax)) {
+          if (d == cmax) ++ties;  // rejected on an equal key (:461 strict)
+          continue;
+        }
+        const u32 id = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(my_id), j));
+        int pos = 0;
+        bool eq = false;
+        float carry_k[R];
+        u32 carry_i[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          pos += __popcll(__ballot(ck[r] < d));
+          eq |= __ballot(ck[r] == d) != 0ull;
+          carry_k[r] = r == 0 ? INF : __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ck[r - 1]), 63));
+          carry_i[r] = r == 0 ? INV : static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(ci[r - 1]), 63));
+        }
+        if (eq) ++ties;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int pp = 64 * r + lane;
+          const float sk = dpp_shr1(ck[r], carry_k[r]);
+          const u32 si = dpp_shr1(ci[r], carry_i[r]);
+          const bool keep = pp < pos;
+          ck[r] = keep ? ck[r] : (pp == pos ? d : (pp < ef ? sk : INF));
+          ci[r] = keep ? ci[r] : (pp == pos ? id : (pp < ef ? si : INV));
+        }
+        if (cs < ef) ++cs;
+        if (cs == ef) {
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            if (((ef - 1) >> 6) == r) cmax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ck[r]), (ef - 1) & 63));
+        }
+      }
+    }
+
+    // top-k in ascending order
+    const u64 obase = static_cast<u64>(qi) * A.k;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const u32 i = static_cast<u32>(64 * r + lane);
+      if (i < A.k) {
+        const bool ok = status == 0 && static_cast<int>(i) < cs;
+        A.out_ids[obase + i] = ok ? A.g.uid[ci[r] & ~EXPANDED] : INV;
+        if (A.out_dists) A.out_dists[obase + i] = ok ? ck[r] : 0.f;
+      }
+    }
+    if (status == ST_OVERFLOW && A.out_list && lane == 0) A.out_list[atomicAdd(A.out_count, 1u)] = qi;
+    if (A.qstats && lane == 0) {
+      u32* qs = A.qstats + static_cast<u64>(qi) * 8;
+      qs[0] = st_dist;
+      qs[1] = st_vup;
+      qs[2] = st_vl0;
+      qs[3] = st_lup;
+      qs[4] = st_ll0;
+      qs[5] = ties;
+      qs[6] = status;
+      qs[7] = status == 0 ? static_cast<u32>(cs < static_cast<int>(A.k) ? cs : A.k) : 0u;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -737,6 +989,22 @@ hipError_t launch_search_t(uint32_t grid, const SearchArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, s, a);
     return hipGetLastError();
   };
+  if (a.fast) {  // sorted-list kernel; the launcher's caller guarantees ef <= 256 and a visited table in LDS
+    const size_t lds_f = search_fast_lds_bytes(a.vis_cap);
+    auto runf = [&](auto kern) -> hipError_t {
+      if (lds_f > 65536) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_f));
+        if (e != hipSuccess) return e;
+      }
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds_f, s, a);
+      return hipGetLastError();
+    };
+    if (a.vis_cap == 0 || a.ef == 0 || a.ef > 256) return hipErrorInvalidValue;
+    if (a.ef <= 64) return runf(search_fast_kernel<D, METRIC, E, 1>);
+    if (a.ef <= 128) return runf(search_fast_kernel<D, METRIC, E, 2>);
+    return runf(search_fast_kernel<D, METRIC, E, 4>);
+  }
   if constexpr (D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
     if (a.prof && a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0, true>);
   }

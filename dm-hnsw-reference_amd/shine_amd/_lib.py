@@ -19,6 +19,8 @@ METRIC_L2, METRIC_IP = 0, 1
 ELEM_F32, ELEM_F16 = 0, 1
 QS_DISTCOMPS, QS_VISITED_UPPER, QS_VISITED_L0, QS_LISTS_UPPER, QS_LISTS_L0, QS_MAX_NEXT, QS_STATUS, QS_NRESULT = range(8)
 QS_WORDS = 8
+QS_TIES = 5  # fast mode's meaning of word 5
+MODE_EXACT, MODE_FAST = 0, 1
 
 
 class ShineError(RuntimeError):
@@ -76,6 +78,7 @@ PROTOTYPES = {
     "shine_knn_batch": (I32, [P, P, U32, U32, U32, P, P, P, C.POINTER(Stats)]),
     "shine_knn_batch_device": (I32, [P, U32, P, U32, U32, U32, P, P, P, P]),
     "shine_distance_batch_device": (I32, [P, U32, P, U32, P, U32, P, P]),
+    "shine_set_search_mode": (I32, [P, I32]),
     "shine_index_get_info": (I32, [P, C.POINTER(IndexInfo)]),
     "shine_algorithmic_bytes": (U64, [P, P, U32]),
     "shine_close": (I32, [P]),

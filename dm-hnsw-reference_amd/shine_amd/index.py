@@ -39,6 +39,7 @@ class Index:
         self._h = C.c_void_p(handle)
         self.dim = dim
         self.metric = metric
+        self.mode = L.MODE_EXACT
 
     # ---- construction ----------------------------------------------------------------------------------
     @classmethod
@@ -85,6 +86,11 @@ class Index:
         inf = L.IndexInfo()
         L.check(L.lib().shine_index_get_info(self._h, C.byref(inf)))
         return inf.as_dict()
+
+    def set_search_mode(self, mode: int) -> None:
+        """L.MODE_EXACT (reference heap order, tie-exact) or L.MODE_FAST (sorted list, ascending results)."""
+        L.check(L.lib().shine_set_search_mode(self._h, mode))
+        self.mode = mode
 
     # ---- queries -----------------------------------------------------------------------------------------
     def knn(self, queries: np.ndarray, k: int, ef: int) -> KnnResult:

@@ -41,7 +41,8 @@ extern "C" {
 #define SHINE_QS_VISITED_L0 2    /* stats.visited_nodes_l0                  (statistics.hh:164-170) */
 #define SHINE_QS_LISTS_UPPER 3   /* stats.visited_neighborlists, level > 0  (hnsw.hh:359) */
 #define SHINE_QS_LISTS_L0 4      /* stats.visited_neighborlists, level 0    (hnsw.hh:438) */
-#define SHINE_QS_MAX_NEXT 5      /* peak size of next_candidates (diagnostic) */
+#define SHINE_QS_MAX_NEXT 5      /* exact mode: peak size of next_candidates (diagnostic) */
+#define SHINE_QS_TIES 5          /* fast mode: equal-key events met (0 = result identical to exact mode) */
 #define SHINE_QS_STATUS 6        /* 0 = ok, otherwise the SHINE_ERR_* that stopped this query */
 #define SHINE_QS_NRESULT 7       /* number of ids written (< k only if the graph has fewer nodes) */
 #define SHINE_QS_WORDS 8
@@ -104,6 +105,15 @@ int shine_knn_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_qu
  * out[i*n_per_query + j] = Distance::dist(q_i, x_uid) (distance.hh:153-161).  Device pointers, async. */
 int shine_distance_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_queries, uint32_t nq,
                                 const uint32_t* d_node_uids, uint32_t n_per_query, float* d_out, void* stream);
+
+/* Search modes.  EXACT (default): the reference's two std heaps replayed step for step — ids in heap-array
+ * order, identical to HNSW::knn under distance ties.  FAST: one sorted candidate list per query held in
+ * registers (ef <= 256; larger ef runs the exact kernel); same expansions, ids, distances and counters whenever
+ * no two distances compare equal where the reference's heap layout would break the tie (qstats word
+ * SHINE_QS_TIES counts such events, 0 = identical set), results in ascending distance order. */
+#define SHINE_MODE_EXACT 0
+#define SHINE_MODE_FAST 1
+int shine_set_search_mode(shine_index_t h, int mode);
 
 int shine_index_get_info(shine_index_t h, shine_index_info* out);
 
