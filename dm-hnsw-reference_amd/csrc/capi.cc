@@ -465,9 +465,14 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
       std::fprintf(stderr, "SHINE_PHASE_PROFILE entries:");
       for (int i = 12; i < 24; ++i) std::fprintf(stderr, " %llu", ph[i]);
       std::fprintf(stderr, "\n");
-      std::fprintf(stderr, "SHINE_PHASE_PROFILE cycles: setup %llu greedy %llu pop %llu adj+visited %llu dist %llu "
-                           "predict %llu accept-loop %llu out %llu next-push %llu top-pop %llu top-push %llu trim %llu\n",
-                   ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6], ph[7], ph[8], ph[9], ph[10], ph[11]);
+      if (h->search_mode == SHINE_MODE_FAST)
+        std::fprintf(stderr, "SHINE_PHASE_PROFILE cycles: setup %llu greedy %llu pick %llu adj-wait %llu dist %llu "
+                             "predict %llu insert %llu out %llu visited %llu\n",
+                     ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6], ph[7], ph[8]);
+      else
+        std::fprintf(stderr, "SHINE_PHASE_PROFILE cycles: setup %llu greedy %llu pop %llu adj+visited %llu dist %llu "
+                             "predict %llu accept-loop %llu out %llu next-push %llu top-pop %llu top-push %llu trim %llu\n",
+                     ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6], ph[7], ph[8], ph[9], ph[10], ph[11]);
     }
     uint32_t ovf_counts[2] = {0, 0};  // queries handed to the fixup passes
     HIP_TRY(hipMemcpy(ovf_counts, R.counter.p + 3, sizeof(ovf_counts), hipMemcpyDeviceToHost));

@@ -686,7 +686,12 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
 // ends when none is left (the break at :424).  One expansion's accept / push / push_k sequence leaves top equal to
 // the ef smallest of (top ∪ fresh).  Hence, when no two keys compare equal where the reference's tie-breaking
 // could decide, this kernel expands the same nodes in the same order and returns the same ids, distances and
-// counters; it counts the equal-key events it meets (qstats word 5) so a caller can tell.  Results are written
+// counters.  The events where heap layout decides are counted in qstats word 5 (0 = identical result):
+//   * a key inserted equal to an unexpanded one (which of the two next_candidates yields first),
+//   * an eviction whose farthest entry had an equal twin (which one push_k pops, heap.hh:34-41),
+//   * equal keys at positions k-1 and k at the end (which one the trim to k pops, hnsw.hh:296-299),
+//   * NaN keys.
+// A key equal to the farthest with the list full is rejected by both (:461 is strict).  Results are written
 // in ascending distance order.  Costs: an insertion is two ballots per register plus one DPP wave_shr per
 // register (no LDS), the next candidate is one ballot per register.
 // ------------------------------------------------------------------------------------------------------------
@@ -699,8 +704,10 @@ __device__ __forceinline__ u32 dpp_shr1(u32 v, u32 fill) {
   return static_cast<u32>(__builtin_amdgcn_update_dpp(static_cast<int>(fill), static_cast<int>(v), 0x138, 0xF, 0xF, false));
 }
 
-template <int D, int METRIC, typename E, int R>
+template <int D, int METRIC, typename E, int R, bool PROF = false>
 __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
+  PhaseClock<PROF> clk;
+  clk.start();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   u32* vtab = reinterpret_cast<u32*>(smem);  // visited table
   u32* sc_ids = vtab + A.vis_cap;             // fresh neighbours
@@ -721,6 +728,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
     if (item >= n_items) break;
     const u32 qi = A.in_list ? A.in_list[item] : item;
 
+    PHASE(0)
     QueryRegs<D> Q;
     load_query<D>(A.queries + static_cast<u64>(qi) * D, lane, Q);
     {
@@ -728,6 +736,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       for (u32 i = lane; i < A.vis_cap / 4; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
     }
     u32 st_dist = 0, st_vup = 0, st_vl0 = 0, st_lup = 0, st_ll0 = 0, ties = 0, status = 0;
+    PHASE(1)
     u32 nn;
     float closest;
     entry_and_descent<D, METRIC, E>(A, vec, Q, sc_ids, sc_d, lane, nn, closest, st_dist, st_vup, st_vl0, st_lup, status);
@@ -755,6 +764,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
 
     while (status == 0) {
       // smallest unexpanded candidate = next_candidates.top() (:418)
+      PHASE(2)
       int p = -1;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -774,6 +784,11 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       u32 e = INV;
       if (cid == pre_id) e = pre_e;
       else if (static_cast<u32>(lane) < M0) e = A.g.adj0[static_cast<u64>(cid) * M0 + lane];
+      if (PROF) {  // diagnostics: charge the adjacency-row wait to phase 3, the probes to phase 8
+        PHASE(3)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PHASE(8)
+      }
       bool cand = e != INV;
       if (!A.g.lists_unique) {
         for (u32 j = 0; j < M0; ++j) {
@@ -799,9 +814,11 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       st_dist += nf;
       if (nvis > A.vis_limit) { status = ST_OVERFLOW; break; }
       if (nf == 0) continue;
+      PHASE(4)
       wave_sync();
       dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, nf, lane);
       wave_sync();
+      PHASE(5)
       float my_d = lane < nf ? sc_d[lane] : INF;
       const u32 my_id = lane < nf ? sc_ids[lane] : INV;
       if (my_d != my_d) {  // NaN: the reference's comparisons are all false; no ordered slot exists here
@@ -835,15 +852,13 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       }
 
       // insertion in list order (the set outcome is order-free; ties are what the order could decide)
+      PHASE(6)
       u64 todo = acc;
       while (todo) {
         const int j = static_cast<int>(__builtin_ctzll(todo));
         todo &= todo - 1;
         const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_d), j));
-        if (cs == ef && !(d < cmax)) {
-          if (d == cmax) ++ties;  // rejected on an equal key (:461 strict)
-          continue;
-        }
+        if (cs == ef && !(d < cmax)) continue;  // rejected (:461 strict) — same outcome for an equal key
         const u32 id = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(my_id), j));
         int pos = 0;
         bool eq = false;
@@ -852,7 +867,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           pos += __popcll(__ballot(ck[r] < d));
-          eq |= __ballot(ck[r] == d) != 0ull;
+          eq |= __ballot(ck[r] == d && (ci[r] & EXPANDED) == 0) != 0ull;  // expansion order would be a tie-break
           carry_k[r] = r == 0 ? INF : __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ck[r - 1]), 63));
           carry_i[r] = r == 0 ? INV : static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(ci[r - 1]), 63));
         }
@@ -866,16 +881,30 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
           ck[r] = keep ? ck[r] : (pp == pos ? d : (pp < ef ? sk : INF));
           ci[r] = keep ? ci[r] : (pp == pos ? id : (pp < ef ? si : INV));
         }
+        const bool was_full = cs == ef;
         if (cs < ef) ++cs;
         if (cs == ef) {
+          const float old_max = cmax;
 #pragma unroll
           for (int r = 0; r < R; ++r)
             if (((ef - 1) >> 6) == r) cmax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ck[r]), (ef - 1) & 63));
+          if (was_full && cmax == old_max) ++ties;  // the evicted farthest had an equal twin: heap layout decides
         }
       }
     }
 
-    // top-k in ascending order
+    PHASE(7)
+    // top-k in ascending order; an equal pair straddling position k is decided by heap layout in the reference
+    if (status == 0 && cs > static_cast<int>(A.k)) {
+      const int k = static_cast<int>(A.k);
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (((k - 1) >> 6) == r) a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ck[r]), (k - 1) & 63));
+        if ((k >> 6) == r) b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ck[r]), k & 63));
+      }
+      if (a == b) ++ties;
+    }
     const u64 obase = static_cast<u64>(qi) * A.k;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -899,6 +928,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       qs[7] = status == 0 ? static_cast<u32>(cs < static_cast<int>(A.k) ? cs : A.k) : 0u;
     }
   }
+  clk.flush(A.prof, lane);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -1001,6 +1031,9 @@ hipError_t launch_search_t(uint32_t grid, const SearchArgs& a, hipStream_t s) {
       return hipGetLastError();
     };
     if (a.vis_cap == 0 || a.ef == 0 || a.ef > 256) return hipErrorInvalidValue;
+    if constexpr (D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
+      if (a.prof && a.ef > 64 && a.ef <= 128) return runf(search_fast_kernel<D, METRIC, E, 2, true>);
+    }
     if (a.ef <= 64) return runf(search_fast_kernel<D, METRIC, E, 1>);
     if (a.ef <= 128) return runf(search_fast_kernel<D, METRIC, E, 2>);
     return runf(search_fast_kernel<D, METRIC, E, 4>);

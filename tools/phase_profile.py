@@ -28,6 +28,8 @@ if not path.exists():
     dumps[0].tofile(path)
 q = D.sift_like(1024, seed=2)
 idx = shine_amd.Index.open([path], 128, 16, 0, gpus=[0])
+if os.environ.get("MODE", "exact") == "fast":
+    idx.set_search_mode(shine_amd.MODE_FAST)
 r = idx.knn(q, 10, ef)
 print("plain kernel_ms", r.stats["kernel_ms"], file=sys.stderr)
 os.environ["SHINE_PHASE_PROFILE"] = "1"
