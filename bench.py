@@ -67,7 +67,9 @@ def parse():
     p.add_argument("--mode", choices=["fast", "exact", "both"], default="both",
                    help="search mode(s); the first one measured gives `value` (fast, then exact with 'both')")
     p.add_argument("--cache", default=os.environ.get("SHINE_BENCH_CACHE", "/tmp/shine_bench"))
-    p.add_argument("--pmc-json", default=None, help="per-launch HBM bytes measured by rocprofv3 --pmc (tools/pmc.py)")
+    p.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r01" / "bench_fast_v2_pmc.json"),
+                   help="per-launch HBM bytes of the search kernel measured by rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                        "passes of this bench (tools/pmc.py; tools/gpu_round.sh)")
     return p.parse_args()
 
 
@@ -198,9 +200,12 @@ def main():
         clean = runs["fast"]["qs"][:, 5] == 0
         mode_report["fast"]["tie_free_same_ids_as_exact"] = float(same[clean].mean()) if clean.any() else None
 
-    traffic = None
+    traffic, traffic_src = None, None
     if a.pmc_json and Path(a.pmc_json).exists():
-        traffic = json.loads(Path(a.pmc_json).read_text()).get("hbm_bytes_per_launch")
+        pmc = json.loads(Path(a.pmc_json).read_text())
+        if any(k.startswith("void shine::(anonymous namespace)::search_fast_kernel<128, 0, float, 2,") for k in pmc.get("kernels", [])):
+            traffic = pmc.get("hbm_bytes_per_launch")
+            traffic_src = str(Path(a.pmc_json).relative_to(ROOT)) if Path(a.pmc_json).is_relative_to(ROOT) else a.pmc_json
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
@@ -228,8 +233,8 @@ def main():
                        "global_batch": a.batch * world, "batch_per_gpu": a.batch, "M": a.M, "efc": a.efc,
                        "ef": a.ef, "k": a.k, "shards": a.shards, "parallelism": f"replica{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                         "kernel": ("search_fast_kernel<128,L2,f32,2>" if modes[0] == "fast"
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": ("search_fast_kernel<128,L2,f32,R=2,P=2>" if modes[0] == "fast"
                                     else "search_kernel<128,L2,f32,0>"), "avg_launch_ms": avg_launch_ms,
                          "algorithmic_bytes_per_launch": float(np.mean(bytes_steps)),
                          "mean_distcomps_per_query": float(qs_h[:, 0].mean())},

@@ -153,16 +153,25 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
   std::vector<uint32_t> inv(h->inv_size, kInvalid);
   for (uint64_t g = 0; g < G.N; ++g) inv[G.uid[g]] = static_cast<uint32_t>(g);
 
-  std::vector<uint8_t> vbytes;
-  const uint8_t* vsrc = reinterpret_cast<const uint8_t*>(G.vec.data());
-  size_t vlen = G.vec.size() * sizeof(float);
-  if (elem == SHINE_ELEM_F16) {  // config 5: records converted to fp16 at load
-    vbytes.resize(G.vec.size() * sizeof(__half));
+  // rows in the device layout (kernels.h permuted_index); config 5 converts records to fp16 at load
+  const uint32_t dim = G.L.dim;
+  std::vector<uint32_t> perm(dim);
+  for (uint32_t i = 0; i < dim; ++i) perm[i] = permuted_index(dim, i);
+  const size_t esz = elem == SHINE_ELEM_F16 ? sizeof(__half) : sizeof(float);
+  std::vector<uint8_t> vbytes(G.vec.size() * esz);
+  {
+    float* fp = reinterpret_cast<float*>(vbytes.data());
     __half* hp = reinterpret_cast<__half*>(vbytes.data());
-    for (size_t i = 0; i < G.vec.size(); ++i) hp[i] = __float2half(G.vec[i]);
-    vsrc = vbytes.data();
-    vlen = vbytes.size();
+    for (uint64_t n = 0; n < G.N; ++n) {
+      const float* src = G.vec.data() + n * dim;
+      for (uint32_t i = 0; i < dim; ++i) {
+        if (elem == SHINE_ELEM_F16) hp[n * dim + perm[i]] = __float2half(src[i]);
+        else fp[n * dim + perm[i]] = src[i];
+      }
+    }
   }
+  const uint8_t* vsrc = vbytes.data();
+  const size_t vlen = vbytes.size();
 
   h->reps.resize(devs.size());
   for (size_t r = 0; r < devs.size(); ++r) {
@@ -466,8 +475,8 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
       for (int i = 12; i < 24; ++i) std::fprintf(stderr, " %llu", ph[i]);
       std::fprintf(stderr, "\n");
       if (h->search_mode == SHINE_MODE_FAST)
-        std::fprintf(stderr, "SHINE_PHASE_PROFILE cycles: setup %llu greedy %llu pick %llu adj-wait %llu dist %llu "
-                             "predict %llu insert %llu out %llu visited %llu\n",
+        std::fprintf(stderr, "SHINE_PHASE_PROFILE cycles: setup %llu greedy %llu pick %llu row-wait %llu dist %llu "
+                             "accept %llu merge %llu out %llu visited %llu\n",
                      ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6], ph[7], ph[8]);
       else
         std::fprintf(stderr, "SHINE_PHASE_PROFILE cycles: setup %llu greedy %llu pop %llu adj+visited %llu dist %llu "

@@ -57,9 +57,23 @@ inline size_t search_lds_bytes(uint32_t ef, uint32_t cap, uint32_t vis_cap) {
   return align16(8ull * ef) + align16(8ull * cap) + 4ull * vis_cap + 64 * 4 * 2;
 }
 
-// LDS of the fast kernel: visited table[vis_cap] | scratch ids[64], dists[64]
-inline size_t search_fast_lds_bytes(uint32_t vis_cap) { return 4ull * vis_cap + 64 * 4 * 2; }
+// LDS of the fast kernel: visited table[vis_cap] | scratch ids[64], dists[64] | merge scratch[kFastMaxEf + 1] u64
 constexpr uint32_t kFastMaxEf = 256;
+inline size_t search_fast_lds_bytes(uint32_t vis_cap) { return 4ull * vis_cap + 64 * 4 * 2 + 8ull * (kFastMaxEf + 2); }
+
+// Device row layout of the vectors.  The reference's AVX2 kernels keep 8 accumulators: accumulator a sums the
+// elements i ≡ a (mod 8) of the 16-aligned prefix in increasing i (distance.hh:11-76).  A distance kernel lane
+// plays accumulators 2c and 2c+1 (c = 0..3) as the halves of a packed-FP32 pair, so the device row stores the
+// prefix in 4-element chunks [acc 2c elem t, acc 2c+1 elem t, acc 2c elem t+1, acc 2c+1 elem t+1] (t even),
+// ordered by (t/2, c):  element a + 8t lives at (t >> 1) * 16 + (a >> 1) * 4 + (t & 1) * 2 + (a & 1).
+// One 16-byte load per lane (8 bytes for f16) then brings two ready-made pairs, and the 4 lanes of a vector read
+// 64 contiguous bytes.  The scalar tail (elements DB..dim-1, distance.hh:112-115) follows unpermuted.
+__host__ __device__ inline uint32_t permuted_index(uint32_t dim, uint32_t i) {
+  const uint32_t db = dim >> 4 << 4;
+  if (i >= db) return i;
+  const uint32_t a = i & 7u, t = i >> 3;
+  return (t >> 1) * 16u + (a >> 1) * 4u + (t & 1u) * 2u + (a & 1u);
+}
 
 bool dim_supported(uint32_t dim, int elem);
 

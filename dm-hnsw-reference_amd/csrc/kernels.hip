@@ -217,88 +217,166 @@ __device__ __forceinline__ u64 heap_pop(u64* h, int n, int lane) {
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// Distance evaluation in the oracle's FP order.  Lane l: group g = l >> 3 evaluates one vector, a = l & 7 is
-// the AVX2 accumulator it plays.  Up to NPB passes of 8 vectors have their loads in flight together.
+// Distance evaluation in the oracle's FP order.  A "pass" evaluates 16 vectors: lane l of the wavefront belongs
+// to group g = l >> 2 (the vector, or slot) and plays the two AVX2 accumulators 2c and 2c+1, c = l & 3, as the
+// two halves of a packed-FP32 register pair: each half runs the scalar fmaf chain of its accumulator
+// (distance.hh:11-76), so v_pk_fma_f32 does two accumulators per instruction.  Rows are stored in the device
+// layout of kernels.h (permuted_index): one 16-byte load (f32; 8 bytes for f16) brings elements t and t+1 of
+// both of the lane's accumulators, already paired, and the 4 lanes of a group read 64 contiguous bytes.  The
+// eight partial sums are folded left to right, ((((a0 + a1) + a2) ... ) + a7), by a 3-step DPP row_shr:1 chain
+// that ends in the group's lane c = 3, which then adds the scalar tail.
 // ------------------------------------------------------------------------------------------------------------
-template <int D>
-struct Geo {
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int D, typename E>
+struct Lay {
   static constexpr int DB = D >> 4 << 4;  // elements handled by the SIMD16 kernel (qty16 << 4)
-  static constexpr int PER = DB / 8;      // elements per accumulator lane
+  static constexpr int PER = DB / 8;      // elements per accumulator
+  static constexpr int NCH = PER / 2;     // 4-element chunks per lane
   static constexpr int TAIL = D - DB;     // scalar tail (distance.hh:112-115, 136-139)
-  static constexpr int PERA = PER > 0 ? PER : 1;
   static constexpr int TAILA = TAIL > 0 ? TAIL : 1;
-  static constexpr int NPB = PER == 0 ? 4 : (64 / PER < 1 ? 1 : (64 / PER > 4 ? 4 : 64 / PER));
+  static_assert(DB >= 16, "dimension must be >= 16");
 };
 
 template <int D>
 struct QueryRegs {
-  float qv[Geo<D>::PERA];
-  float qt[Geo<D>::TAILA];
+  f32x2 q2[D / 16 * 2];  // {q[2c + 8t], q[2c + 1 + 8t]}, t < PER
+  float qt[(D & 15) > 0 ? (D & 15) : 1];
 };
 
 template <int D>
 __device__ __forceinline__ void load_query(const float* __restrict__ q, int lane, QueryRegs<D>& Q) {
-  using G = Geo<D>;
-  const int a8 = lane & 7;
+  constexpr int DB = D >> 4 << 4, PER = DB / 8, TAIL = D - DB;
+  const int c2 = 2 * (lane & 3);
 #pragma unroll
-  for (int t = 0; t < G::PER; ++t) Q.qv[t] = q[a8 + 8 * t];
+  for (int t = 0; t < PER; ++t) Q.q2[t] = f32x2{q[c2 + 8 * t], q[c2 + 1 + 8 * t]};
 #pragma unroll
-  for (int t = 0; t < G::TAIL; ++t) Q.qt[t] = q[G::DB + t];
+  for (int t = 0; t < TAIL; ++t) Q.qt[t] = q[DB + t];
+}
+
+// One chunk = elements (t, t+1) of accumulators (2c, 2c+1): f32 → 4 floats, f16 → 4 halves in 2 words.
+template <typename E>
+struct ChunkT {
+  using type = f32x4;
+};
+template <>
+struct ChunkT<__half> {
+  using type = uint2;
+};
+
+// The neighbour vectors of P passes (16 slots each) in VGPRs.
+template <int D, typename E, int P>
+struct NbrBuf {
+  using L = Lay<D, E>;
+  typename ChunkT<E>::type x[P][L::NCH];
+  float xt[P][L::TAILA];  // scalar tail, lane c = 3 only
+};
+
+// Issue the loads of pass p: this lane's group evaluates node `id` (INV: nothing to load).
+template <int D, typename E, int P>
+__device__ __forceinline__ void issue_pass(NbrBuf<D, E, P>& B, int p, const E* __restrict__ vec, u32 id, int c4) {
+  using L = Lay<D, E>;
+  using C = typename ChunkT<E>::type;
+  if (id != INV) {
+    const E* row = vec + static_cast<u64>(id) * D;
+#pragma unroll
+    for (int u = 0; u < L::NCH; ++u) B.x[p][u] = *reinterpret_cast<const C*>(row + u * 16 + c4 * 4);
+    if (c4 == 3) {
+#pragma unroll
+      for (int t = 0; t < L::TAIL; ++t) B.xt[p][t] = to_f32(row[L::DB + t]);
+    }
+  }
+}
+
+__device__ __forceinline__ f32x2 half2_to_f32x2(u32 w) {
+  return f32x2{__half2float(__ushort_as_half(static_cast<unsigned short>(w & 0xFFFFu))),
+               __half2float(__ushort_as_half(static_cast<unsigned short>(w >> 16)))};
+}
+
+// Left fold of a group's 8 accumulators (lane c holds 2c, 2c+1) into its lane c = 3.
+__device__ __forceinline__ float fold8(f32x2 acc) {
+  float s = acc.x + acc.y;
+#pragma unroll
+  for (int j = 1; j < 4; ++j)
+    s = (__int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x111, 0xF, 0xF, false)) + acc.x) + acc.y;
+  return s;
+}
+
+template <int D, int METRIC>
+__device__ __forceinline__ float add_tail(const QueryRegs<D>& Q, const float* xt, float s) {
+  constexpr int TAIL = D & 15;
+  if constexpr (METRIC == 0) {
+#pragma unroll
+    for (int t = 0; t < TAIL; ++t) {
+      const float df = Q.qt[t] - xt[t];
+      s = __builtin_fmaf(df, df, s);
+    }
+    return s;
+  } else {
+    float tl = 0.f;
+#pragma unroll
+    for (int t = 0; t < TAIL; ++t) tl = __builtin_fmaf(Q.qt[t], xt[t], tl);
+    return 1.0f - (s + tl);
+  }
+}
+
+template <int METRIC>
+__device__ __forceinline__ f32x2 acc_step(f32x2 q, f32x2 x, f32x2 acc) {
+  if constexpr (METRIC == 0) {
+    const f32x2 df = q - x;
+    return __builtin_elementwise_fma(df, df, acc);
+  } else {
+    return __builtin_elementwise_fma(q, x, acc);
+  }
+}
+
+// out[p] = distance of the pass-p vector of this lane's group; valid in lanes c = 3.
+template <int D, int METRIC, typename E, int P>
+__device__ __forceinline__ void pass_dists(const QueryRegs<D>& Q, const NbrBuf<D, E, P>& B, float (&out)[P]) {
+  using L = Lay<D, E>;
+  f32x2 acc[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) acc[p] = f32x2{0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < L::NCH; ++u) {
+#pragma unroll
+    for (int p = 0; p < P; ++p) {  // P independent chains interleaved
+      f32x2 x0, x1;
+      if constexpr (std::is_same_v<E, float>) {
+        x0 = B.x[p][u].xy;
+        x1 = B.x[p][u].zw;
+      } else {
+        x0 = half2_to_f32x2(B.x[p][u].x);
+        x1 = half2_to_f32x2(B.x[p][u].y);
+      }
+      acc[p] = acc_step<METRIC>(Q.q2[2 * u], x0, acc[p]);
+      acc[p] = acc_step<METRIC>(Q.q2[2 * u + 1], x1, acc[p]);
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < P; ++p) out[p] = add_tail<D, METRIC>(Q, B.xt[p], fold8(acc[p]));
 }
 
 // sc_d[j] = dist(q, vec[sc_ids[j]]) for j < n.  All 64 lanes must call it.
 template <int D, int METRIC, typename E>
 __device__ __forceinline__ void dist_list(const E* __restrict__ vec, const QueryRegs<D>& Q, const u32* sc_ids,
                                           float* sc_d, int n, int lane) {
-  using G = Geo<D>;
-  const int g8 = lane >> 3, a8 = lane & 7, base = lane & ~7;
-  for (int p0 = 0; p0 < n; p0 += 8 * G::NPB) {
-    float x[G::NPB][G::PERA];
-    float xt[G::NPB][G::TAILA];
+  constexpr int P = 2;
+  const int g4 = lane >> 2, c4 = lane & 3;
+  for (int p0 = 0; p0 < n; p0 += 16 * P) {
+    NbrBuf<D, E, P> B;
 #pragma unroll
-    for (int pp = 0; pp < G::NPB; ++pp) {
-      const int slot = p0 + pp * 8 + g8;
-      if (slot < n) {
-        const E* row = vec + static_cast<u64>(sc_ids[slot]) * D;
-#pragma unroll
-        for (int t = 0; t < G::PER; ++t) x[pp][t] = to_f32(row[a8 + 8 * t]);
-        if (a8 == 0) {
-#pragma unroll
-          for (int t = 0; t < G::TAIL; ++t) xt[pp][t] = to_f32(row[G::DB + t]);
-        }
-      }
+    for (int p = 0; p < P; ++p) {
+      const int slot = p0 + 16 * p + g4;
+      issue_pass<D, E, P>(B, p, vec, slot < n ? sc_ids[slot] : INV, c4);
     }
+    float out[P];
+    pass_dists<D, METRIC, E, P>(Q, B, out);
 #pragma unroll
-    for (int pp = 0; pp < G::NPB; ++pp) {
-      float acc = 0.f;
-#pragma unroll
-      for (int t = 0; t < G::PER; ++t) {
-        if constexpr (METRIC == 0) {
-          const float df = Q.qv[t] - x[pp][t];
-          acc = __builtin_fmaf(df, df, acc);
-        } else {
-          acc = __builtin_fmaf(Q.qv[t], x[pp][t], acc);
-        }
-      }
-      float s = __shfl(acc, base);
-#pragma unroll
-      for (int j = 1; j < 8; ++j) s = s + __shfl(acc, base + j);
-      const int slot = p0 + pp * 8 + g8;
-      if (a8 == 0 && slot < n) {
-        if constexpr (METRIC == 0) {
-#pragma unroll
-          for (int t = 0; t < G::TAIL; ++t) {
-            const float df = Q.qt[t] - xt[pp][t];
-            s = __builtin_fmaf(df, df, s);
-          }
-        } else {
-          float tl = 0.f;
-#pragma unroll
-          for (int t = 0; t < G::TAIL; ++t) tl = __builtin_fmaf(Q.qt[t], xt[pp][t], tl);
-          s = 1.0f - (s + tl);
-        }
-        sc_d[slot] = s;
-      }
+    for (int p = 0; p < P; ++p) {
+      const int slot = p0 + 16 * p + g4;
+      if (c4 == 3 && slot < n) sc_d[slot] = out[p];
     }
   }
 }
@@ -402,9 +480,9 @@ struct PhaseClock {  // empty unless PROF
   __device__ void flush(unsigned long long*, int) {}
 };
 template <>
-struct PhaseClock<true> {
-  u64 ph[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  u32 cnt[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // entries into each phase
+struct PhaseClock<true> {  // lane i accumulates phase i: one compare and one 64-bit add per mark
+  u64 acc = 0;
+  u32 cnt = 0;
   u64 t_last = 0;
   int cur = 0;
   __device__ void start() { t_last = stamp(); }
@@ -412,21 +490,18 @@ struct PhaseClock<true> {
     __builtin_amdgcn_sched_barrier(0);
     const u64 t = stamp();
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < 12; ++j) {
-      if (j == cur) ph[j] += t - t_last;
-      if (j == i) ++cnt[j];
-    }
+    const int lane = static_cast<int>(threadIdx.x);
+    if (lane == cur) acc += t - t_last;
+    if (lane == i) ++cnt;
     t_last = t;
     cur = i;
   }
   __device__ void flush(unsigned long long* out, int lane) {
     mark(0);
-    if (lane == 0 && out)
-      for (int j = 0; j < 12; ++j) {
-        atomicAdd(&out[j], static_cast<unsigned long long>(ph[j]));
-        atomicAdd(&out[12 + j], static_cast<unsigned long long>(cnt[j]));
-      }
+    if (out && lane < 12) {
+      atomicAdd(&out[lane], static_cast<unsigned long long>(acc));
+      atomicAdd(&out[12 + lane], static_cast<unsigned long long>(cnt));
+    }
   }
 };
 #define PHASE(i) clk.mark(i);
@@ -704,21 +779,23 @@ __device__ __forceinline__ u32 dpp_shr1(u32 v, u32 fill) {
   return static_cast<u32>(__builtin_amdgcn_update_dpp(static_cast<int>(fill), static_cast<int>(v), 0x138, 0xF, 0xF, false));
 }
 
-template <int D, int METRIC, typename E, int R, bool PROF = false>
+template <int D, int METRIC, typename E, int R, int P, bool PROF = false>
 __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
   PhaseClock<PROF> clk;
   clk.start();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   u32* vtab = reinterpret_cast<u32*>(smem);  // visited table
-  u32* sc_ids = vtab + A.vis_cap;             // fresh neighbours
+  u32* sc_ids = vtab + A.vis_cap;             // greedy-descent scratch
   float* sc_d = reinterpret_cast<float*>(sc_ids + 64);
-  const int lane = threadIdx.x;
+  u64* mrg = reinterpret_cast<u64*>(sc_d + 64);  // merge scratch: (key, id) at merged positions 0 .. ef
+  const int lane = threadIdx.x, g4 = lane >> 2, c4 = lane & 3;
   const E* __restrict__ vec = static_cast<const E*>(A.g.vec);
+  const u32* __restrict__ adj0 = A.g.adj0;
   const u32 M0 = A.g.M0;
   const int ef = static_cast<int>(A.ef);
   const u32 vmask = A.vis_cap - 1, vshift = 32 - (31 - __clz(static_cast<int>(A.vis_cap)));
-  const u64 below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const float INF = __builtin_inff();
+  const bool in_row = static_cast<u32>(lane) < M0;
 
   const u32 n_items = A.in_count ? *A.in_count : A.nq;
   for (;;) {
@@ -750,47 +827,50 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       ci[r] = INV;
     }
     int cs = 0;
+    float cmax = INF;  // key at position ef - 1 once the list is full
     if (status == 0) {
       ck[0] = lane == 0 ? closest : INF;
-      ci[0] = lane == 0 ? nn : INV;
+      ci[0] = lane == 0 ? (nn | EXPANDED) : INV;  // popped right away (:418)
       cs = 1;
       if (closest != closest) ++ties;
       if (lane == 0) vtab[vhash(nn, vshift)] = nn;
       wave_sync();
     }
     u32 nvis = 1;
-    u32 pre_id = INV, pre_e = INV;
-    float cmax = INF;  // key at position ef - 1 once the list is full
+    u32 row = (status == 0 && in_row) ? adj0[static_cast<u64>(nn) * M0 + lane] : INV;  // list of the candidate
+    // The runner-up unexpanded candidate's list is prefetched one expansion ahead (it is the next candidate
+    // unless a fresh key overtakes it).  Its load is issued right after the current list has arrived, so that
+    // waiting for a list never waits for the younger prefetch (vmcnt counts in order).
+    u32 want = INV;              // runner-up to prefetch at the top of the next expansion
+    u32 nid = INV, nrow = INV;   // prefetched list and its node
+    u32 cur = nn;                // the candidate being expanded
 
     while (status == 0) {
-      // smallest unexpanded candidate = next_candidates.top() (:418)
-      PHASE(2)
-      int p = -1;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const u64 m = __ballot(ci[r] != INV && (ci[r] & EXPANDED) == 0);
-        if (p < 0 && m) p = 64 * r + static_cast<int>(__builtin_ctzll(m));
-      }
-      if (p < 0) break;  // every candidate within the radius expanded: the break at :424
-      u32 cid = 0;
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-        if ((p >> 6) == r) {
-          cid = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(ci[r]), p & 63));
-          ci[r] = lane == (p & 63) ? (ci[r] | EXPANDED) : ci[r];
-        }
-
+      // ---- expand the candidate whose list is in `row` (:436-465) -------------------------------------------
       ++st_ll0;  // read_neighborlist (:436-438)
-      u32 e = INV;
-      if (cid == pre_id) e = pre_e;
-      else if (static_cast<u32>(lane) < M0) e = A.g.adj0[static_cast<u64>(cid) * M0 + lane];
-      if (PROF) {  // diagnostics: charge the adjacency-row wait to phase 3, the probes to phase 8
-        PHASE(3)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        PHASE(8)
+      PHASE(3)
+      const u32 e = row;
+      {  // issued on every path, so the wait for `row` is always vmcnt(1) and never covers this load
+        const u32 pf = want != INV ? want : cur;
+        const u32 v = adj0[static_cast<u64>(pf) * M0 + (in_row ? lane : 0)];
+        nrow = in_row ? v : INV;
+        nid = pf;
       }
+      // Every neighbour's vector is requested before the visited test: the test (LDS atomics) then runs under
+      // the loads' latency.  Already-visited neighbours were read by this query before, mostly from L2.
+      // slot j = list position j; pass p holds slots 16p .. 16p+15, group g4 evaluates slot 16p + g4.
+      PHASE(4)
+      NbrBuf<D, E, P> X;
+      {
+        u32 sid[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) sid[p] = static_cast<u32>(__shfl(static_cast<int>(e), 16 * p + g4));
+#pragma unroll
+        for (int p = 0; p < P; ++p) issue_pass<D, E, P>(X, p, vec, sid[p], c4);
+      }
+      PHASE(8)
       bool cand = e != INV;
-      if (!A.g.lists_unique) {
+      if (!A.g.lists_unique) {  // first occurrence in list order wins (visited.insert order, :443)
         for (u32 j = 0; j < M0; ++j) {
           const u32 ej = __shfl(e, static_cast<int>(j));
           if (j < static_cast<u32>(lane) && ej == e) cand = false;
@@ -808,89 +888,123 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       }
       const u64 fm = __ballot(fresh);
       const int nf = __popcll(fm);
-      if (fresh) sc_ids[__popcll(fm & below)] = e;
       nvis += nf;
       st_vl0 += nf;
       st_dist += nf;
       if (nvis > A.vis_limit) { status = ST_OVERFLOW; break; }
-      if (nf == 0) continue;
-      PHASE(4)
-      wave_sync();
-      dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, nf, lane);
-      wave_sync();
-      PHASE(5)
-      float my_d = lane < nf ? sc_d[lane] : INF;
-      const u32 my_id = lane < nf ? sc_ids[lane] : INV;
-      if (my_d != my_d) {  // NaN: the reference's comparisons are all false; no ordered slot exists here
-        my_d = INF;
-        ++ties;
-      }
-      // fresh keys that can enter (:461): below the current farthest, or the list not yet full
-      const u64 acc = __ballot(lane < nf && (cs < ef || my_d < cmax));
 
-      // prefetch the adjacency row of the candidate expected next: the smallest unexpanded key after insertion
-      {
-        const float fmin = wave_min(((acc >> lane) & 1ull) ? my_d : INF);
-        float emin = INF;
-        u32 eid_ = INV;
+      if (nf > 0) {
+        PHASE(5)
+        float out[P];
+        pass_dists<D, METRIC, E, P>(Q, X, out);
+        float my_d = INF;  // lane j: distance of slot j
+        const int src = ((lane & 15) << 2) + 3;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const u64 m = __ballot(ci[r] != INV && (ci[r] & EXPANDED) == 0);
-          if (emin == INF && m) {
-            const int l = static_cast<int>(__builtin_ctzll(m));
-            emin = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ck[r]), l));
-            eid_ = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(ci[r]), l));
+        for (int p = 0; p < P; ++p) {
+          const float v = __shfl(out[p], src);
+          if ((lane >> 4) == p) my_d = v;
+        }
+        if (!fresh) my_d = INF;
+        if (fresh && my_d != my_d) {  // NaN: the reference's comparisons are all false; no ordered slot exists here
+          my_d = INF;
+          ++ties;
+        }
+        // fresh keys that can enter (:461): below the current farthest, or the list not yet full
+        const u64 acc = __ballot(fresh && (cs < ef || my_d < cmax));
+
+        // ---- merge (:456-465 over the whole list at once) -------------------------------------------------
+        // One expansion's accept / push / push_k sequence leaves the ef smallest of (list ∪ accepted).  Merged
+        // order: ascending key; among equal keys the fresh ones first, later list positions first (the order
+        // successive push_k calls would leave).  Every equality the order could decide is counted in `ties`:
+        // equal neighbours in the merged list with one of them unexpanded (which one next_candidates yields
+        // first), and equal keys on both sides of the cut at ef (which one push_k pops).
+        PHASE(6)
+        if (acc) {
+          int shift[R];
+#pragma unroll
+          for (int r = 0; r < R; ++r) shift[r] = 0;
+          int frank = 0;  // fresh lane: accepted keys ordered before it
+          int fbase = 0;  // fresh lane: list entries below it
+          u64 todo = acc;
+          while (todo) {
+            const int i = static_cast<int>(__builtin_ctzll(todo));
+            todo &= todo - 1;
+            const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_d), i));
+            int below = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              shift[r] += d <= ck[r] ? 1 : 0;
+              below += __popcll(__ballot(ck[r] < d));
+            }
+            frank += (d < my_d || (d == my_d && i > lane)) ? 1 : 0;
+            fbase = lane == i ? below : fbase;
+          }
+          const int total = cs + __popcll(acc);
+          const int hi = total < ef + 1 ? total : ef + 1;  // merged positions written: 0 .. hi-1
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int p = 64 * r + lane;
+            const int np = p + shift[r];
+            if (p < cs && np <= ef) mrg[np] = (static_cast<u64>(ci[r]) << 32) | __float_as_uint(ck[r]);
+          }
+          if ((acc >> lane) & 1ull) {
+            const int np = fbase + frank;
+            if (np <= ef) mrg[np] = (static_cast<u64>(e) << 32) | __float_as_uint(my_d);
+          }
+          wave_sync();
+          cs = total < ef ? total : ef;
+          bool tie = false;
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int p = 64 * r + lane;
+            u64 m0 = (static_cast<u64>(INV) << 32) | __float_as_uint(INF), m1 = m0;
+            if (p + 1 < hi) {
+              m0 = mrg[p];
+              m1 = mrg[p + 1];
+              tie |= key(m0) == key(m1) && ((eid(m0) & EXPANDED) == 0 || (eid(m1) & EXPANDED) == 0 || p + 1 == ef);
+            } else if (p < hi) {
+              m0 = mrg[p];
+            }
+            if (p >= cs) m0 = (static_cast<u64>(INV) << 32) | __float_as_uint(INF);
+            ck[r] = key(m0);
+            ci[r] = eid(m0);
+          }
+          if (__ballot(tie)) ++ties;
+          wave_sync();
+          if (cs == ef) {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+              if (((ef - 1) >> 6) == r) cmax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ck[r]), (ef - 1) & 63));
           }
         }
-        u32 pid = eid_;
-        if (fmin < emin) {
-          const u64 hit = __ballot(((acc >> lane) & 1ull) && my_d == fmin);
-          pid = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(my_id), static_cast<int>(__builtin_ctzll(hit))));
-        }
-        pre_id = pid;
-        if (pid != INV && static_cast<u32>(lane) < M0) pre_e = A.g.adj0[static_cast<u64>(pid) * M0 + lane];
       }
 
-      // insertion in list order (the set outcome is order-free; ties are what the order could decide)
-      PHASE(6)
-      u64 todo = acc;
-      while (todo) {
-        const int j = static_cast<int>(__builtin_ctzll(todo));
-        todo &= todo - 1;
-        const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_d), j));
-        if (cs == ef && !(d < cmax)) continue;  // rejected (:461 strict) — same outcome for an equal key
-        const u32 id = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(my_id), j));
-        int pos = 0;
-        bool eq = false;
-        float carry_k[R];
-        u32 carry_i[R];
+      // ---- next_candidates.top(); pop() (:418-426): the smallest unexpanded candidate -------------------------
+      PHASE(2)
+      int p1 = -1, p2 = -1;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          pos += __popcll(__ballot(ck[r] < d));
-          eq |= __ballot(ck[r] == d && (ci[r] & EXPANDED) == 0) != 0ull;  // expansion order would be a tie-break
-          carry_k[r] = r == 0 ? INF : __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ck[r - 1]), 63));
-          carry_i[r] = r == 0 ? INV : static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(ci[r - 1]), 63));
+      for (int r = 0; r < R; ++r) {
+        u64 m = __ballot(ci[r] != INV && (ci[r] & EXPANDED) == 0);
+        if (p1 < 0 && m) {
+          p1 = 64 * r + static_cast<int>(__builtin_ctzll(m));
+          m &= m - 1;
         }
-        if (eq) ++ties;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int pp = 64 * r + lane;
-          const float sk = dpp_shr1(ck[r], carry_k[r]);
-          const u32 si = dpp_shr1(ci[r], carry_i[r]);
-          const bool keep = pp < pos;
-          ck[r] = keep ? ck[r] : (pp == pos ? d : (pp < ef ? sk : INF));
-          ci[r] = keep ? ci[r] : (pp == pos ? id : (pp < ef ? si : INV));
-        }
-        const bool was_full = cs == ef;
-        if (cs < ef) ++cs;
-        if (cs == ef) {
-          const float old_max = cmax;
-#pragma unroll
-          for (int r = 0; r < R; ++r)
-            if (((ef - 1) >> 6) == r) cmax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ck[r]), (ef - 1) & 63));
-          if (was_full && cmax == old_max) ++ties;  // the evicted farthest had an equal twin: heap layout decides
-        }
+        if (p1 >= 0 && p2 < 0 && m) p2 = 64 * r + static_cast<int>(__builtin_ctzll(m));
       }
+      if (p1 < 0) break;  // every candidate within the radius expanded: the break at :424
+      u32 c = 0, c2 = INV;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if ((p1 >> 6) == r) {
+          c = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(ci[r]), p1 & 63));
+          ci[r] = lane == (p1 & 63) ? (ci[r] | EXPANDED) : ci[r];
+        }
+        if (p2 >= 0 && (p2 >> 6) == r) c2 = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(ci[r]), p2 & 63));
+      }
+      if (c == nid) row = nrow;
+      else row = in_row ? adj0[static_cast<u64>(c) * M0 + lane] : INV;
+      want = c2;
+      cur = c;
     }
 
     PHASE(7)
@@ -1031,12 +1145,15 @@ hipError_t launch_search_t(uint32_t grid, const SearchArgs& a, hipStream_t s) {
       return hipGetLastError();
     };
     if (a.vis_cap == 0 || a.ef == 0 || a.ef > 256) return hipErrorInvalidValue;
+    // P = passes of 16 list slots: 2 covers M0 <= 32 (M <= 16), 4 covers M0 <= 64
+    if (a.g.M0 > 64) return hipErrorInvalidValue;
+    const bool wide = a.g.M0 > 32;
     if constexpr (D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
-      if (a.prof && a.ef > 64 && a.ef <= 128) return runf(search_fast_kernel<D, METRIC, E, 2, true>);
+      if (a.prof && !wide && a.ef > 64 && a.ef <= 128) return runf(search_fast_kernel<D, METRIC, E, 2, 2, true>);
     }
-    if (a.ef <= 64) return runf(search_fast_kernel<D, METRIC, E, 1>);
-    if (a.ef <= 128) return runf(search_fast_kernel<D, METRIC, E, 2>);
-    return runf(search_fast_kernel<D, METRIC, E, 4>);
+    if (a.ef <= 64) return wide ? runf(search_fast_kernel<D, METRIC, E, 1, 4>) : runf(search_fast_kernel<D, METRIC, E, 1, 2>);
+    if (a.ef <= 128) return wide ? runf(search_fast_kernel<D, METRIC, E, 2, 4>) : runf(search_fast_kernel<D, METRIC, E, 2, 2>);
+    return wide ? runf(search_fast_kernel<D, METRIC, E, 4, 4>) : runf(search_fast_kernel<D, METRIC, E, 4, 2>);
   }
   if constexpr (D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
     if (a.prof && a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0, true>);
@@ -1055,7 +1172,11 @@ hipError_t launch_distance_t(const DistArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+#ifdef SHINE_ISA_ONLY_128  // development: device-ISA inspection of the d = 128 kernels only
+#define SHINE_DIMS(X) X(128)
+#else
 #define SHINE_DIMS(X) X(16) X(32) X(64) X(96) X(100) X(128) X(200) X(256)
+#endif
 
 }  // namespace
 

@@ -17,8 +17,8 @@ from shine_amd import datasets as D  # noqa: E402
 
 n = int(os.environ.get("N", "1000000"))
 ef = int(os.environ.get("EF", "128"))
-cache = Path("/tmp/shine_bench_phase")
-path = cache / "dump" / shine_amd.dump_name(16, 200, 0, 1)
+cache = Path("/tmp/shine_bench_phase") if n == 1_000_000 else Path(f"/tmp/shine_size_probe/n{n}")
+path = (cache / "dump" if n == 1_000_000 else cache) / shine_amd.dump_name(16, 200, 0, 1)
 if not path.exists():
     base = D.sift_like(n, seed=1)
     t = time.time()
