@@ -474,9 +474,9 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
       std::fprintf(stderr, "SHINE_PHASE_PROFILE entries:");
       for (int i = 12; i < 24; ++i) std::fprintf(stderr, " %llu", ph[i]);
       std::fprintf(stderr, "\n");
-      if (h->search_mode == SHINE_MODE_FAST)
-        std::fprintf(stderr, "SHINE_PHASE_PROFILE cycles: setup %llu greedy %llu pick %llu row-wait %llu dist %llu "
-                             "accept %llu merge %llu out %llu visited %llu\n",
+      if (h->search_mode == SHINE_MODE_FAST)  // entry counts 9..11: next = runner-up / fresh, mispredicted
+        std::fprintf(stderr, "SHINE_PHASE_PROFILE cycles: setup %llu greedy %llu pick %llu - %llu predict+issue %llu "
+                             "dist %llu merge %llu out %llu visited %llu\n",
                      ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6], ph[7], ph[8]);
       else
         std::fprintf(stderr, "SHINE_PHASE_PROFILE cycles: setup %llu greedy %llu pop %llu adj+visited %llu dist %llu "

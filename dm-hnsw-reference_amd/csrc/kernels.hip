@@ -289,6 +289,19 @@ __device__ __forceinline__ void issue_pass(NbrBuf<D, E, P>& B, int p, const E* _
   }
 }
 
+// Unconditional form: always the same number of load instructions (an INV slot reads node 0 and is ignored), so
+// that the compiler's vmcnt bookkeeping stays exact across the software pipeline of search_fast_kernel.
+template <int D, typename E, int P>
+__device__ __forceinline__ void issue_pass_u(NbrBuf<D, E, P>& B, int p, const E* __restrict__ vec, u32 id, int c4) {
+  using L = Lay<D, E>;
+  using C = typename ChunkT<E>::type;
+  const E* row = vec + static_cast<u64>(id == INV ? 0u : id) * D;
+#pragma unroll
+  for (int u = 0; u < L::NCH; ++u) B.x[p][u] = *reinterpret_cast<const C*>(row + u * 16 + c4 * 4);
+#pragma unroll
+  for (int t = 0; t < L::TAIL; ++t) B.xt[p][t] = to_f32(row[L::DB + t]);
+}
+
 __device__ __forceinline__ f32x2 half2_to_f32x2(u32 w) {
   return f32x2{__half2float(__ushort_as_half(static_cast<unsigned short>(w & 0xFFFFu))),
                __half2float(__ushort_as_half(static_cast<unsigned short>(w >> 16)))};
@@ -477,6 +490,7 @@ template <bool PROF>
 struct PhaseClock {  // empty unless PROF
   __device__ void start() {}
   __device__ void mark(int) {}
+  __device__ void event(int) {}
   __device__ void flush(unsigned long long*, int) {}
 };
 template <>
@@ -496,6 +510,9 @@ struct PhaseClock<true> {  // lane i accumulates phase i: one compare and one 64
     t_last = t;
     cur = i;
   }
+  __device__ void event(int i) {  // counts only (slots no phase uses)
+    if (static_cast<int>(threadIdx.x) == i) ++cnt;
+  }
   __device__ void flush(unsigned long long* out, int lane) {
     mark(0);
     if (out && lane < 12) {
@@ -505,6 +522,7 @@ struct PhaseClock<true> {  // lane i accumulates phase i: one compare and one 64
   }
 };
 #define PHASE(i) clk.mark(i);
+#define EVENT(i) clk.event(i);
 
 template <int D, int METRIC, typename E, int VIS, bool PROF = false>
 __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
@@ -772,11 +790,23 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
 // ------------------------------------------------------------------------------------------------------------
 constexpr u32 EXPANDED = 0x80000000u;  // id bit: this candidate has been expanded (ids < 2^31)
 
-__device__ __forceinline__ float dpp_shr1(float v, float fill) {  // lane l <- lane l-1, lane 0 <- fill
-  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(fill), __float_as_int(v), 0x138, 0xF, 0xF, false));
-}
-__device__ __forceinline__ u32 dpp_shr1(u32 v, u32 fill) {
-  return static_cast<u32>(__builtin_amdgcn_update_dpp(static_cast<int>(fill), static_cast<int>(v), 0x138, 0xF, 0xF, false));
+// ------------------------------------------------------------------------------------------------------------
+// Pipelining.  The neighbour-vector loads of the NEXT expansion are issued before the current one's merge: once
+// the distances of expansion t are known, the next candidate is already determined — the smaller of the runner-up
+// unexpanded entry r (whose list was prefetched one expansion earlier) and the best accepted fresh key f* (merged
+// order puts fresh keys first among equals, later list positions first).  For r the vectors are requested at once;
+// for f* its list is loaded first.  Either way they land while the merge and the pick run.  A misprediction (only
+// possible through ties or NaN keys) re-issues the loads for the picked candidate.  The one neighbour buffer is
+// refilled as soon as the current distances have consumed it, and every list / vector load on the common path is
+// unconditional, so every wait is an exact vmcnt that never covers the younger prefetches.
+// ------------------------------------------------------------------------------------------------------------
+template <int D, typename E, int P>
+__device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restrict__ vec, u32 e, int g4, int c4) {
+  u32 sid[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) sid[p] = static_cast<u32>(__shfl(static_cast<int>(e), 16 * p + g4));
+#pragma unroll
+  for (int p = 0; p < P; ++p) issue_pass_u<D, E, P>(B, p, vec, sid[p], c4);
 }
 
 template <int D, int METRIC, typename E, int R, int P, bool PROF = false>
@@ -796,6 +826,10 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
   const u32 vmask = A.vis_cap - 1, vshift = 32 - (31 - __clz(static_cast<int>(A.vis_cap)));
   const float INF = __builtin_inff();
   const bool in_row = static_cast<u32>(lane) < M0;
+  const u32 row_lane = in_row ? static_cast<u32>(lane) : 0u;
+  // Unconditional, and never masked right after the load (that would wait for it): lanes beyond M0 hold a copy of
+  // entry 0 and are excluded where the list is used (the visited test; slots >= M0 are never fresh).
+  auto load_row = [&](u32 node) -> u32 { return adj0[static_cast<u64>(node) * M0 + row_lane]; };
 
   const u32 n_items = A.in_count ? *A.in_count : A.nq;
   for (;;) {
@@ -828,6 +862,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
     }
     int cs = 0;
     float cmax = INF;  // key at position ef - 1 once the list is full
+    u32 nvis = 1;
     if (status == 0) {
       ck[0] = lane == 0 ? closest : INF;
       ci[0] = lane == 0 ? (nn | EXPANDED) : INV;  // popped right away (:418)
@@ -836,40 +871,21 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       if (lane == 0) vtab[vhash(nn, vshift)] = nn;
       wave_sync();
     }
-    u32 nvis = 1;
-    u32 row = (status == 0 && in_row) ? adj0[static_cast<u64>(nn) * M0 + lane] : INV;  // list of the candidate
-    // The runner-up unexpanded candidate's list is prefetched one expansion ahead (it is the next candidate
-    // unless a fresh key overtakes it).  Its load is issued right after the current list has arrived, so that
-    // waiting for a list never waits for the younger prefetch (vmcnt counts in order).
-    u32 want = INV;              // runner-up to prefetch at the top of the next expansion
-    u32 nid = INV, nrow = INV;   // prefetched list and its node
-    u32 cur = nn;                // the candidate being expanded
+
+    // pipeline state: the candidate's list `e` and its vectors in X (in flight); the runner-up r and its
+    // prefetched list.  X is refilled for the next candidate as soon as the current distances have consumed it.
+    NbrBuf<D, E, P> X;
+    u32 e = load_row(status == 0 ? nn : 0u);
+    issue_list<D, E, P>(X, vec, e, g4, c4);
+    u32 r_id = INV;
+    float r_key = INF;
+    u32 nid = nn;
+    u32 nrow = load_row(nn);
 
     while (status == 0) {
-      // ---- expand the candidate whose list is in `row` (:436-465) -------------------------------------------
       ++st_ll0;  // read_neighborlist (:436-438)
-      PHASE(3)
-      const u32 e = row;
-      {  // issued on every path, so the wait for `row` is always vmcnt(1) and never covers this load
-        const u32 pf = want != INV ? want : cur;
-        const u32 v = adj0[static_cast<u64>(pf) * M0 + (in_row ? lane : 0)];
-        nrow = in_row ? v : INV;
-        nid = pf;
-      }
-      // Every neighbour's vector is requested before the visited test: the test (LDS atomics) then runs under
-      // the loads' latency.  Already-visited neighbours were read by this query before, mostly from L2.
-      // slot j = list position j; pass p holds slots 16p .. 16p+15, group g4 evaluates slot 16p + g4.
-      PHASE(4)
-      NbrBuf<D, E, P> X;
-      {
-        u32 sid[P];
-#pragma unroll
-        for (int p = 0; p < P; ++p) sid[p] = static_cast<u32>(__shfl(static_cast<int>(e), 16 * p + g4));
-#pragma unroll
-        for (int p = 0; p < P; ++p) issue_pass<D, E, P>(X, p, vec, sid[p], c4);
-      }
       PHASE(8)
-      bool cand = e != INV;
+      bool cand = in_row && e != INV;
       if (!A.g.lists_unique) {  // first occurrence in list order wins (visited.insert order, :443)
         for (u32 j = 0; j < M0; ++j) {
           const u32 ej = __shfl(e, static_cast<int>(j));
@@ -891,13 +907,17 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       nvis += nf;
       st_vl0 += nf;
       st_dist += nf;
-      if (nvis > A.vis_limit) { status = ST_OVERFLOW; break; }
+      if (nvis > A.vis_limit) {
+        status = ST_OVERFLOW;
+        break;
+      }
 
+      PHASE(5)
+      float my_d = INF;  // lane j: distance of list slot j
+      u64 acc = 0;
       if (nf > 0) {
-        PHASE(5)
         float out[P];
         pass_dists<D, METRIC, E, P>(Q, X, out);
-        float my_d = INF;  // lane j: distance of slot j
         const int src = ((lane & 15) << 2) + 3;
 #pragma unroll
         for (int p = 0; p < P; ++p) {
@@ -909,102 +929,129 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
           my_d = INF;
           ++ties;
         }
-        // fresh keys that can enter (:461): below the current farthest, or the list not yet full
-        const u64 acc = __ballot(fresh && (cs < ef || my_d < cmax));
+        acc = __ballot(fresh && (cs < ef || my_d < cmax));  // fresh keys that can enter (:461)
+      }
 
-        // ---- merge (:456-465 over the whole list at once) -------------------------------------------------
-        // One expansion's accept / push / push_k sequence leaves the ef smallest of (list ∪ accepted).  Merged
-        // order: ascending key; among equal keys the fresh ones first, later list positions first (the order
-        // successive push_k calls would leave).  Every equality the order could decide is counted in `ties`:
-        // equal neighbours in the merged list with one of them unexpanded (which one next_candidates yields
-        // first), and equal keys on both sides of the cut at ef (which one push_k pops).
-        PHASE(6)
-        if (acc) {
-          int shift[R];
+      // ---- the next candidate, known before the merge ----------------------------------------------------------
+      // the smaller of f* (best accepted fresh key; among equals the last list position, as merged) and the
+      // runner-up r; its vectors are requested here, one issue point for every path, into the buffer the
+      // distances above have just consumed
+      PHASE(4)
+      u32 pid = r_id;
+      if (acc) {
+        const float fstar = wave_min(((acc >> lane) & 1ull) ? my_d : INF);
+        const u64 hit = acc & __ballot(my_d == fstar);
+        if (r_id == INV || fstar <= r_key)
+          pid = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(e), 63 - static_cast<int>(__clzll(hit))));
+      }
+      if (pid == r_id) EVENT(9) else EVENT(10)
+      const u32 prow = pid == r_id ? nrow : load_row(pid != INV ? pid : 0u);  // a fresh f*: its list now
+      issue_list<D, E, P>(X, vec, prow, g4, c4);
+
+      // ---- merge (:456-465 over the whole list at once) ----------------------------------------------------------
+      PHASE(6)
+      if (acc) {
+        int shift[R];
 #pragma unroll
-          for (int r = 0; r < R; ++r) shift[r] = 0;
-          int frank = 0;  // fresh lane: accepted keys ordered before it
-          int fbase = 0;  // fresh lane: list entries below it
-          u64 todo = acc;
-          while (todo) {
-            const int i = static_cast<int>(__builtin_ctzll(todo));
-            todo &= todo - 1;
-            const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_d), i));
-            int below = 0;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-              shift[r] += d <= ck[r] ? 1 : 0;
-              below += __popcll(__ballot(ck[r] < d));
-            }
-            frank += (d < my_d || (d == my_d && i > lane)) ? 1 : 0;
-            fbase = lane == i ? below : fbase;
-          }
-          const int total = cs + __popcll(acc);
-          const int hi = total < ef + 1 ? total : ef + 1;  // merged positions written: 0 .. hi-1
-#pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const int p = 64 * r + lane;
-            const int np = p + shift[r];
-            if (p < cs && np <= ef) mrg[np] = (static_cast<u64>(ci[r]) << 32) | __float_as_uint(ck[r]);
-          }
-          if ((acc >> lane) & 1ull) {
-            const int np = fbase + frank;
-            if (np <= ef) mrg[np] = (static_cast<u64>(e) << 32) | __float_as_uint(my_d);
-          }
-          wave_sync();
-          cs = total < ef ? total : ef;
-          bool tie = false;
+        for (int r = 0; r < R; ++r) shift[r] = 0;
+        int frank = 0;  // fresh lane: accepted keys ordered before it
+        int fbase = 0;  // fresh lane: list entries below it
+        u64 todo = acc;
+        while (todo) {
+          const int i = static_cast<int>(__builtin_ctzll(todo));
+          todo &= todo - 1;
+          const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_d), i));
+          int below = 0;
 #pragma unroll
           for (int r = 0; r < R; ++r) {
-            const int p = 64 * r + lane;
-            u64 m0 = (static_cast<u64>(INV) << 32) | __float_as_uint(INF), m1 = m0;
-            if (p + 1 < hi) {
-              m0 = mrg[p];
-              m1 = mrg[p + 1];
-              tie |= key(m0) == key(m1) && ((eid(m0) & EXPANDED) == 0 || (eid(m1) & EXPANDED) == 0 || p + 1 == ef);
-            } else if (p < hi) {
-              m0 = mrg[p];
-            }
-            if (p >= cs) m0 = (static_cast<u64>(INV) << 32) | __float_as_uint(INF);
-            ck[r] = key(m0);
-            ci[r] = eid(m0);
+            shift[r] += d <= ck[r] ? 1 : 0;
+            below += __popcll(__ballot(ck[r] < d));
           }
-          if (__ballot(tie)) ++ties;
-          wave_sync();
-          if (cs == ef) {
+          frank += (d < my_d || (d == my_d && i > lane)) ? 1 : 0;
+          fbase = lane == i ? below : fbase;
+        }
+        const int total = cs + __popcll(acc);
+        const int hi = total < ef + 1 ? total : ef + 1;  // merged positions written: 0 .. hi-1
+        const int sink = ef + 1;  // entries that fall past the cut are written to a scratch slot (no branches)
 #pragma unroll
-            for (int r = 0; r < R; ++r)
-              if (((ef - 1) >> 6) == r) cmax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ck[r]), (ef - 1) & 63));
-          }
+        for (int r = 0; r < R; ++r) {
+          const int p = 64 * r + lane;
+          const int np = p + shift[r];
+          mrg[(p < cs && np <= ef) ? np : sink] = (static_cast<u64>(ci[r]) << 32) | __float_as_uint(ck[r]);
+        }
+        {
+          const int np = fbase + frank;
+          mrg[(((acc >> lane) & 1ull) && np <= ef) ? np : sink] = (static_cast<u64>(e) << 32) | __float_as_uint(my_d);
+        }
+        wave_sync();
+        cs = total < ef ? total : ef;
+        bool tie = false;
+        const u64 none = (static_cast<u64>(INV) << 32) | __float_as_uint(INF);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int p = 64 * r + lane;
+          const int pc = p < ef ? p : ef;  // positions p, p + 1 in one ds_read2 (p + 1 <= sink)
+          const u64 m0r = mrg[pc], m1r = mrg[pc + 1];
+          tie |= p + 1 < hi && key(m0r) == key(m1r) &&
+                 ((eid(m0r) & EXPANDED) == 0 || (eid(m1r) & EXPANDED) == 0 || p + 1 == ef);
+          const u64 m0 = p < cs ? m0r : none;
+          ck[r] = key(m0);
+          ci[r] = eid(m0);
+        }
+        if (__ballot(tie)) ++ties;
+        wave_sync();
+        if (cs == ef) {
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            if (((ef - 1) >> 6) == r) cmax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ck[r]), (ef - 1) & 63));
         }
       }
 
-      // ---- next_candidates.top(); pop() (:418-426): the smallest unexpanded candidate -------------------------
+      // ---- next_candidates.top(); pop() (:418-426) and the new runner-up -----------------------------------
       PHASE(2)
-      int p1 = -1, p2 = -1;
+      u64 um[R];  // unexpanded entries (INV carries the EXPANDED bit)
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        u64 m = __ballot(ci[r] != INV && (ci[r] & EXPANDED) == 0);
-        if (p1 < 0 && m) {
-          p1 = 64 * r + static_cast<int>(__builtin_ctzll(m));
-          m &= m - 1;
-        }
-        if (p1 >= 0 && p2 < 0 && m) p2 = 64 * r + static_cast<int>(__builtin_ctzll(m));
-      }
+      for (int r = 0; r < R; ++r) um[r] = __ballot(static_cast<int>(ci[r]) >= 0);
+      int p1 = -1;
+#pragma unroll
+      for (int r = R - 1; r >= 0; --r) p1 = um[r] ? 64 * r + static_cast<int>(__builtin_ctzll(um[r])) : p1;
       if (p1 < 0) break;  // every candidate within the radius expanded: the break at :424
-      u32 c = 0, c2 = INV;
+      const int r1 = p1 >> 6, l1 = p1 & 63;
+      u32 c = 0;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        if ((p1 >> 6) == r) {
-          c = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(ci[r]), p1 & 63));
-          ci[r] = lane == (p1 & 63) ? (ci[r] | EXPANDED) : ci[r];
-        }
-        if (p2 >= 0 && (p2 >> 6) == r) c2 = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(ci[r]), p2 & 63));
+        const u32 cr = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(ci[r]), l1));
+        c = r == r1 ? cr : c;
+        ci[r] = (r == r1 && lane == l1) ? (ci[r] | EXPANDED) : ci[r];
+        um[r] = r == r1 ? (um[r] & (um[r] - 1)) : um[r];
       }
-      if (c == nid) row = nrow;
-      else row = in_row ? adj0[static_cast<u64>(c) * M0 + lane] : INV;
-      want = c2;
-      cur = c;
+      int p2 = -1;
+#pragma unroll
+      for (int r = R - 1; r >= 0; --r) p2 = um[r] ? 64 * r + static_cast<int>(__builtin_ctzll(um[r])) : p2;
+      u32 c2 = INV;
+      float k2 = INF;
+      {
+        const int r2 = p2 >> 6, l2 = p2 & 63;  // p2 = -1: r2 = -1 matches no register
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const u32 cr = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(ci[r]), l2 & 63));
+          const float kr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ck[r]), l2 & 63));
+          c2 = r == r2 ? cr : c2;
+          k2 = r == r2 ? kr : k2;
+        }
+      }
+      u32 erow = prow;
+      if (c != pid) {  // mispredicted (ties / NaN keys): fetch the picked candidate's list and vectors
+        EVENT(11)
+        erow = c == nid ? nrow : load_row(c);
+        issue_list<D, E, P>(X, vec, erow, g4, c4);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this rare path leaves nothing in flight behind the prefetch
+      }
+      nid = c2 != INV ? c2 : c;
+      nrow = load_row(nid);  // unconditional: always the youngest load
+      e = erow;
+      r_id = c2;
+      r_key = k2;
     }
 
     PHASE(7)
