@@ -60,8 +60,27 @@ struct DevBuf {
   }
 };
 
+// One virtual range whose pieces live in different GPUs' HBM (SHINE_PLACE_SHARDED): the owner of each piece holds
+// the physical allocation, every GPU of the handle maps the whole range.
+struct StripedRange {
+  char* va = nullptr;
+  size_t bytes = 0;  // reserved
+  std::vector<std::pair<size_t, size_t>> maps;  // (offset, size) of each mapped piece
+  std::vector<hipMemGenericAllocationHandle_t> handles;
+  void release() {
+    for (auto& m : maps) (void)hipMemUnmap(va + m.first, m.second);
+    for (auto& hd : handles) (void)hipMemRelease(hd);
+    if (va) (void)hipMemAddressFree(va, bytes);
+    maps.clear();
+    handles.clear();
+    va = nullptr;
+    bytes = 0;
+  }
+};
+
 struct Replica {
   int device = 0;
+  uint32_t pad_node = 0;  // a node of this slot's own stripe (sharded) for the unconditional loads of empty slots
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   DevBuf<uint8_t> vec;
@@ -86,6 +105,10 @@ struct shine_index {
   uint64_t words_per_slot = 0;
   uint64_t device_bytes = 0;
   int search_mode = SHINE_MODE_EXACT;
+  int placement = SHINE_PLACE_REPLICA;
+  uint64_t id_space = 0;       // device ids are < id_space (sharded: slot o owns [o * ids_per_slot, ...))
+  uint64_t ids_per_slot = 0;
+  StripedRange svec, sadj0;    // sharded: level-0 records of all slots in one virtual range
   std::vector<Replica> reps;
   std::mutex mu;
 };
@@ -94,14 +117,16 @@ namespace {
 
 DevGraph dev_graph(const shine_index* h, const Replica& r) {
   DevGraph g{};
-  g.vec = r.vec.p;
-  g.adj0 = r.adj0.p;
+  const bool sharded = h->placement == SHINE_PLACE_SHARDED;
+  g.vec = sharded ? static_cast<const void*>(h->svec.va) : r.vec.p;
+  g.adj0 = sharded ? reinterpret_cast<const uint32_t*>(h->sadj0.va) : r.adj0.p;
   g.uid = r.uid.p;
   g.up_base = r.up_base.p;
   g.adjU = r.adjU.p;
   g.inv_uid = r.inv_uid.p;
   g.inv_size = h->inv_size;
-  g.N = static_cast<uint32_t>(h->N);
+  g.pad_node = r.pad_node;
+  g.N = static_cast<uint32_t>(h->id_space);
   g.M0 = h->M0;
   g.MU = h->M;
   g.ep = h->ep;
@@ -117,9 +142,70 @@ int upload(DevBuf<T>& dst, const T* src, size_t n, hipStream_t s) {
   return 0;
 }
 
-int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus, shine_index_t* out) {
+void release_index(shine_index* h) {
+  for (auto& R : h->reps) {
+    (void)hipSetDevice(R.device);
+    if (R.stream) (void)hipStreamSynchronize(R.stream);
+    for (auto* b : {&R.adj0, &R.uid, &R.up_base, &R.adjU, &R.inv_uid, &R.visited, &R.vlog, &R.counter, &R.ids, &R.qs,
+                    &R.ovf})
+      b->release();
+    R.prof.release();
+    R.vec.release();
+    R.q.release();
+    R.d.release();
+    if (R.ev0) (void)hipEventDestroy(R.ev0);
+    if (R.ev1) (void)hipEventDestroy(R.ev1);
+    if (R.stream) (void)hipStreamDestroy(R.stream);
+  }
+  h->svec.release();
+  h->sadj0.release();
+  delete h;
+}
+
+hipMemAllocationProp device_prop(int device) {
+  hipMemAllocationProp p{};
+  p.type = hipMemAllocationTypePinned;
+  p.location.type = hipMemLocationTypeDevice;
+  p.location.id = device;
+  return p;
+}
+
+// Reserve slots × U rows of row_bytes, back slot o's first owned[o] rows with HBM of devs[o], and map the whole
+// range for every device of the handle (peer access over xGMI for the pieces another GPU owns).
+int map_striped(StripedRange& S, uint64_t row_bytes, uint64_t U, const std::vector<uint64_t>& owned,
+                const std::vector<int>& devs, size_t gran) {
+  S.bytes = U * row_bytes * devs.size();
+  void* va = nullptr;
+  HIP_TRY(hipMemAddressReserve(&va, S.bytes, gran, nullptr, 0));
+  S.va = static_cast<char*>(va);
+  for (size_t o = 0; o < devs.size(); ++o) {
+    if (owned[o] == 0) continue;
+    const size_t sz = (owned[o] * row_bytes + gran - 1) / gran * gran;
+    const hipMemAllocationProp prop = device_prop(devs[o]);
+    hipMemGenericAllocationHandle_t hd{};
+    HIP_TRY(hipMemCreate(&hd, sz, &prop, 0));
+    S.handles.push_back(hd);
+    HIP_TRY(hipMemMap(S.va + o * U * row_bytes, sz, 0, hd, 0));
+    S.maps.emplace_back(o * U * row_bytes, sz);
+  }
+  std::vector<int> uniq(devs);
+  std::sort(uniq.begin(), uniq.end());
+  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+  std::vector<hipMemAccessDesc> acc(uniq.size());
+  for (size_t i = 0; i < uniq.size(); ++i) {
+    acc[i].location.type = hipMemLocationTypeDevice;
+    acc[i].location.id = uniq[i];
+    acc[i].flags = hipMemAccessFlagsProtReadWrite;
+  }
+  for (auto& m : S.maps) HIP_TRY(hipMemSetAccess(S.va + m.first, m.second, acc.data(), acc.size()));
+  return 0;
+}
+
+int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus, int placement, shine_index_t* out) {
   if (!out) return set_error(SHINE_ERR_ARG, "out is NULL");
   if (elem != SHINE_ELEM_F32 && elem != SHINE_ELEM_F16) return set_error(SHINE_ERR_ARG, "elem must be 0 (f32) or 1 (f16)");
+  if (placement != SHINE_PLACE_REPLICA && placement != SHINE_PLACE_SHARDED)
+    return set_error(SHINE_ERR_ARG, "placement must be SHINE_PLACE_REPLICA or SHINE_PLACE_SHARDED");
   if (!dim_supported(G.L.dim, elem))
     return set_error(SHINE_ERR_ARG, "dim " + std::to_string(G.L.dim) + " has no compiled kernel for this element type");
   int ndev = 0;
@@ -130,8 +216,15 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
   else devs.assign(gpu_ids, gpu_ids + n_gpus);
   for (int d : devs)
     if (d < 0 || d >= ndev) return set_error(SHINE_ERR_ARG, "gpu id " + std::to_string(d) + " out of range");
+  const bool sharded = placement == SHINE_PLACE_SHARDED;
 
-  auto h = std::make_unique<shine_index>();
+  std::unique_ptr<shine_index> h(new shine_index);
+  struct Guard {  // a failed open releases what it had already placed on the devices
+    std::unique_ptr<shine_index>& p;
+    ~Guard() {
+      if (p) release_index(p.release());
+    }
+  } guard{h};
   h->dim = G.L.dim;
   h->M = G.L.M;
   h->M0 = 2 * G.L.M;
@@ -139,25 +232,88 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
   h->elem = elem;
   h->N = G.N;
   h->upper_rows = G.adjU.size() / G.L.M;
-  h->ep = G.ep;
   h->ep_level = G.ep_level;
   h->ep_uid = G.uid[G.ep];
   h->n_shards = G.n_shards;
   h->lists_unique = G.lists_unique ? 1 : 0;
-  h->words_per_slot = (G.N + 31) / 32;
+  h->placement = placement;
 
-  // uid → dense id (for the distance-batch API); uids are the base-file positions, so dense-ish
+  const uint32_t dim = G.L.dim, M0 = h->M0, S = G.n_shards;
+  const uint32_t slots = static_cast<uint32_t>(devs.size());
+  const size_t esz = elem == SHINE_ELEM_F16 ? sizeof(__half) : sizeof(float);
+  const uint64_t vrow = dim * esz, arow = 4ull * M0;
+  const std::vector<uint64_t>& start = G.shard_start;
+
+  // Device id space.  Replica: graph.cc's dense ids.  Sharded: slot o = s % slots owns memory node s; its records
+  // are numbered o * U + (records of its earlier memory nodes) + position, with U a whole number of VM pages of
+  // rows, so that every slot's stripe starts on its own pages of the shared virtual range.
+  std::vector<uint64_t> first(S), owned(slots, 0);
+  uint64_t U = G.N;
+  size_t gran = 0;
+  if (sharded) {
+    for (uint32_t s = 0; s < S; ++s) {
+      first[s] = owned[s % slots];
+      owned[s % slots] += start[s + 1] - start[s];
+    }
+    for (int d : devs) {
+      const hipMemAllocationProp prop = device_prop(d);
+      size_t g = 0;
+      HIP_TRY(hipMemGetAllocationGranularity(&g, &prop, hipMemAllocationGranularityRecommended));
+      gran = std::max(gran, g);
+    }
+    gran = std::max(gran, size_t(1) << 21);  // whole 2 MiB pages per piece (4 KiB pieces were refused access)
+    uint64_t unit = 1;
+    while ((unit * vrow) % gran != 0 || (unit * arow) % gran != 0) unit <<= 1;
+    const uint64_t most = *std::max_element(owned.begin(), owned.end());
+    U = std::max<uint64_t>(unit, (most + unit - 1) / unit * unit);
+    if (U * slots >= 0x80000000ull)
+      return set_error(SHINE_ERR_ARG, "sharded id space of " + std::to_string(U * slots) + " ids exceeds 2^31");
+    for (uint32_t s = 0; s < S; ++s) first[s] += static_cast<uint64_t>(s % slots) * U;
+  } else {
+    for (uint32_t s = 0; s < S; ++s) first[s] = start[s];
+  }
+  const uint64_t id_space = sharded ? U * slots : G.N;
+  h->id_space = id_space;
+  h->ids_per_slot = U;
+  h->words_per_slot = (id_space + 31) / 32;
+  std::vector<uint32_t> newid;
+  if (sharded) {
+    newid.resize(G.N);
+    for (uint32_t s = 0; s < S; ++s)
+      for (uint64_t g = start[s]; g < start[s + 1]; ++g) newid[g] = static_cast<uint32_t>(first[s] + (g - start[s]));
+  }
+  auto dev_id = [&](uint32_t g) -> uint32_t { return (!sharded || g == kInvalid) ? g : newid[g]; };
+  h->ep = dev_id(G.ep);
+
+  // per-node arrays in device order (sharded: holes between the stripes stay kInvalid and are never referenced)
+  std::vector<uint32_t> uid_s, upb_s, adjU_s;
+  const std::vector<uint32_t>* uid_d = &G.uid;
+  const std::vector<uint32_t>* upb_d = &G.up_base;
+  const std::vector<uint32_t>* adjU_d = &G.adjU;
+  if (sharded) {
+    uid_s.assign(id_space, kInvalid);
+    upb_s.assign(id_space, kInvalid);
+    for (uint64_t g = 0; g < G.N; ++g) {
+      uid_s[newid[g]] = G.uid[g];
+      upb_s[newid[g]] = G.up_base[g];
+    }
+    adjU_s.resize(G.adjU.size());
+    for (size_t i = 0; i < G.adjU.size(); ++i) adjU_s[i] = dev_id(G.adjU[i]);
+    uid_d = &uid_s;
+    upb_d = &upb_s;
+    adjU_d = &adjU_s;
+  }
+
+  // uid → device id (for the distance-batch API); uids are the base-file positions, so dense-ish
   uint32_t max_uid = 0;
   for (uint32_t u : G.uid) max_uid = std::max(max_uid, u);
   h->inv_size = max_uid + 1;
   std::vector<uint32_t> inv(h->inv_size, kInvalid);
-  for (uint64_t g = 0; g < G.N; ++g) inv[G.uid[g]] = static_cast<uint32_t>(g);
+  for (uint64_t g = 0; g < G.N; ++g) inv[G.uid[g]] = dev_id(static_cast<uint32_t>(g));
 
   // rows in the device layout (kernels.h permuted_index); config 5 converts records to fp16 at load
-  const uint32_t dim = G.L.dim;
   std::vector<uint32_t> perm(dim);
   for (uint32_t i = 0; i < dim; ++i) perm[i] = permuted_index(dim, i);
-  const size_t esz = elem == SHINE_ELEM_F16 ? sizeof(__half) : sizeof(float);
   std::vector<uint8_t> vbytes(G.vec.size() * esz);
   {
     float* fp = reinterpret_cast<float*>(vbytes.data());
@@ -173,24 +329,52 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
   const uint8_t* vsrc = vbytes.data();
   const size_t vlen = vbytes.size();
 
-  h->reps.resize(devs.size());
-  for (size_t r = 0; r < devs.size(); ++r) {
+  uint32_t pad_default = 0;  // a mapped node for slots that own no records
+  for (uint32_t o = 0; o < slots; ++o)
+    if (sharded && owned[o] > 0) {
+      pad_default = static_cast<uint32_t>(o * U);
+      break;
+    }
+  h->reps.resize(slots);
+  for (uint32_t r = 0; r < slots; ++r) {
     Replica& R = h->reps[r];
     R.device = devs[r];
+    R.pad_node = sharded && owned[r] > 0 ? static_cast<uint32_t>(r * U) : pad_default;
     HIP_TRY(hipSetDevice(R.device));
     HIP_TRY(hipStreamCreateWithFlags(&R.stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&R.ev0));
     HIP_TRY(hipEventCreate(&R.ev1));
-    if (int rc = upload(R.vec, vsrc, vlen, R.stream)) return rc;
-    if (int rc = upload(R.adj0, G.adj0.data(), G.adj0.size(), R.stream)) return rc;
-    if (int rc = upload(R.uid, G.uid.data(), G.uid.size(), R.stream)) return rc;
-    if (int rc = upload(R.up_base, G.up_base.data(), G.up_base.size(), R.stream)) return rc;
-    if (int rc = upload(R.adjU, G.adjU.data(), G.adjU.size(), R.stream)) return rc;
+    if (!sharded) {
+      if (int rc = upload(R.vec, vsrc, vlen, R.stream)) return rc;
+      if (int rc = upload(R.adj0, G.adj0.data(), G.adj0.size(), R.stream)) return rc;
+    }
+    if (int rc = upload(R.uid, uid_d->data(), uid_d->size(), R.stream)) return rc;
+    if (int rc = upload(R.up_base, upb_d->data(), upb_d->size(), R.stream)) return rc;
+    if (int rc = upload(R.adjU, adjU_d->data(), adjU_d->size(), R.stream)) return rc;
     if (int rc = upload(R.inv_uid, inv.data(), inv.size(), R.stream)) return rc;
     if (int rc = R.counter.grow(8)) return rc;
     HIP_TRY(hipStreamSynchronize(R.stream));
   }
-  h->device_bytes = vlen + 4 * (G.adj0.size() + G.uid.size() + G.up_base.size() + G.adjU.size() + inv.size());
+  const uint64_t replicated = 4 * (uid_d->size() + upb_d->size() + adjU_d->size() + inv.size());
+  if (sharded) {
+    if (int rc = map_striped(h->svec, vrow, U, owned, devs, gran)) return rc;
+    if (int rc = map_striped(h->sadj0, arow, U, owned, devs, gran)) return rc;
+    std::vector<uint32_t> rows;
+    for (uint32_t s = 0; s < S; ++s) {
+      const uint64_t n_s = start[s + 1] - start[s];
+      if (n_s == 0) continue;
+      HIP_TRY(hipSetDevice(devs[s % slots]));
+      HIP_TRY(hipMemcpy(h->svec.va + first[s] * vrow, vsrc + start[s] * vrow, n_s * vrow, hipMemcpyHostToDevice));
+      rows.resize(n_s * M0);
+      for (uint64_t i = 0; i < n_s * M0; ++i) rows[i] = dev_id(G.adj0[start[s] * M0 + i]);
+      HIP_TRY(hipMemcpy(h->sadj0.va + first[s] * arow, rows.data(), n_s * arow, hipMemcpyHostToDevice));
+    }
+    uint64_t most = 0;
+    for (uint32_t o = 0; o < slots; ++o) most = std::max(most, owned[o]);
+    h->device_bytes = most * (vrow + arow) + replicated;
+  } else {
+    h->device_bytes = vlen + 4 * G.adj0.size() + replicated;
+  }
   *out = h.release();
   return SHINE_OK;
 }
@@ -350,17 +534,18 @@ extern "C" {
 
 const char* shine_last_error(void) { return last_error(); }
 
-int shine_open_buffers(const uint8_t* const* dumps, const uint64_t* sizes, uint32_t n_dumps, uint32_t dim,
-                       uint32_t M, int metric, int elem, const int* gpu_ids, uint32_t n_gpus, shine_index_t* out) {
+int shine_open_buffers_ex(const uint8_t* const* dumps, const uint64_t* sizes, uint32_t n_dumps, uint32_t dim,
+                          uint32_t M, int metric, int elem, const int* gpu_ids, uint32_t n_gpus, int placement,
+                          shine_index_t* out) {
   if (!dumps || !sizes) return set_error(SHINE_ERR_ARG, "dumps / sizes is NULL");
   if (metric != SHINE_METRIC_L2 && metric != SHINE_METRIC_IP) return set_error(SHINE_ERR_ARG, "metric must be 0 or 1");
   HostGraph G;
   if (int rc = parse_dumps(dumps, sizes, n_dumps, dim, M, metric, 0, G)) return rc;
-  return make_index(G, elem, gpu_ids, n_gpus, out);
+  return make_index(G, elem, gpu_ids, n_gpus, placement, out);
 }
 
-int shine_open(const char* const* dump_paths, uint32_t n_dumps, uint32_t dim, uint32_t M, int metric, int elem,
-               const int* gpu_ids, uint32_t n_gpus, shine_index_t* out) {
+int shine_open_ex(const char* const* dump_paths, uint32_t n_dumps, uint32_t dim, uint32_t M, int metric, int elem,
+                  const int* gpu_ids, uint32_t n_gpus, int placement, shine_index_t* out) {
   if (!dump_paths || n_dumps == 0) return set_error(SHINE_ERR_ARG, "no dump paths");
   std::vector<std::vector<uint8_t>> files(n_dumps);
   std::vector<const uint8_t*> ptrs(n_dumps);
@@ -371,14 +556,25 @@ int shine_open(const char* const* dump_paths, uint32_t n_dumps, uint32_t dim, ui
     ptrs[i] = files[i].data();
     sizes[i] = files[i].size();
   }
-  return shine_open_buffers(ptrs.data(), sizes.data(), n_dumps, dim, M, metric, elem, gpu_ids, n_gpus, out);
+  return shine_open_buffers_ex(ptrs.data(), sizes.data(), n_dumps, dim, M, metric, elem, gpu_ids, n_gpus, placement,
+                               out);
+}
+
+int shine_open_buffers(const uint8_t* const* dumps, const uint64_t* sizes, uint32_t n_dumps, uint32_t dim,
+                       uint32_t M, int metric, int elem, const int* gpu_ids, uint32_t n_gpus, shine_index_t* out) {
+  return shine_open_buffers_ex(dumps, sizes, n_dumps, dim, M, metric, elem, gpu_ids, n_gpus, SHINE_PLACE_REPLICA, out);
+}
+
+int shine_open(const char* const* dump_paths, uint32_t n_dumps, uint32_t dim, uint32_t M, int metric, int elem,
+               const int* gpu_ids, uint32_t n_gpus, shine_index_t* out) {
+  return shine_open_ex(dump_paths, n_dumps, dim, M, metric, elem, gpu_ids, n_gpus, SHINE_PLACE_REPLICA, out);
 }
 
 int shine_set_search_mode(shine_index_t h, int mode) {
   if (!h) return set_error(SHINE_ERR_ARG, "index handle is NULL");
   if (mode != SHINE_MODE_EXACT && mode != SHINE_MODE_FAST) return set_error(SHINE_ERR_ARG, "unknown search mode");
-  if (mode == SHINE_MODE_FAST && h->N >= 0x80000000ull)
-    return set_error(SHINE_ERR_ARG, "fast mode needs fewer than 2^31 nodes per GPU");
+  if (mode == SHINE_MODE_FAST && h->id_space >= 0x80000000ull)
+    return set_error(SHINE_ERR_ARG, "fast mode needs fewer than 2^31 node ids");
   std::lock_guard<std::mutex> lk(h->mu);
   h->search_mode = mode;
   return SHINE_OK;
@@ -398,6 +594,8 @@ int shine_index_get_info(shine_index_t h, shine_index_info* o) {
   o->entry_uid = h->ep_uid;
   o->n_shards = h->n_shards;
   o->n_gpus = static_cast<uint32_t>(h->reps.size());
+  o->placement = static_cast<uint32_t>(h->placement);
+  o->id_space = h->id_space;
   return SHINE_OK;
 }
 
@@ -570,22 +768,7 @@ int shine_selftest_heap(int is_max, const int32_t* ops, const float* vals, const
 }
 
 int shine_close(shine_index_t h) {
-  if (!h) return SHINE_OK;
-  for (auto& R : h->reps) {
-    (void)hipSetDevice(R.device);
-    if (R.stream) (void)hipStreamSynchronize(R.stream);
-    for (auto* b : {&R.adj0, &R.uid, &R.up_base, &R.adjU, &R.inv_uid, &R.visited, &R.vlog, &R.counter, &R.ids, &R.qs,
-                    &R.ovf})
-      b->release();
-    R.prof.release();
-    R.vec.release();
-    R.q.release();
-    R.d.release();
-    if (R.ev0) (void)hipEventDestroy(R.ev0);
-    if (R.ev1) (void)hipEventDestroy(R.ev1);
-    if (R.stream) (void)hipStreamDestroy(R.stream);
-  }
-  delete h;
+  if (h) release_index(h);
   return SHINE_OK;
 }
 

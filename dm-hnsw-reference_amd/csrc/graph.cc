@@ -98,6 +98,7 @@ int parse_dumps(const u8* const* bufs, const u64* sizes, u32 n, u32 dim, u32 M, 
   if (N == 0) return set_error(3, "the dumps hold no records");
   if (N >= kInvalid) return set_error(3, "more than 2^32-1 records");
   G.N = N;
+  G.shard_start = start;
 
   auto translate = [&](u64 rp, u32& out) -> bool {  // RemotePtr → dense id (remote_pointer.hh:19-20)
     const u32 s = static_cast<u32>(rp >> 48);

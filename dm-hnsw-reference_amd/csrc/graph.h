@@ -54,6 +54,7 @@ struct HostGraph {
   u32 ep = kInvalid, ep_level = 0;
   bool lists_unique = true;  // no list holds the same neighbour twice (lets the kernel skip in-list dedup)
   u32 n_shards = 0;
+  std::vector<u64> shard_start;  // [n_shards + 1]: dense ids of memory node s are shard_start[s] .. shard_start[s+1]-1
   u64 bytes_reference_node() const { return L.size_until_components(); }
 };
 

@@ -16,6 +16,7 @@ struct DevGraph {
   const uint32_t* inv_uid;// [inv_size] uid → dense id (distance-batch API)
   uint32_t inv_size;
   uint32_t N, M0, MU, ep, ep_level, lists_unique;
+  uint32_t pad_node;      // a node local to this GPU: unconditional loads of empty list slots read it
 };
 
 struct SearchArgs {

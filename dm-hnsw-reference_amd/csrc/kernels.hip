@@ -289,13 +289,14 @@ __device__ __forceinline__ void issue_pass(NbrBuf<D, E, P>& B, int p, const E* _
   }
 }
 
-// Unconditional form: always the same number of load instructions (an INV slot reads node 0 and is ignored), so
-// that the compiler's vmcnt bookkeeping stays exact across the software pipeline of search_fast_kernel.
+// Unconditional form: always the same number of load instructions (an INV slot reads the local node `pad` and is
+// ignored), so that the compiler's vmcnt bookkeeping stays exact across the software pipeline of search_fast_kernel.
 template <int D, typename E, int P>
-__device__ __forceinline__ void issue_pass_u(NbrBuf<D, E, P>& B, int p, const E* __restrict__ vec, u32 id, int c4) {
+__device__ __forceinline__ void issue_pass_u(NbrBuf<D, E, P>& B, int p, const E* __restrict__ vec, u32 id, u32 pad,
+                                             int c4) {
   using L = Lay<D, E>;
   using C = typename ChunkT<E>::type;
-  const E* row = vec + static_cast<u64>(id == INV ? 0u : id) * D;
+  const E* row = vec + static_cast<u64>(id == INV ? pad : id) * D;
 #pragma unroll
   for (int u = 0; u < L::NCH; ++u) B.x[p][u] = *reinterpret_cast<const C*>(row + u * 16 + c4 * 4);
 #pragma unroll
@@ -801,12 +802,13 @@ constexpr u32 EXPANDED = 0x80000000u;  // id bit: this candidate has been expand
 // unconditional, so every wait is an exact vmcnt that never covers the younger prefetches.
 // ------------------------------------------------------------------------------------------------------------
 template <int D, typename E, int P>
-__device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restrict__ vec, u32 e, int g4, int c4) {
+__device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restrict__ vec, u32 e, u32 pad, int g4,
+                                           int c4) {
   u32 sid[P];
 #pragma unroll
   for (int p = 0; p < P; ++p) sid[p] = static_cast<u32>(__shfl(static_cast<int>(e), 16 * p + g4));
 #pragma unroll
-  for (int p = 0; p < P; ++p) issue_pass_u<D, E, P>(B, p, vec, sid[p], c4);
+  for (int p = 0; p < P; ++p) issue_pass_u<D, E, P>(B, p, vec, sid[p], pad, c4);
 }
 
 template <int D, int METRIC, typename E, int R, int P, bool PROF = false>
@@ -821,7 +823,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
   const int lane = threadIdx.x, g4 = lane >> 2, c4 = lane & 3;
   const E* __restrict__ vec = static_cast<const E*>(A.g.vec);
   const u32* __restrict__ adj0 = A.g.adj0;
-  const u32 M0 = A.g.M0;
+  const u32 M0 = A.g.M0, pad = A.g.pad_node;
   const int ef = static_cast<int>(A.ef);
   const u32 vmask = A.vis_cap - 1, vshift = 32 - (31 - __clz(static_cast<int>(A.vis_cap)));
   const float INF = __builtin_inff();
@@ -875,8 +877,8 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
     // pipeline state: the candidate's list `e` and its vectors in X (in flight); the runner-up r and its
     // prefetched list.  X is refilled for the next candidate as soon as the current distances have consumed it.
     NbrBuf<D, E, P> X;
-    u32 e = load_row(status == 0 ? nn : 0u);
-    issue_list<D, E, P>(X, vec, e, g4, c4);
+    u32 e = load_row(status == 0 ? nn : pad);
+    issue_list<D, E, P>(X, vec, e, pad, g4, c4);
     u32 r_id = INV;
     float r_key = INF;
     u32 nid = nn;
@@ -945,8 +947,8 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
           pid = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(e), 63 - static_cast<int>(__clzll(hit))));
       }
       if (pid == r_id) EVENT(9) else EVENT(10)
-      const u32 prow = pid == r_id ? nrow : load_row(pid != INV ? pid : 0u);  // a fresh f*: its list now
-      issue_list<D, E, P>(X, vec, prow, g4, c4);
+      const u32 prow = pid == r_id ? nrow : load_row(pid != INV ? pid : pad);  // a fresh f*: its list now
+      issue_list<D, E, P>(X, vec, prow, pad, g4, c4);
 
       // ---- merge (:456-465 over the whole list at once) ----------------------------------------------------------
       PHASE(6)
@@ -1044,7 +1046,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       if (c != pid) {  // mispredicted (ties / NaN keys): fetch the picked candidate's list and vectors
         EVENT(11)
         erow = c == nid ? nrow : load_row(c);
-        issue_list<D, E, P>(X, vec, erow, g4, c4);
+        issue_list<D, E, P>(X, vec, erow, pad, g4, c4);
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this rare path leaves nothing in flight behind the prefetch
       }
       nid = c2 != INV ? c2 : c;

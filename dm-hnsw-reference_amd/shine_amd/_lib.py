@@ -21,6 +21,7 @@ QS_DISTCOMPS, QS_VISITED_UPPER, QS_VISITED_L0, QS_LISTS_UPPER, QS_LISTS_L0, QS_M
 QS_WORDS = 8
 QS_TIES = 5  # fast mode's meaning of word 5
 MODE_EXACT, MODE_FAST = 0, 1
+PLACE_REPLICA, PLACE_SHARDED = 0, 1
 
 
 class ShineError(RuntimeError):
@@ -60,6 +61,9 @@ class IndexInfo(C.Structure):
         ("entry_uid", C.c_uint32),
         ("n_shards", C.c_uint32),
         ("n_gpus", C.c_uint32),
+        ("placement", C.c_uint32),
+        ("reserved0", C.c_uint32),
+        ("id_space", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -75,6 +79,9 @@ PROTOTYPES = {
     "shine_open": (I32, [C.POINTER(C.c_char_p), U32, U32, U32, I32, I32, C.POINTER(I32), U32, C.POINTER(P)]),
     "shine_open_buffers": (I32, [C.POINTER(PU8), C.POINTER(U64), U32, U32, U32, I32, I32, C.POINTER(I32), U32,
                                  C.POINTER(P)]),
+    "shine_open_ex": (I32, [C.POINTER(C.c_char_p), U32, U32, U32, I32, I32, C.POINTER(I32), U32, I32, C.POINTER(P)]),
+    "shine_open_buffers_ex": (I32, [C.POINTER(PU8), C.POINTER(U64), U32, U32, U32, I32, I32, C.POINTER(I32), U32, I32,
+                                    C.POINTER(P)]),
     "shine_knn_batch": (I32, [P, P, U32, U32, U32, P, P, P, C.POINTER(Stats)]),
     "shine_knn_batch_device": (I32, [P, U32, P, U32, U32, U32, P, P, P, P]),
     "shine_distance_batch_device": (I32, [P, U32, P, U32, P, U32, P, P]),

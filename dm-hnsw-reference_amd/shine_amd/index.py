@@ -26,6 +26,15 @@ def _gpus(gpus):
     return arr, len(gpus)
 
 
+def _placement(p) -> int:
+    if isinstance(p, int):
+        return p
+    try:
+        return {"replica": L.PLACE_REPLICA, "sharded": L.PLACE_SHARDED}[p]
+    except KeyError:
+        raise ValueError(f"placement must be 'replica' or 'sharded', not {p!r}") from None
+
+
 @dataclass
 class KnnResult:
     ids: np.ndarray      # (nq, k) uint32 uids, reference result order (heap-array order)
@@ -43,22 +52,28 @@ class Index:
 
     # ---- construction ----------------------------------------------------------------------------------
     @classmethod
-    def open(cls, dump_paths, dim: int, M: int, metric: int = L.METRIC_L2, elem: int = L.ELEM_F32, gpus=None):
+    def open(cls, dump_paths, dim: int, M: int, metric: int = L.METRIC_L2, elem: int = L.ELEM_F32, gpus=None,
+             placement: str = "replica"):
+        """placement "replica": every GPU holds the whole index; "sharded": memory node s lives on GPU slot
+        s % len(gpus) only and the others read it over xGMI (include/shine_gpu.h, SHINE_PLACE_SHARDED)."""
         arr = (C.c_char_p * len(dump_paths))(*[str(p).encode() for p in dump_paths])
         g, ng = _gpus(gpus)
         h = C.c_void_p()
-        L.check(L.lib().shine_open(arr, len(dump_paths), dim, M, metric, elem, g, ng, C.byref(h)))
+        L.check(L.lib().shine_open_ex(arr, len(dump_paths), dim, M, metric, elem, g, ng, _placement(placement),
+                                      C.byref(h)))
         return cls(h.value, dim, metric)
 
     @classmethod
-    def from_buffers(cls, dumps, dim: int, M: int, metric: int = L.METRIC_L2, elem: int = L.ELEM_F32, gpus=None):
+    def from_buffers(cls, dumps, dim: int, M: int, metric: int = L.METRIC_L2, elem: int = L.ELEM_F32, gpus=None,
+                     placement: str = "replica"):
         dumps = [np.ascontiguousarray(np.frombuffer(d, dtype=np.uint8) if not isinstance(d, np.ndarray) else d,
                                       dtype=np.uint8) for d in dumps]
         ptrs = (C.POINTER(C.c_uint8) * len(dumps))(*[d.ctypes.data_as(C.POINTER(C.c_uint8)) for d in dumps])
         sizes = (C.c_uint64 * len(dumps))(*[d.size for d in dumps])
         g, ng = _gpus(gpus)
         h = C.c_void_p()
-        L.check(L.lib().shine_open_buffers(ptrs, sizes, len(dumps), dim, M, metric, elem, g, ng, C.byref(h)))
+        L.check(L.lib().shine_open_buffers_ex(ptrs, sizes, len(dumps), dim, M, metric, elem, g, ng,
+                                              _placement(placement), C.byref(h)))
         return cls(h.value, dim, metric)
 
     def close(self):

@@ -72,7 +72,22 @@ typedef struct shine_index_info {
   uint32_t entry_uid;      /* uid of the entry point (ep_ptr in node1's dump, bytes 8..15) */
   uint32_t n_shards;       /* dump files (memory nodes) */
   uint32_t n_gpus;
+  uint32_t placement;      /* SHINE_PLACE_* */
+  uint32_t reserved0;
+  uint64_t id_space;       /* device node-id range: num_nodes (replica) or n_gpus x ids_per_gpu (sharded) */
 } shine_index_info;
+
+/* Placement of the records over the GPUs of a handle.
+ * REPLICA: every GPU holds the whole index (the bench metric's index fits one GPU).
+ * SHARDED: memory node s (dump s+1) lives in the HBM of GPU slot s % n_gpus only, as the reference places records
+ *   on memory nodes (RemotePtr bits 63..48, remote_pointer.hh:9-22, rdma_atomics.hh:89).  The level-0 records
+ *   (vectors and lists) of all slots form one virtual range mapped on every GPU (HIP virtual memory, peer access
+ *   over xGMI): a search dereferences any record directly, local or remote, the way read_node / read_neighborlist
+ *   dereference a RemotePtr (rdma_reads.hh:9-72).  Upper-level lists, uids and the entry point are replicated
+ *   (about 1/M of the index; the reference's read_entry_point_ptr, rdma_reads.hh:74-99).  Queries are split over
+ *   the slots like over compute nodes (id % G, read_data.hh:57-58); no collective is on the query path. */
+#define SHINE_PLACE_REPLICA 0
+#define SHINE_PLACE_SHARDED 1
 
 /* Open the index from the memory nodes' dumps `index_m{M}_efc{efC}_node{i}_of{N}.dat`, i = 1..N, in that
  * order (replaces MemoryNode::store_or_load_index, memory_node.hh:130-209, plus the token/EP distribution,
@@ -85,6 +100,14 @@ int shine_open(const char* const* dump_paths, uint32_t n_dumps, uint32_t dim, ui
 /* Same, from dump images already in host memory (e.g. produced by shine_build). */
 int shine_open_buffers(const uint8_t* const* dumps, const uint64_t* sizes, uint32_t n_dumps, uint32_t dim,
                        uint32_t M, int metric, int elem, const int* gpu_ids, uint32_t n_gpus, shine_index_t* out);
+
+/* shine_open / shine_open_buffers with an explicit placement (SHINE_PLACE_*).  gpu_ids may repeat a device (e.g.
+ * {0, 0}): each slot then owns its own stripe on that device, which exercises the sharded layout on one GPU. */
+int shine_open_ex(const char* const* dump_paths, uint32_t n_dumps, uint32_t dim, uint32_t M, int metric, int elem,
+                  const int* gpu_ids, uint32_t n_gpus, int placement, shine_index_t* out);
+int shine_open_buffers_ex(const uint8_t* const* dumps, const uint64_t* sizes, uint32_t n_dumps, uint32_t dim,
+                          uint32_t M, int metric, int elem, const int* gpu_ids, uint32_t n_gpus, int placement,
+                          shine_index_t* out);
 
 /* knn over a batch of host-resident queries (replaces the WorkerPool::process_queries → hnsw::schedule →
  * HNSW::knn loop, worker_pool.hh:78-89, scheduler.hh:19-102, hnsw.hh:253-307).  queries: nq × dim row-major.

@@ -85,6 +85,14 @@ def test_valid_dump_without_gpu_fails_loudly(small_dumps):
     assert e.value.code == L.ERR_HIP
 
 
+def test_unknown_placement_is_rejected_before_any_device_work(small_dumps):
+    with pytest.raises(shine_amd.ShineError) as e:
+        shine_amd.Index.from_buffers(small_dumps, 128, 8, 0, gpus=[0], placement=7)
+    assert e.value.code == L.ERR_ARG and "placement" in str(e.value)
+    with pytest.raises(ValueError):
+        shine_amd.Index.from_buffers(small_dumps, 128, 8, 0, gpus=[0], placement="striped")
+
+
 def test_missing_file_is_io_error(tmp_path):
     with pytest.raises(shine_amd.ShineError) as e:
         shine_amd.Index.open([tmp_path / "nope.dat"], 128, 8, 0)

@@ -1,0 +1,114 @@
+"""Sharded placement (SHINE_PLACE_SHARDED) against the oracle and against the replica placement.
+
+Memory node s lives on GPU slot s % G only and every slot reads the others' records through one virtual range
+(include/shine_gpu.h).  On a one-GPU box the slots are repeated device ids (gpus=[0, 0, ...]): each slot still
+owns a separate physical stripe and a separate id range, so the id renumbering, the holes between stripes, the
+replicated upper levels / uids and the per-slot query split are all exercised; only the xGMI hop is not.
+Bar: identical ids, bitwise distances and counters to the oracle (exact mode), and identical output to the
+replica placement in every mode.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import shine_amd
+from shine_amd import _lib as L
+from shine_amd import datasets as D
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def four_shards():
+    base = D.sift_like(4000, seed=61)
+    q = D.sift_like(150, seed=62)
+    dumps, _, _ = O.build(base, 8, 48, 0, 4, seed=5)
+    return base, q, dumps
+
+
+@pytest.mark.parametrize("gpus", [[0], [0, 0], [0, 0, 0], [0, 0, 0, 0, 0]])
+def test_sharded_exact_matches_oracle(four_shards, gpus, gpu_available):
+    base, q, dumps = four_shards
+    ref_ids, ref_d, ref_qs = O.OracleIndex(dumps, 128, 8, 0).knn(q, k=10, ef=48)
+    with shine_amd.Index.from_buffers(dumps, 128, 8, 0, gpus=gpus, placement="sharded") as idx:
+        info = idx.info()
+        r = idx.knn(q, 10, 48)
+    assert info["placement"] == L.PLACE_SHARDED and info["n_gpus"] == len(gpus)
+    assert info["num_nodes"] == 4000 and info["id_space"] % len(gpus) == 0 and info["id_space"] >= 4000
+    np.testing.assert_array_equal(r.ids, ref_ids)
+    np.testing.assert_array_equal(r.dists.view(np.uint32), ref_d.view(np.uint32))
+    np.testing.assert_array_equal(r.qstats[:, :5], ref_qs[:, :5])
+    np.testing.assert_array_equal(r.qstats[:, 7], ref_qs[:, 7])
+
+
+@pytest.mark.parametrize("gpus", [[0, 0], [0, 0, 0]])
+def test_sharded_fast_equals_replica_fast(four_shards, gpus, gpu_available):
+    _, q, dumps = four_shards
+    out = {}
+    for placement in ("replica", "sharded"):
+        with shine_amd.Index.from_buffers(dumps, 128, 8, 0, gpus=gpus, placement=placement) as idx:
+            idx.set_search_mode(L.MODE_FAST)
+            out[placement] = idx.knn(q, 10, 64)
+    a, b = out["replica"], out["sharded"]
+    np.testing.assert_array_equal(a.ids, b.ids)
+    np.testing.assert_array_equal(a.dists.view(np.uint32), b.dists.view(np.uint32))
+    np.testing.assert_array_equal(a.qstats, b.qstats)
+
+
+@pytest.mark.parametrize("start_mode", ["1", "2"])
+def test_sharded_fixup_passes(four_shards, start_mode, monkeypatch, gpu_available):
+    """Mode 2 keeps the visited set as a bitmap over the device id space (holes included)."""
+    _, q, dumps = four_shards
+    ref_ids, ref_d, ref_qs = O.OracleIndex(dumps, 128, 8, 0).knn(q[:40], k=10, ef=32)
+    monkeypatch.setenv("SHINE_DEBUG_START_MODE", start_mode)
+    with shine_amd.Index.from_buffers(dumps, 128, 8, 0, gpus=[0, 0], placement="sharded") as idx:
+        r = idx.knn(q[:40], 10, 32)
+    np.testing.assert_array_equal(r.ids, ref_ids)
+    np.testing.assert_array_equal(r.qstats[:, :5], ref_qs[:, :5])
+
+
+def test_sharded_ip_f16_equals_replica(gpu_available):
+    base = D.tti_like(2500, seed=71)
+    q = D.tti_like(80, seed=72)
+    dumps, _, _ = O.build(base, 8, 40, 1, 3, seed=9)
+    out = {}
+    for placement in ("replica", "sharded"):
+        with shine_amd.Index.from_buffers(dumps, 200, 8, 1, elem=L.ELEM_F16, gpus=[0, 0],
+                                          placement=placement) as idx:
+            out[placement] = idx.knn(q, 10, 40)
+    np.testing.assert_array_equal(out["replica"].ids, out["sharded"].ids)
+    np.testing.assert_array_equal(out["replica"].dists.view(np.uint32), out["sharded"].dists.view(np.uint32))
+
+
+def test_sharded_distance_kernel(four_shards, gpu_available):
+    import torch
+    base, q, dumps = four_shards
+    rng = np.random.default_rng(3)
+    uids = rng.integers(0, 4000, (16, 50)).astype(np.uint32)
+    with shine_amd.Index.from_buffers(dumps, 128, 8, 0, gpus=[0, 0], placement="sharded") as idx:
+        for slot in (0, 1):
+            qt = torch.from_numpy(q[:16]).cuda()
+            ut = torch.from_numpy(uids.view(np.int32)).cuda()
+            out = torch.empty((16, 50), dtype=torch.float32, device="cuda")
+            idx.distance_device(qt.data_ptr(), 16, ut.data_ptr(), 50, out.data_ptr(),
+                                stream=torch.cuda.current_stream().cuda_stream, gpu_slot=slot)
+            torch.cuda.synchronize()
+            got = out.cpu().numpy()
+            for i in range(16):
+                for j in range(50):
+                    ref = O.distance(0, q[i], base[uids[i, j]])
+                    assert np.float32(ref).view(np.uint32) == got[i, j].view(np.uint32), (slot, i, j)
+
+
+def test_sharded_device_entry_point_per_slot(four_shards, gpu_available):
+    import torch
+    _, q, dumps = four_shards
+    ref_ids, _, _ = O.OracleIndex(dumps, 128, 8, 0).knn(q[:64], k=10, ef=48)
+    with shine_amd.Index.from_buffers(dumps, 128, 8, 0, gpus=[0, 0], placement="sharded") as idx:
+        for slot in (0, 1):
+            qt = torch.from_numpy(q[:64]).cuda()
+            ids = torch.empty((64, 10), dtype=torch.int32, device="cuda")
+            idx.knn_device(qt.data_ptr(), 64, 10, 48, ids.data_ptr(), None, None,
+                           stream=torch.cuda.current_stream().cuda_stream, gpu_slot=slot)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32), ref_ids)
