@@ -170,24 +170,26 @@ hipMemAllocationProp device_prop(int device) {
   return p;
 }
 
-// Reserve slots × U rows of row_bytes, back slot o's first owned[o] rows with HBM of devs[o], and map the whole
-// range for every device of the handle (peer access over xGMI for the pieces another GPU owns).
+// Reserve slots × U rows of row_bytes, back slot o's U rows with HBM of devs[o] (its first owned[o] rows hold
+// records) and map the whole range for every device of the handle (xGMI peer access for other GPUs' stripes).
 int map_striped(StripedRange& S, uint64_t row_bytes, uint64_t U, const std::vector<uint64_t>& owned,
                 const std::vector<int>& devs, size_t gran) {
   S.bytes = U * row_bytes * devs.size();
   void* va = nullptr;
   HIP_TRY(hipMemAddressReserve(&va, S.bytes, gran, nullptr, 0));
   S.va = static_cast<char*>(va);
+  // Every slot's stripe is one physical allocation of the full stride, so the reservation is mapped without holes
+  // and access is granted once for the whole range (the driver refused per-piece access on ranges with holes).
   for (size_t o = 0; o < devs.size(); ++o) {
-    if (owned[o] == 0) continue;
-    const size_t sz = (owned[o] * row_bytes + gran - 1) / gran * gran;
+    const size_t stride = U * row_bytes;  // a multiple of gran by the choice of U
     const hipMemAllocationProp prop = device_prop(devs[o]);
     hipMemGenericAllocationHandle_t hd{};
-    HIP_TRY(hipMemCreate(&hd, sz, &prop, 0));
+    HIP_TRY(hipMemCreate(&hd, stride, &prop, 0));
     S.handles.push_back(hd);
-    HIP_TRY(hipMemMap(S.va + o * U * row_bytes, sz, 0, hd, 0));
-    S.maps.emplace_back(o * U * row_bytes, sz);
+    HIP_TRY(hipMemMap(S.va + o * stride, stride, 0, hd, 0));
+    S.maps.emplace_back(o * stride, stride);
   }
+  (void)owned;
   std::vector<int> uniq(devs);
   std::sort(uniq.begin(), uniq.end());
   uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
@@ -197,7 +199,10 @@ int map_striped(StripedRange& S, uint64_t row_bytes, uint64_t U, const std::vect
     acc[i].location.id = uniq[i];
     acc[i].flags = hipMemAccessFlagsProtReadWrite;
   }
-  for (auto& m : S.maps) HIP_TRY(hipMemSetAccess(S.va + m.first, m.second, acc.data(), acc.size()));
+  const hipError_t e = hipMemSetAccess(S.va, S.bytes, acc.data(), acc.size());
+  if (e != hipSuccess)
+    return set_error(SHINE_ERR_HIP, std::string("hipMemSetAccess(") + std::to_string(S.bytes) + "-byte range, " +
+                                        std::to_string(S.maps.size()) + " stripes): " + hipGetErrorString(e));
   return 0;
 }
 
@@ -402,9 +407,20 @@ int64_t env_int(const char* name, int64_t dflt) {
 // mode 1: one wavefront per CU with the whole 160 KiB: 16K-entry visited table, larger next queue (fixup).
 // mode 2: one wavefront per CU, visited bitmap in HBM, next queue takes the LDS (fixup).
 // fast (mode 0 of SHINE_MODE_FAST): the sorted list lives in VGPRs, LDS holds only the visited table.
+//   The table is sized for concurrency first: as large as the LDS share of the wavefronts that hold the whole
+//   batch (up to 16 per CU), never below pow2(24·ef) (a query visits ~5-20·ef nodes; one that fills 7/8 of the
+//   table is re-run exactly by the fixup passes) and never above pow2(48·ef).
 LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef) {
   LaunchShape sh{};
-  sh.vis_cap = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(48 * ef)));
+  {
+    const uint32_t want = std::max<uint32_t>(1, std::min<uint32_t>(16, (nq + kCus - 1) / kCus));
+    const int64_t budget = static_cast<int64_t>(kLdsPerCu / want) - static_cast<int64_t>(search_fast_lds_bytes(0));
+    uint32_t fit = 1024;
+    while (static_cast<int64_t>(fit) * 2 * 4 <= budget) fit *= 2;
+    const uint32_t lo = std::min<uint32_t>(8192, std::max<uint32_t>(2048, pow2_at_least(24 * ef)));
+    const uint32_t hi = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(48 * ef)));
+    sh.vis_cap = std::max(lo, std::min(hi, fit));
+  }
   sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
   const uint64_t need = search_fast_lds_bytes(sh.vis_cap);
   const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(kLdsPerCu / need));

@@ -1,0 +1,170 @@
+#!/usr/bin/env python3
+"""Measurement lines for the BASELINE.json configs other than the headline one (bench.py measures configs[1]).
+
+Each workload builds its index in-run (parallel HNSW::insert restatement), keeps queries and outputs in HBM, runs a
+validation pass (status, recall@10 against exact ground truth computed on the GPU), then times K batches with HIP
+events.  One JSON line per workload and search mode is printed and appended to --out.
+
+  cfg3     DEEP-shaped 96-d inner product, ef=256, batch 4096 (configs[2]; N reduced from 10M, see `n`)
+  cfg5     TTI-shaped 200-d inner product, records in fp16, Zipf-skewed query mix (alpha 1.0, skew.py:114-164),
+           ef=250 (scripts/datasets.py: TTI reaches ~95 % at 250) (configs[4]; N reduced from 50M, one GPU)
+  sharded  the bench's SIFT-shaped L2 index as 4 memory-node dumps under SHINE_PLACE_SHARDED over GPU slots [0, 0]
+           (one physical GPU: both stripes are local, so this checks the layout's cost, not xGMI)
+
+Usage: python tools/config_lines.py [--which cfg3,cfg5,sharded] [--n 1000000] [--steps 10]
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "dm-hnsw-reference_amd"))
+sys.path.insert(0, str(ROOT))
+from bench import HBM_PEAK_GBPS, host_threads, log  # noqa: E402
+
+WORKLOADS = {
+    # name: generator, dim, metric, elem, M, efc, ef, batch, shards, placement, gpus
+    "cfg3": ("deep_like", 96, 1, 0, 16, 200, 256, 4096, 1, "replica", [0]),
+    "cfg5": ("tti_like", 200, 1, 1, 16, 200, 250, 1024, 1, "replica", [0]),
+    "sharded": ("sift_like", 128, 0, 0, 16, 200, 128, 1024, 4, "sharded", [0, 0]),
+}
+
+
+def ground_truth(torch, base_t, q_t, k, metric):
+    out = []
+    bn = (base_t * base_t).sum(1) if metric == 0 else None
+    for s in range(0, q_t.shape[0], 256):
+        qq = q_t[s:s + 256]
+        dot = qq @ base_t.T
+        if metric == 0:
+            d = (qq * qq).sum(1)[:, None] + bn[None, :] - 2.0 * dot
+            out.append(torch.topk(d, k, largest=False).indices.cpu().numpy())
+        else:
+            out.append(torch.topk(dot, k, largest=True).indices.cpu().numpy())
+    return np.concatenate(out)
+
+
+def run(name, a):
+    import torch
+    import shine_amd
+    from shine_amd import datasets as D
+    gen, dim, metric, elem, M, efc, ef, batch, shards, placement, gpus = WORKLOADS[name]
+    n = a.n
+    key = hashlib.sha1(f"{name}-{n}-{dim}-{M}-{efc}-{shards}-{gen}-v1".encode()).hexdigest()[:12]
+    cache = Path(a.cache) / key
+    base = getattr(D, gen)(n, seed=1, d=dim)
+    paths = [cache / shine_amd.dump_name(M, efc, i, shards) for i in range(shards)]
+    if not all(p.exists() for p in paths):
+        t0 = time.time()
+        dumps, _ = shine_amd.build(base, M, efc, metric, shards, seed=1234, threads=host_threads())
+        log(f"{name}: built {n} x {dim} in {time.time() - t0:.1f}s")
+        cache.mkdir(parents=True, exist_ok=True)
+        for p, d in zip(paths, dumps):
+            d.tofile(p)
+        del dumps
+    idx = shine_amd.Index.open(paths, dim, M, metric, elem=elem, gpus=gpus, placement=placement)
+    info = idx.info()
+    slots = len(gpus)
+
+    nb = a.nbatches
+    if name == "cfg5":  # Zipf-skewed replay of a query pool (skew.py), alpha 1.0
+        pool = getattr(D, gen)(50_000, seed=2, d=dim)
+        q, _, _ = D.zipf_query_mix(pool, batch * nb, 1.0, seed=3)
+        q = np.ascontiguousarray(q)
+    else:
+        q = getattr(D, gen)(batch * nb, seed=2, d=dim)
+    qd = torch.from_numpy(q).cuda()
+    gt = ground_truth(torch, torch.from_numpy(base).cuda(), qd, a.k, metric)
+    torch.cuda.empty_cache()
+    ids = torch.empty((nb, batch, a.k), dtype=torch.int32, device="cuda")
+    dists = torch.empty((nb, batch, a.k), dtype=torch.float32, device="cuda")
+    qs = torch.zeros((nb, batch, 8), dtype=torch.int32, device="cuda")
+    streams = [torch.cuda.Stream() for _ in range(slots)]
+    per = batch // slots  # slot s answers rows [s*per, (s+1)*per) of each batch (id % G in the host API)
+
+    def step(i, rec=None):
+        b = i % nb
+        for s in range(slots):
+            lo, hi = s * per, (s + 1) * per if s < slots - 1 else batch
+            if rec is not None:
+                rec[s][0].record(streams[s])
+            idx.knn_device(qd[b * batch + lo:b * batch + hi].data_ptr(), hi - lo, a.k, ef, ids[b, lo:hi].data_ptr(),
+                           dists[b, lo:hi].data_ptr(), qs[b, lo:hi].data_ptr(), stream=streams[s].cuda_stream,
+                           gpu_slot=s)
+            if rec is not None:
+                rec[s][1].record(streams[s])
+
+    lines = []
+    for mode_name, mode in (("fast", shine_amd.MODE_FAST), ("exact", shine_amd.MODE_EXACT)):
+        idx.set_search_mode(mode)
+        for i in range(nb):
+            step(i)
+        torch.cuda.synchronize()
+        qs_h = qs.cpu().numpy().view(np.uint32).reshape(-1, 8).copy()
+        bad = int((qs_h[:, 6] != 0).sum())
+        res = ids.cpu().numpy().view(np.uint32).reshape(-1, a.k)
+        recall = D.recall_at_k(res, gt, a.k)
+        bq = [idx.algorithmic_bytes(qs_h[b * batch:(b + 1) * batch]) for b in range(nb)]
+        for i in range(a.warmup):
+            step(i)
+        torch.cuda.synchronize()
+        evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(slots)]
+               for _ in range(a.steps)]
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            step(a.warmup + i, evs[i])
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        kern = [max(s.elapsed_time(e) for s, e in ev) for ev in evs]  # the slots run concurrently
+        byts = [bq[(a.warmup + i) % nb] for i in range(a.steps)]
+        achieved = sum(byts) / (sum(kern) / 1e3) / 1e9
+        line = {
+            "workload": name, "search_mode": mode_name, "value": a.steps * batch / el, "unit": "queries/s",
+            "ms_per_batch": el * 1e3 / a.steps, "avg_launch_ms": float(np.mean(kern)), "recall_at_10": recall,
+            "failed_queries": bad, "mean_distcomps": float(qs_h[:, 0].mean()),
+            "queries_with_ties": float((qs_h[:, 5] > 0).mean()) if mode_name == "fast" else None,
+            "dtype": "f16 records, f32 accumulate" if elem else "f32",
+            "config": {"generator": gen, "n": n, "dim": dim, "metric": "IP" if metric else "L2", "M": M, "efc": efc,
+                       "ef": ef, "k": a.k, "batch": batch, "shards": shards, "placement": placement, "gpu_slots": gpus,
+                       "device_bytes_per_gpu": info["device_bytes"], "id_space": info["id_space"]},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS, "algorithmic_bytes_per_batch": float(np.mean(byts))},
+            "data": "synthetic, random-seeded; index built in-run",
+        }
+        log(json.dumps(line))
+        lines.append(line)
+    idx.close()
+    return lines
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--which", default="cfg3,cfg5,sharded")
+    p.add_argument("--n", type=int, default=1_000_000)
+    p.add_argument("--k", type=int, default=10)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--nbatches", type=int, default=4)
+    p.add_argument("--cache", default=os.environ.get("SHINE_CFG_CACHE", "/tmp/shine_cfg"))
+    p.add_argument("--out", default=str(ROOT / "gpurun_out" / "config_lines.jsonl"))
+    a = p.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    Path(a.out).parent.mkdir(parents=True, exist_ok=True)
+    for name in a.which.split(","):
+        for line in run(name, a):
+            print(json.dumps(line), flush=True)
+            with open(a.out, "a") as f:
+                f.write(json.dumps(line) + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -64,5 +64,11 @@ int main() {
   trial("2 pieces 1024000 B, stride 1 MiB, reserve aligned 4KB", 1 << 20, 1024000, 2, false, 4096);
   trial("2 pieces 4MB, stride 4MB, reserve aligned 2MB", 2 * MB2, 2 * MB2, 2, false, MB2);
   trial("2 pieces 131072 B contiguous", 131072, 131072, 2, false);
+  trial("1 piece 256 MiB", size_t(256) << 20, size_t(256) << 20, 1, false, MB2);
+  trial("2 pieces 256 MiB, stride 260 MiB, reserve aligned 2MB", size_t(260) << 20, size_t(256) << 20, 2, false, MB2);
+  trial("2 pieces 64 MiB, stride 64 MiB", size_t(64) << 20, size_t(64) << 20, 2, false, MB2);
+  trial("2 pieces 64 MiB, stride 66 MiB", size_t(66) << 20, size_t(64) << 20, 2, false, MB2);
+  trial("2 pieces 32 MiB, stride 34 MiB", size_t(34) << 20, size_t(32) << 20, 2, false, MB2);
+  trial("2 pieces 4 MiB, stride 6 MiB", size_t(6) << 20, size_t(4) << 20, 2, false, MB2);
   return 0;
 }
