@@ -35,6 +35,8 @@ WORKLOADS = {
     "cfg3": ("deep_like", 96, 1, 0, 16, 200, 256, 4096, 1, "replica", [0]),
     "cfg5": ("tti_like", 200, 1, 1, 16, 200, 250, 1024, 1, "replica", [0]),
     "sharded": ("sift_like", 128, 0, 0, 16, 200, 128, 1024, 4, "sharded", [0, 0]),
+    "sharded1": ("sift_like", 128, 0, 0, 16, 200, 128, 1024, 4, "sharded", [0]),   # one slot: the VM layout alone
+    "replica4": ("sift_like", 128, 0, 0, 16, 200, 128, 1024, 4, "replica", [0]),   # same 4 dumps, plain HBM
 }
 
 
@@ -58,7 +60,7 @@ def run(name, a):
     from shine_amd import datasets as D
     gen, dim, metric, elem, M, efc, ef, batch, shards, placement, gpus = WORKLOADS[name]
     n = a.n
-    key = hashlib.sha1(f"{name}-{n}-{dim}-{M}-{efc}-{shards}-{gen}-v1".encode()).hexdigest()[:12]
+    key = hashlib.sha1(f"{n}-{dim}-{M}-{efc}-{shards}-{gen}-v1".encode()).hexdigest()[:12]  # shared by layouts
     cache = Path(a.cache) / key
     base = getattr(D, gen)(n, seed=1, d=dim)
     paths = [cache / shine_amd.dump_name(M, efc, i, shards) for i in range(shards)]
