@@ -48,6 +48,37 @@ def host_threads():
         return os.cpu_count() or 1
 
 
+def rank_queries(pool: np.ndarray, rank: int, world: int, n: int) -> np.ndarray:
+    """This rank's queries: ids ≡ rank (mod world) of the common pool, as compute nodes split them
+    (read_data.hh:57-58: id % num_clients == client_id)."""
+    return np.ascontiguousarray(pool[rank::world][:n])
+
+
+def prepare_dumps(paths, rank: int, dist, build):
+    """Rank 0 builds and writes the memory-node dumps (atomically, via rename) unless they exist; every rank waits
+    at a barrier before reading them."""
+    if rank == 0 and not all(p.exists() for p in paths):
+        dumps = build()
+        paths[0].parent.mkdir(parents=True, exist_ok=True)
+        for p, d in zip(paths, dumps):
+            tmp = p.with_suffix(".tmp")
+            d.tofile(tmp)
+            tmp.rename(p)
+        del dumps
+    if dist:
+        dist.barrier()
+
+
+def max_over_ranks(x: float, dist, device: str) -> float:
+    """The job's wall time is the slowest rank's (compute_node.cc:549-556 takes the max over compute nodes)."""
+    if not dist:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -93,20 +124,16 @@ def main():
     base = D.sift_like(a.n, seed=1, d=a.dim)
     log(f"rank {rank}: generated base {base.shape} in {time.time() - t0:.1f}s")
     paths = [cache / "dump" / shine_amd.dump_name(a.M, a.efc, i, a.shards) for i in range(a.shards)]
-    if rank == 0 and not all(p.exists() for p in paths):
+
+    def build():
         t0 = time.time()
         dumps, bdc = shine_amd.build(base, a.M, a.efc, shine_amd.METRIC_L2, a.shards, seed=1234,
                                      threads=host_threads())
         log(f"built index: {sum(d.size for d in dumps) / 2**20:.0f} MiB in {time.time() - t0:.1f}s "
             f"({host_threads()} threads, {bdc} distcomps)")
-        (cache / "dump").mkdir(parents=True, exist_ok=True)
-        for p, d in zip(paths, dumps):
-            tmp = p.with_suffix(".tmp")
-            d.tofile(tmp)
-            tmp.rename(p)
-        del dumps
-    if dist:
-        dist.barrier()
+        return dumps
+
+    prepare_dumps(paths, rank, dist, build)
     idx = shine_amd.Index.open(paths, a.dim, a.M, shine_amd.METRIC_L2, gpus=[local])
     info = idx.info()
     log(f"rank {rank}: index on GPU {local}: {info['num_nodes']} nodes, max level {info['max_level']}, "
@@ -115,7 +142,7 @@ def main():
     # queries: rank r takes ids ≡ r (mod G) of a common pool (read_data.hh:57-58)
     nq_rank = a.batch * a.nbatches
     pool = D.sift_like(nq_rank * world, seed=2, d=a.dim)
-    q = np.ascontiguousarray(pool[rank::world][:nq_rank])
+    q = rank_queries(pool, rank, world, nq_rank)
     qd = torch.from_numpy(q).cuda()
     ids = torch.empty((a.nbatches, a.batch, a.k), dtype=torch.int32, device="cuda")
     dists = torch.empty((a.nbatches, a.batch, a.k), dtype=torch.float32, device="cuda")
@@ -173,11 +200,7 @@ def main():
         t1 = time.perf_counter()
         if dist:
             dist.barrier()
-        elapsed = t1 - t0
-        if dist:
-            t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
+        elapsed = max_over_ranks(t1 - t0, dist, "cuda")
         kern_ms = [s.elapsed_time(e) for s, e in evs]
         bytes_steps = [bq_batch[(a.warmup + i) % a.nbatches] for i in range(a.steps)]
         return dict(elapsed=elapsed, kern_ms=kern_ms, bytes_steps=bytes_steps, recall=recall, qs=qs_h, ids=res)
