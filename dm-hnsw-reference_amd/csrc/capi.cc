@@ -78,8 +78,31 @@ struct StripedRange {
   }
 };
 
+// A sharded level-0 array (vectors or lists; SHINE_PLACE_SHARDED).  Slot o owns the rows o*U .. o*U+U-1 of the id
+// space, ordered hottest first, in two physical allocations on its GPU: hot[o] (the first `cached` bytes) and
+// cold[o] (the rest).  Every slot has its own view of the whole id space: its own stripe, local copies of every
+// other slot's hot prefix (copy[o]: the cache of remote records, ≙ cache::Cache, cache.hh:102-311) and the other
+// slots' cold rows mapped to their owners' HBM (xGMI peer reads).  Mappings start at offset 0 of a handle.
+struct ShardedArray {
+  uint64_t stride = 0;  // U * row bytes, a multiple of the VM granularity
+  size_t cached = 0;    // bytes of each stripe that other slots keep local copies of (0 = no cache)
+  std::vector<hipMemGenericAllocationHandle_t> hot, cold, copy;  // [slot]; unused entries stay 0
+  std::vector<StripedRange> view;                                // [slot]
+  void release() {
+    for (auto& v : view) v.release();
+    view.clear();
+    for (auto* hs : {&hot, &cold, &copy})
+      for (auto& hd : *hs)
+        if (hd) (void)hipMemRelease(hd);
+    hot.clear();
+    cold.clear();
+    copy.clear();
+  }
+};
+
 struct Replica {
   int device = 0;
+  uint32_t slot = 0;
   uint32_t pad_node = 0;  // a node of this slot's own stripe (sharded) for the unconditional loads of empty slots
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -108,7 +131,8 @@ struct shine_index {
   int placement = SHINE_PLACE_REPLICA;
   uint64_t id_space = 0;       // device ids are < id_space (sharded: slot o owns [o * ids_per_slot, ...))
   uint64_t ids_per_slot = 0;
-  StripedRange svec, sadj0;    // sharded: level-0 records of all slots in one virtual range
+  ShardedArray svec, sadj0;    // sharded: level-0 vectors and lists
+  double cache_fraction = 0;
   std::vector<Replica> reps;
   std::mutex mu;
 };
@@ -118,8 +142,8 @@ namespace {
 DevGraph dev_graph(const shine_index* h, const Replica& r) {
   DevGraph g{};
   const bool sharded = h->placement == SHINE_PLACE_SHARDED;
-  g.vec = sharded ? static_cast<const void*>(h->svec.va) : r.vec.p;
-  g.adj0 = sharded ? reinterpret_cast<const uint32_t*>(h->sadj0.va) : r.adj0.p;
+  g.vec = sharded ? static_cast<const void*>(h->svec.view[r.slot].va) : r.vec.p;
+  g.adj0 = sharded ? reinterpret_cast<const uint32_t*>(h->sadj0.view[r.slot].va) : r.adj0.p;
   g.uid = r.uid.p;
   g.up_base = r.up_base.p;
   g.adjU = r.adjU.p;
@@ -170,26 +194,23 @@ hipMemAllocationProp device_prop(int device) {
   return p;
 }
 
-// Reserve slots × U rows of row_bytes, back slot o's U rows with HBM of devs[o] (its first owned[o] rows hold
-// records) and map the whole range for every device of the handle (xGMI peer access for other GPUs' stripes).
-int map_striped(StripedRange& S, uint64_t row_bytes, uint64_t U, const std::vector<uint64_t>& owned,
-                const std::vector<int>& devs, size_t gran) {
-  S.bytes = U * row_bytes * devs.size();
-  void* va = nullptr;
-  HIP_TRY(hipMemAddressReserve(&va, S.bytes, gran, nullptr, 0));
-  S.va = static_cast<char*>(va);
-  // Every slot's stripe is one physical allocation of the full stride, so the reservation is mapped without holes
-  // and access is granted once for the whole range (the driver refused per-piece access on ranges with holes).
-  for (size_t o = 0; o < devs.size(); ++o) {
-    const size_t stride = U * row_bytes;  // a multiple of gran by the choice of U
+// Allocate and map one sharded array (see ShardedArray), then fill nothing: the caller writes every slot's stripe
+// through that slot's view and calls fill_copies.  Access is granted once per view, for every device of the handle,
+// over a view without holes (per-piece grants on views with holes were refused by the driver).
+int map_sharded(ShardedArray& A, uint64_t stride, size_t cached, const std::vector<int>& devs, size_t gran) {
+  const size_t G = devs.size();
+  A.stride = stride;
+  A.cached = G > 1 ? std::min<size_t>(cached, stride) : 0;
+  A.hot.assign(G, 0);
+  A.cold.assign(G, 0);
+  A.copy.assign(G * G, 0);  // [o * G + q]: slot o's local copy of slot q's hot prefix
+  for (size_t o = 0; o < G; ++o) {
     const hipMemAllocationProp prop = device_prop(devs[o]);
-    hipMemGenericAllocationHandle_t hd{};
-    HIP_TRY(hipMemCreate(&hd, stride, &prop, 0));
-    S.handles.push_back(hd);
-    HIP_TRY(hipMemMap(S.va + o * stride, stride, 0, hd, 0));
-    S.maps.emplace_back(o * stride, stride);
+    if (A.cached) HIP_TRY(hipMemCreate(&A.hot[o], A.cached, &prop, 0));
+    if (A.cached < stride) HIP_TRY(hipMemCreate(&A.cold[o], stride - A.cached, &prop, 0));
+    for (size_t q = 0; q < G; ++q)
+      if (A.cached && q != o) HIP_TRY(hipMemCreate(&A.copy[o * G + q], A.cached, &prop, 0));
   }
-  (void)owned;
   std::vector<int> uniq(devs);
   std::sort(uniq.begin(), uniq.end());
   uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
@@ -199,18 +220,53 @@ int map_striped(StripedRange& S, uint64_t row_bytes, uint64_t U, const std::vect
     acc[i].location.id = uniq[i];
     acc[i].flags = hipMemAccessFlagsProtReadWrite;
   }
-  const hipError_t e = hipMemSetAccess(S.va, S.bytes, acc.data(), acc.size());
-  if (e != hipSuccess)
-    return set_error(SHINE_ERR_HIP, std::string("hipMemSetAccess(") + std::to_string(S.bytes) + "-byte range, " +
-                                        std::to_string(S.maps.size()) + " stripes): " + hipGetErrorString(e));
+  A.view.resize(G);
+  for (size_t o = 0; o < G; ++o) {
+    StripedRange& V = A.view[o];
+    V.bytes = G * stride;
+    void* va = nullptr;
+    HIP_TRY(hipMemAddressReserve(&va, V.bytes, gran, nullptr, 0));
+    V.va = static_cast<char*>(va);
+    for (size_t q = 0; q < G; ++q) {
+      const size_t base = q * stride;
+      if (A.cached) {  // hot prefix: the owner's memory in its own view, a local copy in every other view
+        HIP_TRY(hipMemMap(V.va + base, A.cached, 0, q == o ? A.hot[q] : A.copy[o * G + q], 0));
+        V.maps.emplace_back(base, A.cached);
+      }
+      if (A.cached < stride) {
+        HIP_TRY(hipMemMap(V.va + base + A.cached, stride - A.cached, 0, A.cold[q], 0));
+        V.maps.emplace_back(base + A.cached, stride - A.cached);
+      }
+    }
+    const hipError_t e = hipMemSetAccess(V.va, V.bytes, acc.data(), acc.size());
+    if (e != hipSuccess)
+      return set_error(SHINE_ERR_HIP, std::string("hipMemSetAccess(") + std::to_string(V.bytes) + "-byte view, " +
+                                          std::to_string(V.maps.size()) + " pieces): " + hipGetErrorString(e));
+  }
   return 0;
 }
 
-int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus, int placement, shine_index_t* out) {
+// Refresh every slot's local copies of the other slots' hot prefixes from the owners' stripes.
+int fill_copies(ShardedArray& A, const std::vector<int>& devs) {
+  const size_t G = devs.size();
+  if (!A.cached) return 0;
+  for (size_t o = 0; o < G; ++o) {
+    HIP_TRY(hipSetDevice(devs[o]));
+    for (size_t q = 0; q < G; ++q)
+      if (q != o)
+        HIP_TRY(hipMemcpy(A.view[o].va + q * A.stride, A.view[q].va + q * A.stride, A.cached, hipMemcpyDeviceToDevice));
+  }
+  return 0;
+}
+
+int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus, int placement, double cache_fraction,
+               shine_index_t* out) {
   if (!out) return set_error(SHINE_ERR_ARG, "out is NULL");
   if (elem != SHINE_ELEM_F32 && elem != SHINE_ELEM_F16) return set_error(SHINE_ERR_ARG, "elem must be 0 (f32) or 1 (f16)");
   if (placement != SHINE_PLACE_REPLICA && placement != SHINE_PLACE_SHARDED)
     return set_error(SHINE_ERR_ARG, "placement must be SHINE_PLACE_REPLICA or SHINE_PLACE_SHARDED");
+  if (!(cache_fraction >= 0.0 && cache_fraction <= 1.0))
+    return set_error(SHINE_ERR_ARG, "cache fraction must be in [0, 1]");
   if (!dim_supported(G.L.dim, elem))
     return set_error(SHINE_ERR_ARG, "dim " + std::to_string(G.L.dim) + " has no compiled kernel for this element type");
   int ndev = 0;
@@ -250,8 +306,9 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
   const std::vector<uint64_t>& start = G.shard_start;
 
   // Device id space.  Replica: graph.cc's dense ids.  Sharded: slot o = s % slots owns memory node s; its records
-  // are numbered o * U + (records of its earlier memory nodes) + position, with U a whole number of VM pages of
-  // rows, so that every slot's stripe starts on its own pages of the shared virtual range.
+  // are numbered o * U + rank, hottest first (upper-level nodes by level, then by level-0 in-degree: a static form
+  // of the reference's cache admission, upper levels always, cache.hh:368), with U a whole number of VM pages of
+  // rows, so that every slot's stripe starts on its own pages and its hot prefix is a page range.
   std::vector<uint64_t> first(S), owned(slots, 0);
   uint64_t U = G.N;
   size_t gran = 0;
@@ -282,10 +339,21 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
   h->ids_per_slot = U;
   h->words_per_slot = (id_space + 31) / 32;
   std::vector<uint32_t> newid;
+  std::vector<std::vector<uint32_t>> order(sharded ? slots : 0);  // [slot]: old ids, hottest first
   if (sharded) {
+    std::vector<uint32_t> indeg(G.N, 0);
+    for (uint32_t x : G.adj0)
+      if (x != kInvalid) ++indeg[x];
     newid.resize(G.N);
     for (uint32_t s = 0; s < S; ++s)
-      for (uint64_t g = start[s]; g < start[s + 1]; ++g) newid[g] = static_cast<uint32_t>(first[s] + (g - start[s]));
+      for (uint64_t g = start[s]; g < start[s + 1]; ++g) order[s % slots].push_back(static_cast<uint32_t>(g));
+    for (uint32_t o = 0; o < slots; ++o) {
+      std::stable_sort(order[o].begin(), order[o].end(), [&](uint32_t a, uint32_t b) {
+        if (G.level[a] != G.level[b]) return G.level[a] > G.level[b];
+        return indeg[a] > indeg[b];
+      });
+      for (size_t i = 0; i < order[o].size(); ++i) newid[order[o][i]] = static_cast<uint32_t>(o * U + i);
+    }
   }
   auto dev_id = [&](uint32_t g) -> uint32_t { return (!sharded || g == kInvalid) ? g : newid[g]; };
   h->ep = dev_id(G.ep);
@@ -344,6 +412,7 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
   for (uint32_t r = 0; r < slots; ++r) {
     Replica& R = h->reps[r];
     R.device = devs[r];
+    R.slot = r;
     R.pad_node = sharded && owned[r] > 0 ? static_cast<uint32_t>(r * U) : pad_default;
     HIP_TRY(hipSetDevice(R.device));
     HIP_TRY(hipStreamCreateWithFlags(&R.stream, hipStreamNonBlocking));
@@ -362,21 +431,32 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
   }
   const uint64_t replicated = 4 * (uid_d->size() + upb_d->size() + adjU_d->size() + inv.size());
   if (sharded) {
-    if (int rc = map_striped(h->svec, vrow, U, owned, devs, gran)) return rc;
-    if (int rc = map_striped(h->sadj0, arow, U, owned, devs, gran)) return rc;
+    // the cached prefix of every stripe, in whole VM pages of both arrays (rows of the two arrays stay aligned)
+    uint64_t crows = static_cast<uint64_t>(cache_fraction * static_cast<double>(U) + 0.5);
+    uint64_t step = 1;
+    while ((step * vrow) % gran != 0 || (step * arow) % gran != 0) step <<= 1;
+    crows = std::min<uint64_t>(U, (crows + step - 1) / step * step);
+    h->cache_fraction = static_cast<double>(crows) / static_cast<double>(U);
+    if (int rc = map_sharded(h->svec, U * vrow, crows * vrow, devs, gran)) return rc;
+    if (int rc = map_sharded(h->sadj0, U * arow, crows * arow, devs, gran)) return rc;
+    std::vector<uint8_t> vb;
     std::vector<uint32_t> rows;
-    for (uint32_t s = 0; s < S; ++s) {
-      const uint64_t n_s = start[s + 1] - start[s];
-      if (n_s == 0) continue;
-      HIP_TRY(hipSetDevice(devs[s % slots]));
-      HIP_TRY(hipMemcpy(h->svec.va + first[s] * vrow, vsrc + start[s] * vrow, n_s * vrow, hipMemcpyHostToDevice));
-      rows.resize(n_s * M0);
-      for (uint64_t i = 0; i < n_s * M0; ++i) rows[i] = dev_id(G.adj0[start[s] * M0 + i]);
-      HIP_TRY(hipMemcpy(h->sadj0.va + first[s] * arow, rows.data(), n_s * arow, hipMemcpyHostToDevice));
+    for (uint32_t o = 0; o < slots; ++o) {
+      const auto& ord = order[o];
+      if (ord.empty()) continue;
+      vb.resize(ord.size() * vrow);
+      rows.resize(ord.size() * M0);
+      for (size_t i = 0; i < ord.size(); ++i) {
+        std::memcpy(&vb[i * vrow], vsrc + static_cast<uint64_t>(ord[i]) * vrow, vrow);
+        for (uint32_t j = 0; j < M0; ++j) rows[i * M0 + j] = dev_id(G.adj0[static_cast<uint64_t>(ord[i]) * M0 + j]);
+      }
+      HIP_TRY(hipSetDevice(devs[o]));  // through slot o's own view: its stripe is local there
+      HIP_TRY(hipMemcpy(h->svec.view[o].va + o * U * vrow, vb.data(), vb.size(), hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(h->sadj0.view[o].va + o * U * arow, rows.data(), rows.size() * 4, hipMemcpyHostToDevice));
     }
-    uint64_t most = 0;
-    for (uint32_t o = 0; o < slots; ++o) most = std::max(most, owned[o]);
-    h->device_bytes = most * (vrow + arow) + replicated;
+    if (int rc = fill_copies(h->svec, devs)) return rc;
+    if (int rc = fill_copies(h->sadj0, devs)) return rc;
+    h->device_bytes = U * (vrow + arow) + (slots - 1) * crows * (vrow + arow) + replicated;
   } else {
     h->device_bytes = vlen + 4 * G.adj0.size() + replicated;
   }
@@ -552,16 +632,16 @@ const char* shine_last_error(void) { return last_error(); }
 
 int shine_open_buffers_ex(const uint8_t* const* dumps, const uint64_t* sizes, uint32_t n_dumps, uint32_t dim,
                           uint32_t M, int metric, int elem, const int* gpu_ids, uint32_t n_gpus, int placement,
-                          shine_index_t* out) {
+                          double cache_fraction, shine_index_t* out) {
   if (!dumps || !sizes) return set_error(SHINE_ERR_ARG, "dumps / sizes is NULL");
   if (metric != SHINE_METRIC_L2 && metric != SHINE_METRIC_IP) return set_error(SHINE_ERR_ARG, "metric must be 0 or 1");
   HostGraph G;
   if (int rc = parse_dumps(dumps, sizes, n_dumps, dim, M, metric, 0, G)) return rc;
-  return make_index(G, elem, gpu_ids, n_gpus, placement, out);
+  return make_index(G, elem, gpu_ids, n_gpus, placement, cache_fraction, out);
 }
 
 int shine_open_ex(const char* const* dump_paths, uint32_t n_dumps, uint32_t dim, uint32_t M, int metric, int elem,
-                  const int* gpu_ids, uint32_t n_gpus, int placement, shine_index_t* out) {
+                  const int* gpu_ids, uint32_t n_gpus, int placement, double cache_fraction, shine_index_t* out) {
   if (!dump_paths || n_dumps == 0) return set_error(SHINE_ERR_ARG, "no dump paths");
   std::vector<std::vector<uint8_t>> files(n_dumps);
   std::vector<const uint8_t*> ptrs(n_dumps);
@@ -573,17 +653,18 @@ int shine_open_ex(const char* const* dump_paths, uint32_t n_dumps, uint32_t dim,
     sizes[i] = files[i].size();
   }
   return shine_open_buffers_ex(ptrs.data(), sizes.data(), n_dumps, dim, M, metric, elem, gpu_ids, n_gpus, placement,
-                               out);
+                               cache_fraction, out);
 }
 
 int shine_open_buffers(const uint8_t* const* dumps, const uint64_t* sizes, uint32_t n_dumps, uint32_t dim,
                        uint32_t M, int metric, int elem, const int* gpu_ids, uint32_t n_gpus, shine_index_t* out) {
-  return shine_open_buffers_ex(dumps, sizes, n_dumps, dim, M, metric, elem, gpu_ids, n_gpus, SHINE_PLACE_REPLICA, out);
+  return shine_open_buffers_ex(dumps, sizes, n_dumps, dim, M, metric, elem, gpu_ids, n_gpus, SHINE_PLACE_REPLICA, 0.0,
+                               out);
 }
 
 int shine_open(const char* const* dump_paths, uint32_t n_dumps, uint32_t dim, uint32_t M, int metric, int elem,
                const int* gpu_ids, uint32_t n_gpus, shine_index_t* out) {
-  return shine_open_ex(dump_paths, n_dumps, dim, M, metric, elem, gpu_ids, n_gpus, SHINE_PLACE_REPLICA, out);
+  return shine_open_ex(dump_paths, n_dumps, dim, M, metric, elem, gpu_ids, n_gpus, SHINE_PLACE_REPLICA, 0.0, out);
 }
 
 int shine_set_search_mode(shine_index_t h, int mode) {
@@ -612,6 +693,7 @@ int shine_index_get_info(shine_index_t h, shine_index_info* o) {
   o->n_gpus = static_cast<uint32_t>(h->reps.size());
   o->placement = static_cast<uint32_t>(h->placement);
   o->id_space = h->id_space;
+  o->cache_fraction = h->cache_fraction;
   return SHINE_OK;
 }
 

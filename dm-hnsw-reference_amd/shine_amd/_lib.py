@@ -64,6 +64,7 @@ class IndexInfo(C.Structure):
         ("placement", C.c_uint32),
         ("reserved0", C.c_uint32),
         ("id_space", C.c_uint64),
+        ("cache_fraction", C.c_double),
     ]
 
     def as_dict(self) -> dict:
@@ -79,9 +80,10 @@ PROTOTYPES = {
     "shine_open": (I32, [C.POINTER(C.c_char_p), U32, U32, U32, I32, I32, C.POINTER(I32), U32, C.POINTER(P)]),
     "shine_open_buffers": (I32, [C.POINTER(PU8), C.POINTER(U64), U32, U32, U32, I32, I32, C.POINTER(I32), U32,
                                  C.POINTER(P)]),
-    "shine_open_ex": (I32, [C.POINTER(C.c_char_p), U32, U32, U32, I32, I32, C.POINTER(I32), U32, I32, C.POINTER(P)]),
+    "shine_open_ex": (I32, [C.POINTER(C.c_char_p), U32, U32, U32, I32, I32, C.POINTER(I32), U32, I32, C.c_double,
+                            C.POINTER(P)]),
     "shine_open_buffers_ex": (I32, [C.POINTER(PU8), C.POINTER(U64), U32, U32, U32, I32, I32, C.POINTER(I32), U32, I32,
-                                    C.POINTER(P)]),
+                                    C.c_double, C.POINTER(P)]),
     "shine_knn_batch": (I32, [P, P, U32, U32, U32, P, P, P, C.POINTER(Stats)]),
     "shine_knn_batch_device": (I32, [P, U32, P, U32, U32, U32, P, P, P, P]),
     "shine_distance_batch_device": (I32, [P, U32, P, U32, P, U32, P, P]),

@@ -53,19 +53,20 @@ class Index:
     # ---- construction ----------------------------------------------------------------------------------
     @classmethod
     def open(cls, dump_paths, dim: int, M: int, metric: int = L.METRIC_L2, elem: int = L.ELEM_F32, gpus=None,
-             placement: str = "replica"):
+             placement: str = "replica", cache: float = 0.0):
         """placement "replica": every GPU holds the whole index; "sharded": memory node s lives on GPU slot
-        s % len(gpus) only and the others read it over xGMI (include/shine_gpu.h, SHINE_PLACE_SHARDED)."""
+        s % len(gpus) only and the others read it over xGMI (include/shine_gpu.h, SHINE_PLACE_SHARDED).
+        cache (sharded): share of every other slot's records, hottest first, each GPU keeps local copies of."""
         arr = (C.c_char_p * len(dump_paths))(*[str(p).encode() for p in dump_paths])
         g, ng = _gpus(gpus)
         h = C.c_void_p()
         L.check(L.lib().shine_open_ex(arr, len(dump_paths), dim, M, metric, elem, g, ng, _placement(placement),
-                                      C.byref(h)))
+                                      float(cache), C.byref(h)))
         return cls(h.value, dim, metric)
 
     @classmethod
     def from_buffers(cls, dumps, dim: int, M: int, metric: int = L.METRIC_L2, elem: int = L.ELEM_F32, gpus=None,
-                     placement: str = "replica"):
+                     placement: str = "replica", cache: float = 0.0):
         dumps = [np.ascontiguousarray(np.frombuffer(d, dtype=np.uint8) if not isinstance(d, np.ndarray) else d,
                                       dtype=np.uint8) for d in dumps]
         ptrs = (C.POINTER(C.c_uint8) * len(dumps))(*[d.ctypes.data_as(C.POINTER(C.c_uint8)) for d in dumps])
@@ -73,7 +74,7 @@ class Index:
         g, ng = _gpus(gpus)
         h = C.c_void_p()
         L.check(L.lib().shine_open_buffers_ex(ptrs, sizes, len(dumps), dim, M, metric, elem, g, ng,
-                                              _placement(placement), C.byref(h)))
+                                              _placement(placement), float(cache), C.byref(h)))
         return cls(h.value, dim, metric)
 
     def close(self):

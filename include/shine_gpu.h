@@ -75,15 +75,16 @@ typedef struct shine_index_info {
   uint32_t placement;      /* SHINE_PLACE_* */
   uint32_t reserved0;
   uint64_t id_space;       /* device node-id range: num_nodes (replica) or n_gpus x ids_per_gpu (sharded) */
+  double cache_fraction;   /* sharded: share of every other GPU's records held in local HBM copies */
 } shine_index_info;
 
 /* Placement of the records over the GPUs of a handle.
  * REPLICA: every GPU holds the whole index (the bench metric's index fits one GPU).
  * SHARDED: memory node s (dump s+1) lives in the HBM of GPU slot s % n_gpus only, as the reference places records
- *   on memory nodes (RemotePtr bits 63..48, remote_pointer.hh:9-22, rdma_atomics.hh:89).  The level-0 records
- *   (vectors and lists) of all slots form one virtual range mapped on every GPU (HIP virtual memory, peer access
- *   over xGMI): a search dereferences any record directly, local or remote, the way read_node / read_neighborlist
- *   dereference a RemotePtr (rdma_reads.hh:9-72).  Upper-level lists, uids and the entry point are replicated
+ *   on memory nodes (RemotePtr bits 63..48, remote_pointer.hh:9-22, rdma_atomics.hh:89).  Every GPU maps the
+ *   level-0 records (vectors and lists) of all slots into one virtual range of its own (HIP virtual memory, peer
+ *   access over xGMI): a search dereferences any record directly, local or remote, the way read_node /
+ *   read_neighborlist dereference a RemotePtr (rdma_reads.hh:9-72).  Upper-level lists, uids and the entry point are replicated
  *   (about 1/M of the index; the reference's read_entry_point_ptr, rdma_reads.hh:74-99).  Queries are split over
  *   the slots like over compute nodes (id % G, read_data.hh:57-58); no collective is on the query path. */
 #define SHINE_PLACE_REPLICA 0
@@ -102,12 +103,17 @@ int shine_open_buffers(const uint8_t* const* dumps, const uint64_t* sizes, uint3
                        uint32_t M, int metric, int elem, const int* gpu_ids, uint32_t n_gpus, shine_index_t* out);
 
 /* shine_open / shine_open_buffers with an explicit placement (SHINE_PLACE_*).  gpu_ids may repeat a device (e.g.
- * {0, 0}): each slot then owns its own stripe on that device, which exercises the sharded layout on one GPU. */
+ * {0, 0}): each slot then owns its own stripe on that device, which exercises the sharded layout on one GPU.
+ * cache_fraction (sharded only, in [0, 1]; rounded to whole 2 MiB pages) replaces the compute node's record cache
+ * (cache::Cache, cache.hh:102-311, sized as a share of the index, compute_node.cc:40-56): each slot's records are
+ * ordered hottest first (upper-level nodes, then level-0 in-degree; the reference always admits upper levels,
+ * cache.hh:368) and every GPU keeps local copies of that leading share of every other GPU's records, so those
+ * reads stay in local HBM instead of crossing xGMI.  Results do not depend on it. */
 int shine_open_ex(const char* const* dump_paths, uint32_t n_dumps, uint32_t dim, uint32_t M, int metric, int elem,
-                  const int* gpu_ids, uint32_t n_gpus, int placement, shine_index_t* out);
+                  const int* gpu_ids, uint32_t n_gpus, int placement, double cache_fraction, shine_index_t* out);
 int shine_open_buffers_ex(const uint8_t* const* dumps, const uint64_t* sizes, uint32_t n_dumps, uint32_t dim,
                           uint32_t M, int metric, int elem, const int* gpu_ids, uint32_t n_gpus, int placement,
-                          shine_index_t* out);
+                          double cache_fraction, shine_index_t* out);
 
 /* knn over a batch of host-resident queries (replaces the WorkerPool::process_queries → hnsw::schedule →
  * HNSW::knn loop, worker_pool.hh:78-89, scheduler.hh:19-102, hnsw.hh:253-307).  queries: nq × dim row-major.

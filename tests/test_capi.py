@@ -93,6 +93,13 @@ def test_unknown_placement_is_rejected_before_any_device_work(small_dumps):
         shine_amd.Index.from_buffers(small_dumps, 128, 8, 0, gpus=[0], placement="striped")
 
 
+def test_cache_fraction_outside_unit_interval_is_rejected(small_dumps):
+    for bad in (-0.1, 1.5, float("nan")):
+        with pytest.raises(shine_amd.ShineError) as e:
+            shine_amd.Index.from_buffers(small_dumps, 128, 8, 0, gpus=[0], placement="sharded", cache=bad)
+        assert e.value.code == L.ERR_ARG and "cache" in str(e.value)
+
+
 def test_missing_file_is_io_error(tmp_path):
     with pytest.raises(shine_amd.ShineError) as e:
         shine_amd.Index.open([tmp_path / "nope.dat"], 128, 8, 0)

@@ -112,3 +112,43 @@ def test_sharded_device_entry_point_per_slot(four_shards, gpu_available):
                            stream=torch.cuda.current_stream().cuda_stream, gpu_slot=slot)
             torch.cuda.synchronize()
             np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32), ref_ids)
+
+
+@pytest.mark.parametrize("gpus,cache", [([0, 0], 0.5), ([0, 0, 0], 1.0), ([0, 0, 0], 0.2)])
+def test_sharded_cache_changes_nothing_but_placement(four_shards, gpus, cache, gpu_available):
+    """Local copies of the other slots' hottest records (SHINE cache row): same ids, distances and counters."""
+    _, q, dumps = four_shards
+    ref_ids, ref_d, ref_qs = O.OracleIndex(dumps, 128, 8, 0).knn(q, k=10, ef=48)
+    with shine_amd.Index.from_buffers(dumps, 128, 8, 0, gpus=gpus, placement="sharded", cache=cache) as idx:
+        info = idx.info()
+        r = idx.knn(q, 10, 48)
+        idx.set_search_mode(L.MODE_FAST)
+        f = idx.knn(q, 10, 48)
+    assert 0.0 < info["cache_fraction"] <= 1.0
+    np.testing.assert_array_equal(r.ids, ref_ids)
+    np.testing.assert_array_equal(r.dists.view(np.uint32), ref_d.view(np.uint32))
+    np.testing.assert_array_equal(r.qstats[:, :5], ref_qs[:, :5])
+    with shine_amd.Index.from_buffers(dumps, 128, 8, 0, gpus=gpus, placement="replica") as idx:
+        idx.set_search_mode(L.MODE_FAST)
+        g = idx.knn(q, 10, 48)
+    np.testing.assert_array_equal(f.ids, g.ids)
+    np.testing.assert_array_equal(f.qstats, g.qstats)
+
+
+def test_sharded_partial_cache_on_a_larger_index(gpu_available):
+    """80K records over 2 slots (M=8: a page step is 32768 rows), so each stripe spans two steps and a 0.5 cache
+    maps a hot prefix from local copies and the cold rest from the owner, both kinds of piece in one view.  Must
+    equal the replica exactly."""
+    base = D.sift_like(80000, seed=81)
+    q = D.sift_like(200, seed=82)
+    dumps, _ = shine_amd.build(base, 8, 40, 0, 2, seed=6, threads=8)
+    out = {}
+    for placement, cache in (("replica", 0.0), ("sharded", 0.5)):
+        with shine_amd.Index.from_buffers(dumps, 128, 8, 0, gpus=[0, 0], placement=placement, cache=cache) as idx:
+            if placement == "sharded":
+                assert idx.info()["cache_fraction"] == 0.5
+            out[placement] = idx.knn(q, 10, 40)
+    a, b = out["replica"], out["sharded"]
+    np.testing.assert_array_equal(a.ids, b.ids)
+    np.testing.assert_array_equal(a.dists.view(np.uint32), b.dists.view(np.uint32))
+    np.testing.assert_array_equal(a.qstats, b.qstats)
