@@ -20,6 +20,7 @@
 #include "../../include/shine_gpu.h"
 #include "graph.h"
 #include "kernels.h"
+#include "placement.h"
 
 using namespace shine;
 
@@ -133,6 +134,7 @@ struct shine_index {
   uint64_t ids_per_slot = 0;
   ShardedArray svec, sadj0;    // sharded: level-0 vectors and lists
   double cache_fraction = 0;
+  Regions regions;             // SHINE_PLACE_SHARDED_REGIONS: slot o owns (and is routed) region o
   std::vector<Replica> reps;
   std::mutex mu;
 };
@@ -141,7 +143,7 @@ namespace {
 
 DevGraph dev_graph(const shine_index* h, const Replica& r) {
   DevGraph g{};
-  const bool sharded = h->placement == SHINE_PLACE_SHARDED;
+  const bool sharded = h->placement != SHINE_PLACE_REPLICA;
   g.vec = sharded ? static_cast<const void*>(h->svec.view[r.slot].va) : r.vec.p;
   g.adj0 = sharded ? reinterpret_cast<const uint32_t*>(h->sadj0.view[r.slot].va) : r.adj0.p;
   g.uid = r.uid.p;
@@ -263,8 +265,8 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
                shine_index_t* out) {
   if (!out) return set_error(SHINE_ERR_ARG, "out is NULL");
   if (elem != SHINE_ELEM_F32 && elem != SHINE_ELEM_F16) return set_error(SHINE_ERR_ARG, "elem must be 0 (f32) or 1 (f16)");
-  if (placement != SHINE_PLACE_REPLICA && placement != SHINE_PLACE_SHARDED)
-    return set_error(SHINE_ERR_ARG, "placement must be SHINE_PLACE_REPLICA or SHINE_PLACE_SHARDED");
+  if (placement != SHINE_PLACE_REPLICA && placement != SHINE_PLACE_SHARDED && placement != SHINE_PLACE_SHARDED_REGIONS)
+    return set_error(SHINE_ERR_ARG, "placement must be one of SHINE_PLACE_REPLICA / _SHARDED / _SHARDED_REGIONS");
   if (!(cache_fraction >= 0.0 && cache_fraction <= 1.0))
     return set_error(SHINE_ERR_ARG, "cache fraction must be in [0, 1]");
   if (!dim_supported(G.L.dim, elem))
@@ -277,7 +279,7 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
   else devs.assign(gpu_ids, gpu_ids + n_gpus);
   for (int d : devs)
     if (d < 0 || d >= ndev) return set_error(SHINE_ERR_ARG, "gpu id " + std::to_string(d) + " out of range");
-  const bool sharded = placement == SHINE_PLACE_SHARDED;
+  const bool sharded = placement != SHINE_PLACE_REPLICA;
 
   std::unique_ptr<shine_index> h(new shine_index);
   struct Guard {  // a failed open releases what it had already placed on the devices
@@ -309,14 +311,20 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
   // are numbered o * U + rank, hottest first (upper-level nodes by level, then by level-0 in-degree: a static form
   // of the reference's cache admission, upper levels always, cache.hh:368), with U a whole number of VM pages of
   // rows, so that every slot's stripe starts on its own pages and its hot prefix is a page range.
-  std::vector<uint64_t> first(S), owned(slots, 0);
+  std::vector<uint64_t> owned(slots, 0);
+  std::vector<std::vector<uint32_t>> order(sharded ? slots : 0);  // [slot]: its records (old ids), hottest first
   uint64_t U = G.N;
   size_t gran = 0;
   if (sharded) {
-    for (uint32_t s = 0; s < S; ++s) {
-      first[s] = owned[s % slots];
-      owned[s % slots] += start[s + 1] - start[s];
+    if (placement == SHINE_PLACE_SHARDED_REGIONS) {  // k-means regions of the top levels (placement.hh:22-61)
+      h->regions = kmeans_regions(G, top_level_sample(G, std::max<uint32_t>(500, 64 * slots)), slots, 0);
+      const std::vector<uint32_t> region = assign_regions(G, h->regions, 0.05, 1);
+      for (uint64_t g = 0; g < G.N; ++g) order[region[g]].push_back(static_cast<uint32_t>(g));
+    } else {
+      for (uint32_t s = 0; s < S; ++s)
+        for (uint64_t g = start[s]; g < start[s + 1]; ++g) order[s % slots].push_back(static_cast<uint32_t>(g));
     }
+    for (uint32_t o = 0; o < slots; ++o) owned[o] = order[o].size();
     for (int d : devs) {
       const hipMemAllocationProp prop = device_prop(d);
       size_t g = 0;
@@ -330,23 +338,17 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
     U = std::max<uint64_t>(unit, (most + unit - 1) / unit * unit);
     if (U * slots >= 0x80000000ull)
       return set_error(SHINE_ERR_ARG, "sharded id space of " + std::to_string(U * slots) + " ids exceeds 2^31");
-    for (uint32_t s = 0; s < S; ++s) first[s] += static_cast<uint64_t>(s % slots) * U;
-  } else {
-    for (uint32_t s = 0; s < S; ++s) first[s] = start[s];
   }
   const uint64_t id_space = sharded ? U * slots : G.N;
   h->id_space = id_space;
   h->ids_per_slot = U;
   h->words_per_slot = (id_space + 31) / 32;
   std::vector<uint32_t> newid;
-  std::vector<std::vector<uint32_t>> order(sharded ? slots : 0);  // [slot]: old ids, hottest first
   if (sharded) {
     std::vector<uint32_t> indeg(G.N, 0);
     for (uint32_t x : G.adj0)
       if (x != kInvalid) ++indeg[x];
     newid.resize(G.N);
-    for (uint32_t s = 0; s < S; ++s)
-      for (uint64_t g = start[s]; g < start[s + 1]; ++g) order[s % slots].push_back(static_cast<uint32_t>(g));
     for (uint32_t o = 0; o < slots; ++o) {
       std::stable_sort(order[o].begin(), order[o].end(), [&](uint32_t a, uint32_t b) {
         if (G.level[a] != G.level[b]) return G.level[a] > G.level[b];
@@ -357,6 +359,13 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
   }
   auto dev_id = [&](uint32_t g) -> uint32_t { return (!sharded || g == kInvalid) ? g : newid[g]; };
   h->ep = dev_id(G.ep);
+  if (sharded) {  // every id a kernel can follow must name a record of its slot (never a hole, never past the space)
+    auto real = [&](uint32_t d) { return d / U < slots && d % U < owned[d / U]; };
+    bool ok = real(h->ep);
+    for (uint32_t x : G.adj0) ok = ok && (x == kInvalid || real(newid[x]));
+    for (uint32_t x : G.adjU) ok = ok && (x == kInvalid || real(newid[x]));
+    if (!ok) return set_error(SHINE_ERR_FORMAT, "sharded layout: a list names an id outside the records");
+  }
 
   // per-node arrays in device order (sharded: holes between the stripes stay kInvalid and are never referenced)
   std::vector<uint32_t> uid_s, upb_s, adjU_s;
@@ -568,6 +577,8 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     }
     SearchArgs a{};
     a.g = dev_graph(h, R);
+    if (!a.g.vec || !a.g.adj0 || !a.g.uid || !a.g.up_base)
+      return set_error(SHINE_ERR_HIP, "search launch: an index array is missing on this GPU slot");
     a.queries = d_q;
     a.nq = nq;
     a.k = k;
@@ -610,6 +621,39 @@ int check_knn_args(shine_index* h, uint32_t k, uint32_t ef) {
   if (ef < k) return set_error(SHINE_ERR_ARG, "ef_search must be >= k");  // hnsw.hh:36
   if (ef > 4096) return set_error(SHINE_ERR_ARG, "ef_search must be <= 4096");
   return 0;
+}
+
+// Debug (SHINE_DEBUG_VALIDATE=1): read every slot's level-0 lists back through that slot's own view and check on the
+// host that each entry names a record of the id space, before any search is launched on the layout.
+int validate_views(shine_index* h) {
+  if (h->placement == SHINE_PLACE_REPLICA) return 0;
+  const uint64_t U = h->ids_per_slot, G = h->reps.size();
+  std::vector<uint32_t> rows(U * h->M0), ub(h->id_space);
+  for (uint64_t r = 0; r < G; ++r) {
+    HIP_TRY(hipSetDevice(h->reps[r].device));
+    HIP_TRY(hipMemcpy(ub.data(), h->reps[r].up_base.p, ub.size() * 4, hipMemcpyDeviceToHost));
+    for (uint64_t o = 0; o < G; ++o) {
+      HIP_TRY(hipMemcpy(rows.data(), h->sadj0.view[r].va + o * h->sadj0.stride, rows.size() * 4, hipMemcpyDeviceToHost));
+      for (uint64_t i = 0; i < rows.size(); ++i) {
+        const uint32_t x = rows[i];
+        if (x != kInvalid && x >= h->id_space)
+          return set_error(SHINE_ERR_FORMAT, "validate: slot " + std::to_string(r) + " sees id " + std::to_string(x) +
+                                                 " in row " + std::to_string(o * U + i / h->M0));
+      }
+    }
+    std::fprintf(stderr, "validate: slot %llu view ok (ep %u, ep up_base %u)\n", static_cast<unsigned long long>(r),
+                 h->ep, ub[h->ep]);
+  }
+  return 0;
+}
+
+void route_batch(const shine_index* h, const float* q, uint32_t nq, uint32_t* out) {
+  const uint32_t G = static_cast<uint32_t>(h->reps.size());
+  if (h->placement == SHINE_PLACE_SHARDED_REGIONS && G > 1) {
+    route_queries(h->regions, q, nq, 0.25, out);  // per-batch limits, query_router.hh:359-372
+    return;
+  }
+  for (uint32_t i = 0; i < nq; ++i) out[i] = i % G;
 }
 
 uint64_t bq_bytes(const shine_index* h, const uint32_t* qs) {  // B_q
@@ -731,10 +775,14 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
   std::lock_guard<std::mutex> lk(h->mu);
   const uint32_t G = static_cast<uint32_t>(h->reps.size());
   const size_t d = h->dim;
-  // queries are split over the replicas round-robin by position, as compute nodes split them by id
-  // (read_data.hh:57-58: id % num_clients == client_id)
+  // queries are split over the slots round-robin by position, as compute nodes split them by id
+  // (read_data.hh:57-58: id % num_clients == client_id); a region-placed index routes them to their region instead
+  if (env_int("SHINE_DEBUG_VALIDATE", 0))
+    if (int rc = validate_views(h)) return rc;
+  std::vector<uint32_t> dest(nq);
+  route_batch(h, queries, nq, dest.data());
   std::vector<std::vector<uint32_t>> part(G);
-  for (uint32_t i = 0; i < nq; ++i) part[i % G].push_back(i);
+  for (uint32_t i = 0; i < nq; ++i) part[dest[i]].push_back(i);
   std::vector<std::vector<float>> qbuf(G);
   std::vector<std::vector<uint32_t>> ibuf(G), sbuf(G);
   std::vector<std::vector<float>> dbuf(G);
@@ -816,6 +864,33 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
   return rc;
 }
 
+int shine_route(shine_index_t h, const float* queries, uint32_t nq, uint32_t* out_slot) {
+  if (!h) return set_error(SHINE_ERR_ARG, "index handle is NULL");
+  if (nq == 0) return SHINE_OK;
+  if (!queries || !out_slot) return set_error(SHINE_ERR_ARG, "NULL host pointer");
+  route_batch(h, queries, nq, out_slot);
+  return SHINE_OK;
+}
+
+int shine_plan_regions(const uint8_t* const* dumps, const uint64_t* sizes, uint32_t n_dumps, uint32_t dim, uint32_t M,
+                       int metric, uint32_t k, uint32_t* region_of_uid, uint64_t uid_capacity, float* centroids) {
+  if (!dumps || !sizes) return set_error(SHINE_ERR_ARG, "dumps / sizes is NULL");
+  if (k == 0) return set_error(SHINE_ERR_ARG, "k must be > 0");
+  if (metric != SHINE_METRIC_L2 && metric != SHINE_METRIC_IP) return set_error(SHINE_ERR_ARG, "metric must be 0 or 1");
+  HostGraph G;
+  if (int rc = parse_dumps(dumps, sizes, n_dumps, dim, M, metric, 0, G)) return rc;
+  const Regions R = kmeans_regions(G, top_level_sample(G, std::max<uint32_t>(500, 64 * k)), k, 0);
+  if (centroids) std::memcpy(centroids, R.centroids.data(), R.centroids.size() * sizeof(float));
+  if (region_of_uid) {
+    const std::vector<uint32_t> region = assign_regions(G, R, 0.05, 1);
+    for (uint64_t g = 0; g < G.N; ++g) {
+      if (G.uid[g] >= uid_capacity) return set_error(SHINE_ERR_ARG, "uid_capacity is below the largest uid + 1");
+      region_of_uid[G.uid[g]] = region[g];
+    }
+  }
+  return SHINE_OK;
+}
+
 int shine_distance_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_queries, uint32_t nq,
                                 const uint32_t* d_node_uids, uint32_t n_per_query, float* d_out, void* stream) {
   if (!h) return set_error(SHINE_ERR_ARG, "index handle is NULL");
@@ -827,6 +902,7 @@ int shine_distance_batch_device(shine_index_t h, uint32_t gpu_slot, const float*
   HIP_TRY(hipSetDevice(R.device));
   DistArgs a{};
   a.g = dev_graph(h, R);
+  if (!a.g.vec || !a.g.inv_uid) return set_error(SHINE_ERR_HIP, "distance launch: an index array is missing");
   a.queries = d_queries;
   a.nq = nq;
   a.node_uids = d_node_uids;

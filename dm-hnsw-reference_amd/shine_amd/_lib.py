@@ -21,7 +21,7 @@ QS_DISTCOMPS, QS_VISITED_UPPER, QS_VISITED_L0, QS_LISTS_UPPER, QS_LISTS_L0, QS_M
 QS_WORDS = 8
 QS_TIES = 5  # fast mode's meaning of word 5
 MODE_EXACT, MODE_FAST = 0, 1
-PLACE_REPLICA, PLACE_SHARDED = 0, 1
+PLACE_REPLICA, PLACE_SHARDED, PLACE_SHARDED_REGIONS = 0, 1, 2
 
 
 class ShineError(RuntimeError):
@@ -87,6 +87,8 @@ PROTOTYPES = {
     "shine_knn_batch": (I32, [P, P, U32, U32, U32, P, P, P, C.POINTER(Stats)]),
     "shine_knn_batch_device": (I32, [P, U32, P, U32, U32, U32, P, P, P, P]),
     "shine_distance_batch_device": (I32, [P, U32, P, U32, P, U32, P, P]),
+    "shine_route": (I32, [P, P, U32, P]),
+    "shine_plan_regions": (I32, [C.POINTER(PU8), C.POINTER(U64), U32, U32, U32, I32, U32, P, U64, P]),
     "shine_set_search_mode": (I32, [P, I32]),
     "shine_index_get_info": (I32, [P, C.POINTER(IndexInfo)]),
     "shine_algorithmic_bytes": (U64, [P, P, U32]),

@@ -19,6 +19,14 @@ def _ptr(a: np.ndarray | None):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
 
 
+def _dump_arrays(dumps):
+    dumps = [np.ascontiguousarray(np.frombuffer(d, dtype=np.uint8) if not isinstance(d, np.ndarray) else d,
+                                  dtype=np.uint8) for d in dumps]
+    ptrs = (C.POINTER(C.c_uint8) * len(dumps))(*[d.ctypes.data_as(C.POINTER(C.c_uint8)) for d in dumps])
+    sizes = (C.c_uint64 * len(dumps))(*[d.size for d in dumps])
+    return dumps, ptrs, sizes
+
+
 def _gpus(gpus):
     if not gpus:
         return None, 0
@@ -30,9 +38,9 @@ def _placement(p) -> int:
     if isinstance(p, int):
         return p
     try:
-        return {"replica": L.PLACE_REPLICA, "sharded": L.PLACE_SHARDED}[p]
+        return {"replica": L.PLACE_REPLICA, "sharded": L.PLACE_SHARDED, "regions": L.PLACE_SHARDED_REGIONS}[p]
     except KeyError:
-        raise ValueError(f"placement must be 'replica' or 'sharded', not {p!r}") from None
+        raise ValueError(f"placement must be 'replica', 'sharded' or 'regions', not {p!r}") from None
 
 
 @dataclass
@@ -67,10 +75,7 @@ class Index:
     @classmethod
     def from_buffers(cls, dumps, dim: int, M: int, metric: int = L.METRIC_L2, elem: int = L.ELEM_F32, gpus=None,
                      placement: str = "replica", cache: float = 0.0):
-        dumps = [np.ascontiguousarray(np.frombuffer(d, dtype=np.uint8) if not isinstance(d, np.ndarray) else d,
-                                      dtype=np.uint8) for d in dumps]
-        ptrs = (C.POINTER(C.c_uint8) * len(dumps))(*[d.ctypes.data_as(C.POINTER(C.c_uint8)) for d in dumps])
-        sizes = (C.c_uint64 * len(dumps))(*[d.size for d in dumps])
+        dumps, ptrs, sizes = _dump_arrays(dumps)
         g, ng = _gpus(gpus)
         h = C.c_void_p()
         L.check(L.lib().shine_open_buffers_ex(ptrs, sizes, len(dumps), dim, M, metric, elem, g, ng,
@@ -134,6 +139,13 @@ class Index:
                                                     n_per, C.c_void_p(out_ptr),
                                                     C.c_void_p(stream) if stream else None))
 
+    def route(self, queries: np.ndarray) -> np.ndarray:
+        """GPU slot of every query of a batch (shine_route): id % n_gpus, or the nearest region with room."""
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        out = np.empty(q.shape[0], dtype=np.uint32)
+        L.check(L.lib().shine_route(self._h, _ptr(q), q.shape[0], _ptr(out)))
+        return out
+
     def algorithmic_bytes(self, qstats: np.ndarray) -> int:
         qs = np.ascontiguousarray(qstats, dtype=np.uint32)
         return int(L.lib().shine_algorithmic_bytes(self._h, _ptr(qs), qs.shape[0]))
@@ -156,6 +168,30 @@ def build(base: np.ndarray, M: int, ef_construction: int, metric: int = L.METRIC
     finally:
         L.lib().shine_build_free(h)
     return dumps, dc
+
+
+def plan_regions(dumps, dim: int, M: int, metric: int, k: int) -> tuple[np.ndarray, np.ndarray]:
+    """Host-only region planner of SHINE_PLACE_SHARDED_REGIONS: (centroids [k, dim], region of every uid)."""
+    dumps, ptrs, sizes = _dump_arrays(dumps)
+    cent = np.empty((k, dim), dtype=np.float32)
+    n_uid = _max_uid(dumps, dim, M) + 1
+    region = np.full(n_uid, 0xFFFFFFFF, dtype=np.uint32)
+    L.check(L.lib().shine_plan_regions(ptrs, sizes, len(dumps), dim, M, metric, k, _ptr(region), n_uid, _ptr(cent)))
+    return cent, region
+
+
+def _max_uid(dumps, dim: int, M: int) -> int:
+    """Largest uid in the dumps (record walk of memory_node.hh:15-27 / node.hh:10-19)."""
+    best = 0
+    for d in dumps:
+        free = int(np.frombuffer(d[:8].tobytes(), np.uint64)[0])
+        off = 16
+        while off < free:
+            uid, level = np.frombuffer(d[off + 8:off + 16].tobytes(), np.uint32)
+            best = max(best, int(uid))
+            size = 16 + 4 * dim + 4 + 8 * 2 * M + int(level) * (4 + 8 * M)
+            off += size + (-size) % 8
+    return best
 
 
 def dump_name(M: int, efc: int, i: int, n: int) -> str:

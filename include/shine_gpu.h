@@ -89,6 +89,11 @@ typedef struct shine_index_info {
  *   the slots like over compute nodes (id % G, read_data.hh:57-58); no collective is on the query path. */
 #define SHINE_PLACE_REPLICA 0
 #define SHINE_PLACE_SHARDED 1
+/* SHARDED_REGIONS: as SHARDED, but GPU slot o owns region o of the space rather than memory nodes: k-means (k = n_gpus)
+ *   over the top-level nodes (placement.hh:22-61, kmeans.hh:93-137), every record in its nearest region with at
+ *   most 5 % imbalance, and shine_knn_batch routes each query to its nearest region within per-batch limits
+ *   (query_router.hh:359-372), so that a search reads mostly its own GPU's HBM. */
+#define SHINE_PLACE_SHARDED_REGIONS 2
 
 /* Open the index from the memory nodes' dumps `index_m{M}_efc{efC}_node{i}_of{N}.dat`, i = 1..N, in that
  * order (replaces MemoryNode::store_or_load_index, memory_node.hh:130-209, plus the token/EP distribution,
@@ -129,6 +134,16 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
  * shine_knn_batch (or check qstats) when exactness under overflow must be guaranteed. */
 int shine_knn_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_queries, uint32_t nq, uint32_t k,
                            uint32_t ef, uint32_t* d_out_ids, float* d_out_dists, uint32_t* d_qstats, void* stream);
+
+/* The GPU slot each query of a batch is answered on: id % n_gpus, or for SHINE_PLACE_SHARDED_REGIONS the slot of
+ * the query's nearest region that still has room in this batch (QueryRouter::run_routing, query_router.hh:280-387).
+ * Host-only. */
+int shine_route(shine_index_t h, const float* queries, uint32_t nq, uint32_t* out_slot);
+
+/* Host-only planner behind SHINE_PLACE_SHARDED_REGIONS (no device needed): the k region centroids (k x dim, nullable)
+ * and the region of every record by uid (region_of_uid[uid], capacity uid_capacity, nullable). */
+int shine_plan_regions(const uint8_t* const* dumps, const uint64_t* sizes, uint32_t n_dumps, uint32_t dim, uint32_t M,
+                       int metric, uint32_t k, uint32_t* region_of_uid, uint64_t uid_capacity, float* centroids);
 
 /* Batched distance kernel: for query i and its n_per_query node uids node_uids[i*n_per_query + j], write
  * out[i*n_per_query + j] = Distance::dist(q_i, x_uid) (distance.hh:153-161).  Device pointers, async. */

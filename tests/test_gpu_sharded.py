@@ -152,3 +152,30 @@ def test_sharded_partial_cache_on_a_larger_index(gpu_available):
     np.testing.assert_array_equal(a.ids, b.ids)
     np.testing.assert_array_equal(a.dists.view(np.uint32), b.dists.view(np.uint32))
     np.testing.assert_array_equal(a.qstats, b.qstats)
+
+
+@pytest.mark.parametrize("gpus", [[0, 0], [0, 0, 0, 0]])
+def test_region_placement_matches_oracle_and_routes_locally(four_shards, gpus, gpu_available):
+    """SHINE_PLACE_SHARDED_REGIONS: slot o owns region o; queries are routed to their region.  Results must not
+    change; the routed slot should own most of a query's results (locality the xGMI path is meant to exploit)."""
+    base, q, dumps = four_shards
+    ref_ids, ref_d, ref_qs = O.OracleIndex(dumps, 128, 8, 0).knn(q, k=10, ef=48)
+    with shine_amd.Index.from_buffers(dumps, 128, 8, 0, gpus=gpus, placement="regions", cache=0.5) as idx:
+        assert idx.info()["placement"] == L.PLACE_SHARDED_REGIONS
+        r = idx.knn(q, 10, 48)
+        slots = idx.route(q)
+        idx.set_search_mode(L.MODE_FAST)
+        f = idx.knn(q, 10, 48)
+    np.testing.assert_array_equal(r.ids, ref_ids)
+    np.testing.assert_array_equal(r.dists.view(np.uint32), ref_d.view(np.uint32))
+    np.testing.assert_array_equal(r.qstats[:, :5], ref_qs[:, :5])
+    k = len(gpus)
+    assert np.bincount(slots, minlength=k).max() <= int(np.ceil(len(q) / k * 1.25))
+    _, region = shine_amd.plan_regions(dumps, 128, 8, 0, k)
+    local = (region[r.ids] == slots[:, None]).mean()
+    assert local > 1.5 / k, local  # well above the 1/k of an unrouted split
+    with shine_amd.Index.from_buffers(dumps, 128, 8, 0, gpus=gpus, placement="replica") as idx:
+        idx.set_search_mode(L.MODE_FAST)
+        g = idx.knn(q, 10, 48)
+    np.testing.assert_array_equal(f.ids, g.ids)
+    np.testing.assert_array_equal(f.qstats, g.qstats)

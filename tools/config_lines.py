@@ -40,6 +40,29 @@ WORKLOADS = {
 }
 
 
+class Heartbeat:
+    """Prints a line every 30 s while a long native call (index build, ground truth) runs, so that the GPU box's
+    watchdog, which kills a command silent for 3 minutes, sees progress."""
+
+    def __init__(self, what):
+        import threading
+        self.what, self.stop = what, threading.Event()
+        self.t = threading.Thread(target=self.run, daemon=True)
+
+    def run(self):
+        t0 = time.time()
+        while not self.stop.wait(30):
+            log(f"{self.what}: {time.time() - t0:.0f}s")
+
+    def __enter__(self):
+        self.t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.t.join()
+
+
 def ground_truth(torch, base_t, q_t, k, metric):
     out = []
     bn = (base_t * base_t).sum(1) if metric == 0 else None
@@ -66,13 +89,15 @@ def run(name, a):
     paths = [cache / shine_amd.dump_name(M, efc, i, shards) for i in range(shards)]
     if not all(p.exists() for p in paths):
         t0 = time.time()
-        dumps, _ = shine_amd.build(base, M, efc, metric, shards, seed=1234, threads=host_threads())
+        with Heartbeat(f"{name}: building {n} x {dim}"):
+            dumps, _ = shine_amd.build(base, M, efc, metric, shards, seed=1234, threads=host_threads())
         log(f"{name}: built {n} x {dim} in {time.time() - t0:.1f}s")
         cache.mkdir(parents=True, exist_ok=True)
         for p, d in zip(paths, dumps):
             d.tofile(p)
         del dumps
-    idx = shine_amd.Index.open(paths, dim, M, metric, elem=elem, gpus=gpus, placement=placement)
+    with Heartbeat(f"{name}: opening"):
+        idx = shine_amd.Index.open(paths, dim, M, metric, elem=elem, gpus=gpus, placement=placement)
     info = idx.info()
     slots = len(gpus)
 
@@ -84,7 +109,8 @@ def run(name, a):
     else:
         q = getattr(D, gen)(batch * nb, seed=2, d=dim)
     qd = torch.from_numpy(q).cuda()
-    gt = ground_truth(torch, torch.from_numpy(base).cuda(), qd, a.k, metric)
+    with Heartbeat(f"{name}: ground truth"):
+        gt = ground_truth(torch, torch.from_numpy(base).cuda(), qd, a.k, metric)
     torch.cuda.empty_cache()
     ids = torch.empty((nb, batch, a.k), dtype=torch.int32, device="cuda")
     dists = torch.empty((nb, batch, a.k), dtype=torch.float32, device="cuda")
