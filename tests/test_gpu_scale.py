@@ -1,0 +1,42 @@
+"""Properties at a larger scale (200K SIFT-shaped records, M=16, ef=128, the bench's search parameters).
+
+Size-independent checks, cheap enough for the GPU suite:
+* exact mode equals the oracle (ids, bitwise distances, counters) on a sample of the queries;
+* fast mode equals exact mode on every query without a tie event (same set, same counters);
+* recall@10 against brute force is at least 0.95 in both modes (BASELINE.json's recall bar).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import shine_amd
+from shine_amd import _lib as L
+from shine_amd import datasets as D
+
+pytestmark = pytest.mark.gpu
+
+
+def test_bench_parameters_at_200k(gpu_available):
+    import torch
+    base = D.sift_like(200_000, seed=91)
+    q = D.sift_like(1024, seed=92)
+    dumps, _ = shine_amd.build(base, 16, 100, 0, 1, seed=8, threads=16)
+    with shine_amd.Index.from_buffers(dumps, 128, 16, 0, gpus=[0]) as idx:
+        ex = idx.knn(q, 10, 128)
+        idx.set_search_mode(L.MODE_FAST)
+        fa = idx.knn(q, 10, 128)
+    ref_ids, ref_d, ref_qs = O.OracleIndex(dumps, 128, 16, 0).knn(q[:48], 10, 128)
+    np.testing.assert_array_equal(ex.ids[:48], ref_ids)
+    np.testing.assert_array_equal(ex.dists[:48].view(np.uint32), ref_d.view(np.uint32))
+    np.testing.assert_array_equal(ex.qstats[:48, :5], ref_qs[:, :5])
+    clean = fa.qstats[:, L.QS_TIES] == 0
+    assert clean.mean() > 0.3
+    np.testing.assert_array_equal(np.sort(fa.ids[clean], 1), np.sort(ex.ids[clean], 1))
+    np.testing.assert_array_equal(fa.qstats[clean][:, :5], ex.qstats[clean][:, :5])
+    bt = torch.from_numpy(base).cuda()
+    qt = torch.from_numpy(q).cuda()
+    d = (qt * qt).sum(1)[:, None] + (bt * bt).sum(1)[None, :] - 2.0 * (qt @ bt.T)
+    gt = torch.topk(d, 10, largest=False).indices.cpu().numpy()
+    assert D.recall_at_k(ex.ids, gt, 10) >= 0.95
+    assert D.recall_at_k(fa.ids, gt, 10) >= 0.95
+    assert abs(D.recall_at_k(fa.ids, gt, 10) - D.recall_at_k(ex.ids, gt, 10)) <= 1e-3
