@@ -61,8 +61,7 @@ struct DevBuf {
   }
 };
 
-// One virtual range whose pieces live in different GPUs' HBM (SHINE_PLACE_SHARDED): the owner of each piece holds
-// the physical allocation, every GPU of the handle maps the whole range.
+// A reserved virtual range and the pieces mapped into it (one GPU's view of a sharded array, see ShardedArray).
 struct StripedRange {
   char* va = nullptr;
   size_t bytes = 0;  // reserved
