@@ -95,6 +95,8 @@ def parse():
     p.add_argument("--shards", type=int, default=1, help="memory-node dumps the index is spread over")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of the CPU-baseline sample")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--ef-sweep", default="32,48,64,96",
+                   help="extra ef values timed in fast mode at N=1 (recall/QPS trade-off; not the headline value)")
     p.add_argument("--mode", choices=["fast", "exact", "both"], default="both",
                    help="search mode(s); the first one measured gives `value` (fast, then exact with 'both')")
     p.add_argument("--cache", default=os.environ.get("SHINE_BENCH_CACHE", "/tmp/shine_bench"))
@@ -150,11 +152,11 @@ def main():
     stream = torch.cuda.Stream()  # a real stream: the C ABI reads a NULL stream as "the handle's own stream"
     torch.cuda.set_stream(stream)
 
-    def step(i, rec=None):
+    def step(i, rec=None, ef=None):
         b = i % a.nbatches
         if rec is not None:
             rec[0].record(stream)
-        idx.knn_device(qd[b * a.batch:(b + 1) * a.batch].data_ptr(), a.batch, a.k, a.ef, ids[b].data_ptr(),
+        idx.knn_device(qd[b * a.batch:(b + 1) * a.batch].data_ptr(), a.batch, a.k, ef or a.ef, ids[b].data_ptr(),
                        dists[b].data_ptr(), qs[b].data_ptr(), stream=stream.cuda_stream)
         if rec is not None:
             rec[1].record(stream)
@@ -223,6 +225,37 @@ def main():
         clean = runs["fast"]["qs"][:, 5] == 0
         mode_report["fast"]["tie_free_same_ids_as_exact"] = float(same[clean].mean()) if clean.any() else None
 
+    # recall / QPS trade-off of the fast kernel at other ef (the metric is "QPS at recall@10 >= 0.95"); the
+    # headline value stays at the config's ef
+    sweep = []
+    if world == 1 and a.ef_sweep:
+        idx.set_search_mode(shine_amd.MODE_FAST)
+        for ef in sorted({int(x) for x in a.ef_sweep.split(",") if x.strip()}):
+            if not (a.k <= ef <= 256) or ef == a.ef:
+                continue
+            for i in range(a.nbatches):
+                step(i, ef=ef)
+            torch.cuda.synchronize()
+            qs_e = qs.cpu().numpy().view(np.uint32).reshape(-1, 8)
+            if (qs_e[:, 6] != 0).any():
+                raise SystemExit(f"ef={ef}: queries did not complete")
+            rec_e = D.recall_at_k(ids.cpu().numpy().view(np.uint32).reshape(-1, a.k).copy(), gt, a.k)
+            for i in range(a.warmup):
+                step(i, ef=ef)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(a.steps):
+                step(a.warmup + i, ef=ef)
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            sweep.append({"ef": ef, "value": a.steps * a.batch / el, "ms_per_step": el * 1e3 / a.steps,
+                          "recall_at_10": rec_e})
+            log(f"ef sweep: ef={ef} recall@{a.k}={rec_e:.4f} {a.steps * a.batch / el / 1e6:.2f}M QPS")
+        if "fast" in runs:
+            sweep.append({"ef": a.ef, "value": mode_report["fast"]["value"],
+                          "ms_per_step": mode_report["fast"]["ms_per_step"], "recall_at_10": runs["fast"]["recall"]})
+        sweep.sort(key=lambda x: x["ef"])
+
     traffic, traffic_src = None, None
     if a.pmc_json and Path(a.pmc_json).exists():
         pmc = json.loads(Path(a.pmc_json).read_text())
@@ -252,6 +285,9 @@ def main():
             "recall_at_10": recall,
             "search_mode": modes[0],
             "modes": mode_report,
+            "ef_sweep": sweep or None,
+            "best_at_recall_0.95": max((x for x in sweep if x["recall_at_10"] >= 0.95), key=lambda x: x["value"],
+                                       default=None),
             "config": {"workload": "SIFT1M-shaped L2 knn, M=16 efC=200 ef=128 k=10", "n": a.n, "dim": a.dim,
                        "global_batch": a.batch * world, "batch_per_gpu": a.batch, "M": a.M, "efc": a.efc,
                        "ef": a.ef, "k": a.k, "shards": a.shards, "parallelism": f"replica{world}"},

@@ -39,7 +39,7 @@ struct SearchArgs {
   uint32_t* out_list;        // queries that overflow here are appended for the next pass (nullable)
   uint32_t* out_count;
   unsigned long long* prof; // diagnostics (nullable): per-phase shader-clock totals, PROF kernel variant only
-  uint32_t fast;            // 1: sorted-list kernel (SHINE_MODE_FAST; ef <= 256, vis_cap > 0)
+  uint32_t fast;            // 1: sorted-list kernel (SHINE_MODE_FAST; ef <= kFastMaxEf, vis_cap > 0)
   uint32_t sort_out;        // heap kernel writes ascending order (fast-mode fixup passes)
 };
 
@@ -59,7 +59,7 @@ inline size_t search_lds_bytes(uint32_t ef, uint32_t cap, uint32_t vis_cap) {
 }
 
 // LDS of the fast kernel: visited table[vis_cap] | scratch ids[64], dists[64] | merge scratch[kFastMaxEf + 1] u64
-constexpr uint32_t kFastMaxEf = 256;
+constexpr uint32_t kFastMaxEf = 512;
 inline size_t search_fast_lds_bytes(uint32_t vis_cap) { return 4ull * vis_cap + 64 * 4 * 2 + 8ull * (kFastMaxEf + 2); }
 
 // Device row layout of the vectors.  The reference's AVX2 kernels keep 8 accumulators: accumulator a sums the

@@ -1185,7 +1185,7 @@ hipError_t launch_search_t(uint32_t grid, const SearchArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, s, a);
     return hipGetLastError();
   };
-  if (a.fast) {  // sorted-list kernel; the launcher's caller guarantees ef <= 256 and a visited table in LDS
+  if (a.fast) {  // sorted-list kernel; the launcher's caller guarantees ef <= kFastMaxEf and a visited table in LDS
     const size_t lds_f = search_fast_lds_bytes(a.vis_cap);
     auto runf = [&](auto kern) -> hipError_t {
       if (lds_f > 65536) {
@@ -1196,7 +1196,7 @@ hipError_t launch_search_t(uint32_t grid, const SearchArgs& a, hipStream_t s) {
       hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds_f, s, a);
       return hipGetLastError();
     };
-    if (a.vis_cap == 0 || a.ef == 0 || a.ef > 256) return hipErrorInvalidValue;
+    if (a.vis_cap == 0 || a.ef == 0 || a.ef > kFastMaxEf) return hipErrorInvalidValue;
     // P = passes of 16 list slots: 2 covers M0 <= 32 (M <= 16), 4 covers M0 <= 64
     if (a.g.M0 > 64) return hipErrorInvalidValue;
     const bool wide = a.g.M0 > 32;
@@ -1205,7 +1205,8 @@ hipError_t launch_search_t(uint32_t grid, const SearchArgs& a, hipStream_t s) {
     }
     if (a.ef <= 64) return wide ? runf(search_fast_kernel<D, METRIC, E, 1, 4>) : runf(search_fast_kernel<D, METRIC, E, 1, 2>);
     if (a.ef <= 128) return wide ? runf(search_fast_kernel<D, METRIC, E, 2, 4>) : runf(search_fast_kernel<D, METRIC, E, 2, 2>);
-    return wide ? runf(search_fast_kernel<D, METRIC, E, 4, 4>) : runf(search_fast_kernel<D, METRIC, E, 4, 2>);
+    if (a.ef <= 256) return wide ? runf(search_fast_kernel<D, METRIC, E, 4, 4>) : runf(search_fast_kernel<D, METRIC, E, 4, 2>);
+    return wide ? runf(search_fast_kernel<D, METRIC, E, 8, 4>) : runf(search_fast_kernel<D, METRIC, E, 8, 2>);
   }
   if constexpr (D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
     if (a.prof && a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0, true>);

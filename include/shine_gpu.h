@@ -152,7 +152,7 @@ int shine_distance_batch_device(shine_index_t h, uint32_t gpu_slot, const float*
 
 /* Search modes.  EXACT (default): the reference's two std heaps replayed step for step — ids in heap-array
  * order, identical to HNSW::knn under distance ties.  FAST: one sorted candidate list per query held in
- * registers (ef <= 256; larger ef runs the exact kernel); same expansions, ids, distances and counters whenever
+ * registers (ef <= 512; larger ef runs the exact kernel); same expansions, ids, distances and counters whenever
  * no two distances compare equal where the reference's heap layout would break the tie (qstats word
  * SHINE_QS_TIES counts such events, 0 = identical set), results in ascending distance order. */
 #define SHINE_MODE_EXACT 0

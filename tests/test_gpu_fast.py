@@ -55,7 +55,9 @@ FAST_CASES = [
     ("tti_ip_d200_ef40", D.tti_like, 3000, 100, 200, 16, 80, 1, 1, 10, 40),
     ("m32_ef200", D.deep_like, 3000, 100, 128, 32, 100, 0, 1, 10, 200),
     ("k_eq_ef", D.deep_like, 2000, 64, 128, 16, 64, 0, 1, 20, 20),
-    ("ef_above_fast_limit", D.deep_like, 3000, 50, 96, 16, 80, 0, 1, 10, 300),
+    ("ef300_r8", D.deep_like, 3000, 50, 96, 16, 80, 0, 1, 10, 300),
+    ("m32_ip_ef512_r8_wide", D.deep_like, 4000, 50, 96, 32, 100, 1, 1, 10, 512),
+    ("ef_above_fast_limit", D.deep_like, 3000, 40, 96, 16, 80, 0, 1, 10, 600),
 ]
 
 

@@ -131,7 +131,9 @@ def run(name, a):
                 rec[s][1].record(streams[s])
 
     lines = []
-    for mode_name, mode in (("fast", shine_amd.MODE_FAST), ("exact", shine_amd.MODE_EXACT)):
+    efs = [int(x) for x in a.ef.split(",")] if a.ef else [ef]
+    modes = [m for m in (("fast", shine_amd.MODE_FAST), ("exact", shine_amd.MODE_EXACT)) if m[0] in a.modes.split(",")]
+    for ef, (mode_name, mode) in [(e, m) for e in efs for m in modes]:
         idx.set_search_mode(mode)
         for i in range(nb):
             step(i)
@@ -181,6 +183,8 @@ def main():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--nbatches", type=int, default=4)
+    p.add_argument("--ef", default="", help="comma list overriding the workload's ef (recall / QPS trade-off)")
+    p.add_argument("--modes", default="fast,exact")
     p.add_argument("--cache", default=os.environ.get("SHINE_CFG_CACHE", "/tmp/shine_cfg"))
     p.add_argument("--out", default=str(ROOT / "gpurun_out" / "config_lines.jsonl"))
     a = p.parse_args()
