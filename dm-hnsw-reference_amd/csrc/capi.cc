@@ -100,6 +100,17 @@ struct ShardedArray {
   }
 };
 
+// Device scratch of one search call (work-queue heads, overflow lists, visited bitmaps, per-query counters).  Each
+// stream a caller enqueues on gets its own, so batches on different streams run concurrently on one GPU.
+struct Scratch {
+  DevBuf<uint32_t> visited, vlog, counter, ovf, qs;
+  uint32_t slots = 0;
+  void release() {
+    for (auto* b : {&visited, &vlog, &counter, &ovf, &qs}) b->release();
+    slots = 0;
+  }
+};
+
 struct Replica {
   int device = 0;
   uint32_t slot = 0;
@@ -108,12 +119,12 @@ struct Replica {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   DevBuf<uint8_t> vec;
   DevBuf<uint32_t> adj0, uid, up_base, adjU, inv_uid;
-  // search scratch
-  DevBuf<uint32_t> visited, vlog, counter;
-  uint32_t slots = 0;
+  // search scratch: the handle's own stream, then caller streams of the device API
+  Scratch main;
+  std::vector<std::pair<hipStream_t, std::unique_ptr<Scratch>>> by_stream;
   // staging for the host-pointer API
   DevBuf<float> q, d;
-  DevBuf<uint32_t> ids, qs, ovf;
+  DevBuf<uint32_t> ids;
   DevBuf<unsigned long long> prof;  // SHINE_PHASE_PROFILE diagnostics
 };
 
@@ -171,9 +182,13 @@ void release_index(shine_index* h) {
   for (auto& R : h->reps) {
     (void)hipSetDevice(R.device);
     if (R.stream) (void)hipStreamSynchronize(R.stream);
-    for (auto* b : {&R.adj0, &R.uid, &R.up_base, &R.adjU, &R.inv_uid, &R.visited, &R.vlog, &R.counter, &R.ids, &R.qs,
-                    &R.ovf})
-      b->release();
+    for (auto* b : {&R.adj0, &R.uid, &R.up_base, &R.adjU, &R.inv_uid, &R.ids}) b->release();
+    for (auto& e : R.by_stream) {
+      (void)hipStreamSynchronize(e.first);
+      e.second->release();
+    }
+    R.by_stream.clear();
+    R.main.release();
     R.prof.release();
     R.vec.release();
     R.q.release();
@@ -434,7 +449,7 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
     if (int rc = upload(R.up_base, upb_d->data(), upb_d->size(), R.stream)) return rc;
     if (int rc = upload(R.adjU, adjU_d->data(), adjU_d->size(), R.stream)) return rc;
     if (int rc = upload(R.inv_uid, inv.data(), inv.size(), R.stream)) return rc;
-    if (int rc = R.counter.grow(8)) return rc;
+    if (int rc = R.main.counter.grow(8)) return rc;
     HIP_TRY(hipStreamSynchronize(R.stream));
   }
   const uint64_t replicated = 4 * (uid_d->size() + upb_d->size() + adjU_d->size() + inv.size());
@@ -502,7 +517,7 @@ LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef) {
   LaunchShape sh{};
   {
     const uint32_t want = std::max<uint32_t>(1, std::min<uint32_t>(16, (nq + kCus - 1) / kCus));
-    const int64_t budget = static_cast<int64_t>(kLdsPerCu / want) - static_cast<int64_t>(search_fast_lds_bytes(0));
+    const int64_t budget = static_cast<int64_t>(kLdsPerCu / want) - static_cast<int64_t>(search_fast_lds_bytes(0, ef));
     uint32_t fit = 1024;
     while (static_cast<int64_t>(fit) * 2 * 4 <= budget) fit *= 2;
     const uint32_t lo = std::min<uint32_t>(8192, std::max<uint32_t>(2048, pow2_at_least(24 * ef)));
@@ -510,7 +525,7 @@ LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef) {
     sh.vis_cap = std::max(lo, std::min(hi, fit));
   }
   sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
-  const uint64_t need = search_fast_lds_bytes(sh.vis_cap);
+  const uint64_t need = search_fast_lds_bytes(sh.vis_cap, ef);
   const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(kLdsPerCu / need));
   const uint32_t wpc = std::max<uint32_t>(1, std::min<uint32_t>({(nq + kCus - 1) / kCus, 16u, fit}));
   sh.cap = 0;
@@ -541,16 +556,25 @@ LaunchShape pick_shape(uint32_t nq, uint32_t ef, int mode) {
   return sh;
 }
 
-int ensure_bitmaps(shine_index* h, Replica& R, uint32_t slots) {
-  if (slots <= R.slots) return 0;
-  R.visited.release();
-  R.vlog.release();
-  R.slots = 0;
-  if (int rc = R.visited.grow(static_cast<size_t>(slots) * h->words_per_slot)) return rc;
-  if (int rc = R.vlog.grow(static_cast<size_t>(slots) * kLogCap)) return rc;
-  HIP_TRY(hipMemsetAsync(R.visited.p, 0, R.visited.n * sizeof(uint32_t), R.stream));
-  HIP_TRY(hipStreamSynchronize(R.stream));
-  R.slots = slots;
+Scratch& scratch_for(Replica& R, hipStream_t s) {
+  if (s == R.stream) return R.main;
+  for (auto& e : R.by_stream)
+    if (e.first == s) return *e.second;
+  R.by_stream.emplace_back(s, std::make_unique<Scratch>());
+  return *R.by_stream.back().second;
+}
+
+int ensure_bitmaps(shine_index* h, Scratch& S, hipStream_t s, uint32_t slots) {
+  if (slots <= S.slots) return 0;
+  HIP_TRY(hipStreamSynchronize(s));  // earlier calls on this stream may still read the old bitmaps
+  S.visited.release();
+  S.vlog.release();
+  S.slots = 0;
+  if (int rc = S.visited.grow(static_cast<size_t>(slots) * h->words_per_slot)) return rc;
+  if (int rc = S.vlog.grow(static_cast<size_t>(slots) * kLogCap)) return rc;
+  HIP_TRY(hipMemsetAsync(S.visited.p, 0, S.visited.n * sizeof(uint32_t), s));
+  HIP_TRY(hipStreamSynchronize(s));
+  S.slots = slots;
   return 0;
 }
 
@@ -559,8 +583,11 @@ int ensure_bitmaps(shine_index* h, Replica& R, uint32_t slots) {
 // Everything stays on the device, so the call is asynchronous and still exact.
 int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, uint32_t k, uint32_t ef,
                    uint32_t* d_ids, float* d_dists, uint32_t* d_qs, hipStream_t s, bool timed) {
-  if (int rc = R.ovf.grow(2ull * nq)) return rc;
-  HIP_TRY(hipMemsetAsync(R.counter.p, 0, 8 * sizeof(uint32_t), s));  // 3 queue heads + 2 list counts
+  Scratch& S = scratch_for(R, s);
+  if (int rc = S.counter.grow(8)) return rc;
+  if (S.ovf.n < 2ull * nq) HIP_TRY(hipStreamSynchronize(s));  // a reallocation must not pull the list from under
+  if (int rc = S.ovf.grow(2ull * nq)) return rc;                // an earlier call on this stream
+  HIP_TRY(hipMemsetAsync(S.counter.p, 0, 8 * sizeof(uint32_t), s));  // 3 queue heads + 2 list counts
   if (env_int("SHINE_PHASE_PROFILE", 0)) {
     if (int rc = R.prof.grow(24)) return rc;
     HIP_TRY(hipMemsetAsync(R.prof.p, 0, 24 * sizeof(unsigned long long), s));
@@ -572,7 +599,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     const bool fast = fast_mode && mode == 0 && ef <= kFastMaxEf;
     const LaunchShape sh = fast ? pick_fast_shape(nq, ef) : pick_shape(nq, ef, mode);
     if (mode == 2) {
-      if (int rc = ensure_bitmaps(h, R, sh.grid)) return rc;
+      if (int rc = ensure_bitmaps(h, S, s, sh.grid)) return rc;
     }
     SearchArgs a{};
     a.g = dev_graph(h, R);
@@ -588,24 +615,24 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     a.out_ids = d_ids;
     a.out_dists = d_dists;
     a.qstats = d_qs;
-    a.visited = R.visited.p;
+    a.visited = S.visited.p;
     a.words_per_slot = h->words_per_slot;
-    a.vlog = R.vlog.p;
+    a.vlog = S.vlog.p;
     a.log_cap = kLogCap;
-    a.counter = R.counter.p + mode;
+    a.counter = S.counter.p + mode;
     a.fast = fast ? 1u : 0u;
     a.sort_out = fast_mode ? 1u : 0u;
     if (mode > start) {
-      a.in_list = R.ovf.p + static_cast<size_t>(mode - 1) * nq;
-      a.in_count = R.counter.p + 3 + (mode - 1);
+      a.in_list = S.ovf.p + static_cast<size_t>(mode - 1) * nq;
+      a.in_count = S.counter.p + 3 + (mode - 1);
     }
     if (mode == 0 && env_int("SHINE_PHASE_PROFILE", 0)) {
       if (int rc = R.prof.grow(24)) return rc;
       a.prof = R.prof.p;
     }
     if (mode < 2) {
-      a.out_list = R.ovf.p + static_cast<size_t>(mode) * nq;
-      a.out_count = R.counter.p + 3 + mode;
+      a.out_list = S.ovf.p + static_cast<size_t>(mode) * nq;
+      a.out_count = S.counter.p + 3 + mode;
     }
     hipError_t e = launch_search(h->dim, h->metric, h->elem, sh.grid, a, s);
     if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("search launch: ") + hipGetErrorString(e));
@@ -759,8 +786,10 @@ int shine_knn_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_qu
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : R.stream;
   uint32_t* qs = d_qstats;
   if (!qs) {
-    if (int rc = R.qs.grow(static_cast<size_t>(nq) * SHINE_QS_WORDS)) return rc;
-    qs = R.qs.p;
+    Scratch& S = scratch_for(R, s);
+    if (S.qs.n < static_cast<size_t>(nq) * SHINE_QS_WORDS) HIP_TRY(hipStreamSynchronize(s));
+    if (int rc = S.qs.grow(static_cast<size_t>(nq) * SHINE_QS_WORDS)) return rc;
+    qs = S.qs.p;
   }
   return enqueue_search(h, R, d_queries, nq, k, ef, d_out_ids, d_out_dists, qs, s, false);
 }
@@ -795,8 +824,8 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
     if (int rc = upload(R.q, qbuf[r].data(), qbuf[r].size(), R.stream)) return rc;
     if (int rc = R.ids.grow(static_cast<size_t>(n) * k)) return rc;
     if (int rc = R.d.grow(static_cast<size_t>(n) * k)) return rc;
-    if (int rc = R.qs.grow(static_cast<size_t>(n) * SHINE_QS_WORDS)) return rc;
-    if (int rc = enqueue_search(h, R, R.q.p, n, k, ef, R.ids.p, R.d.p, R.qs.p, R.stream, true)) return rc;
+    if (int rc = R.main.qs.grow(static_cast<size_t>(n) * SHINE_QS_WORDS)) return rc;
+    if (int rc = enqueue_search(h, R, R.q.p, n, k, ef, R.ids.p, R.d.p, R.main.qs.p, R.stream, true)) return rc;
   }
   double kernel_ms = 0;
   uint64_t retries = 0;
@@ -806,7 +835,7 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
     Replica& R = h->reps[r];
     HIP_TRY(hipSetDevice(R.device));
     sbuf[r].resize(static_cast<size_t>(n) * SHINE_QS_WORDS);
-    HIP_TRY(hipMemcpyAsync(sbuf[r].data(), R.qs.p, sbuf[r].size() * 4, hipMemcpyDeviceToHost, R.stream));
+    HIP_TRY(hipMemcpyAsync(sbuf[r].data(), R.main.qs.p, sbuf[r].size() * 4, hipMemcpyDeviceToHost, R.stream));
     HIP_TRY(hipStreamSynchronize(R.stream));
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, R.ev0, R.ev1));
@@ -827,7 +856,7 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
                      ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6], ph[7], ph[8], ph[9], ph[10], ph[11]);
     }
     uint32_t ovf_counts[2] = {0, 0};  // queries handed to the fixup passes
-    HIP_TRY(hipMemcpy(ovf_counts, R.counter.p + 3, sizeof(ovf_counts), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(ovf_counts, R.main.counter.p + 3, sizeof(ovf_counts), hipMemcpyDeviceToHost));
     retries += ovf_counts[0] + ovf_counts[1];
     ibuf[r].resize(static_cast<size_t>(n) * k);
     dbuf[r].resize(static_cast<size_t>(n) * k);

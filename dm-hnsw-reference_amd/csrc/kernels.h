@@ -60,7 +60,12 @@ inline size_t search_lds_bytes(uint32_t ef, uint32_t cap, uint32_t vis_cap) {
 
 // LDS of the fast kernel: visited table[vis_cap] | scratch ids[64], dists[64] | merge scratch[kFastMaxEf + 1] u64
 constexpr uint32_t kFastMaxEf = 512;
-inline size_t search_fast_lds_bytes(uint32_t vis_cap) { return 4ull * vis_cap + 64 * 4 * 2 + 8ull * (kFastMaxEf + 2); }
+// list registers per lane of the fast kernel for this ef (1, 2, 4 or 8)
+inline uint32_t fast_list_regs(uint32_t ef) { return ef <= 64 ? 1 : ef <= 128 ? 2 : ef <= 256 ? 4 : 8; }
+// the merge scratch holds the 64 R list positions plus the cut and sink slots
+inline size_t search_fast_lds_bytes(uint32_t vis_cap, uint32_t ef) {
+  return 4ull * vis_cap + 64 * 4 * 2 + 8ull * (64 * fast_list_regs(ef) + 2);
+}
 
 // Device row layout of the vectors.  The reference's AVX2 kernels keep 8 accumulators: accumulator a sums the
 // elements i ≡ a (mod 8) of the 16-aligned prefix in increasing i (distance.hh:11-76).  A distance kernel lane

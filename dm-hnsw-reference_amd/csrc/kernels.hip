@@ -1186,7 +1186,7 @@ hipError_t launch_search_t(uint32_t grid, const SearchArgs& a, hipStream_t s) {
     return hipGetLastError();
   };
   if (a.fast) {  // sorted-list kernel; the launcher's caller guarantees ef <= kFastMaxEf and a visited table in LDS
-    const size_t lds_f = search_fast_lds_bytes(a.vis_cap);
+    const size_t lds_f = search_fast_lds_bytes(a.vis_cap, a.ef);
     auto runf = [&](auto kern) -> hipError_t {
       if (lds_f > 65536) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),

@@ -133,3 +133,33 @@ def test_set_search_mode_rejects_unknown(gpu_available):
     with shine_amd.Index.from_buffers(dumps, 96, 8, 0, gpus=[0]) as idx:
         with pytest.raises(shine_amd.ShineError):
             idx.set_search_mode(7)
+
+
+@pytest.mark.parametrize("mode", [L.MODE_FAST, L.MODE_EXACT])
+def test_concurrent_batches_on_streams_share_one_handle(mode, gpu_available, monkeypatch):
+    """Batches enqueued back to back on four streams of one handle run concurrently (per-stream device scratch:
+    work-queue heads, overflow lists, visited bitmaps); every batch equals its sequential result.  A small visited
+    table sends queries through the fixup passes, whose lists are per call."""
+    import torch
+    base = D.deep_like(4000, seed=61, d=96)
+    qn = D.deep_like(8 * 96, seed=62, d=96)
+    dumps, _, _ = O.build(base, 16, 80, 0, 1, seed=3)
+    q = torch.from_numpy(qn).cuda()
+    nb, bs = 8, 96
+    monkeypatch.setenv("SHINE_DEBUG_VISCAP", "512")
+    with shine_amd.Index.from_buffers(dumps, 96, 16, 0, gpus=[0]) as idx:
+        idx.set_search_mode(mode)
+        want = idx.knn(qn, 10, 100)
+        assert (want.qstats[:, L.QS_STATUS] == 0).all()
+        streams = [torch.cuda.Stream() for _ in range(4)]
+        ids = torch.full((nb, bs, 10), -1, dtype=torch.int32, device="cuda")
+        qs = torch.zeros((nb, bs, 8), dtype=torch.int32, device="cuda")
+        for rep in range(2):
+            for b in range(nb):
+                s = streams[b % 4]
+                idx.knn_device(q[b * bs:(b + 1) * bs].data_ptr(), bs, 10, 100, ids[b].data_ptr(), None,
+                               qs[b].data_ptr(), stream=s.cuda_stream)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32).reshape(-1, 10), want.ids)
+            np.testing.assert_array_equal(qs.cpu().numpy().view(np.uint32).reshape(-1, 8)[:, :5],
+                                          want.qstats[:, :5])
