@@ -131,7 +131,10 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
 /* Same with device-resident inputs/outputs on GPU `gpu_slot` of the handle, enqueued on `stream`
  * (hipStream_t; NULL = the handle's stream).  Asynchronous: returns after enqueue.  qstats (device,
  * nullable).  Queries whose candidate queue overflowed are flagged in qstats[SHINE_QS_STATUS]; use
- * shine_knn_batch (or check qstats) when exactness under overflow must be guaranteed. */
+ * shine_knn_batch (or check qstats) when exactness under overflow must be guaranteed.
+ * Batches enqueued on different streams run concurrently: the handle keeps its search scratch (work-queue
+ * heads, fixup lists, visited bitmaps) per stream, so a serving loop may keep several batches in flight
+ * (bench.py keeps two).  Calls on one stream are ordered as usual. */
 int shine_knn_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_queries, uint32_t nq, uint32_t k,
                            uint32_t ef, uint32_t* d_out_ids, float* d_out_dists, uint32_t* d_qstats, void* stream);
 
