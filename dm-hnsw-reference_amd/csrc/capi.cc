@@ -622,7 +622,6 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     a.counter = S.counter.p + mode;
     a.fast = fast ? 1u : 0u;
     a.sort_out = fast_mode ? 1u : 0u;
-    a.no_seen = static_cast<uint32_t>(env_int("SHINE_FAST_NO_SEEN", 0));
     if (mode > start) {
       a.in_list = S.ovf.p + static_cast<size_t>(mode - 1) * nq;
       a.in_count = S.counter.p + 3 + (mode - 1);

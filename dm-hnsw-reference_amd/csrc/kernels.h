@@ -41,7 +41,6 @@ struct SearchArgs {
   unsigned long long* prof; // diagnostics (nullable): per-phase shader-clock totals, PROF kernel variant only
   uint32_t fast;            // 1: sorted-list kernel (SHINE_MODE_FAST; ef <= kFastMaxEf, vis_cap > 0)
   uint32_t sort_out;        // heap kernel writes ascending order (fast-mode fixup passes)
-  uint32_t no_seen;         // diagnostics (SHINE_FAST_NO_SEEN): fast kernel requests rows of entries already visited
 };
 
 struct DistArgs {

@@ -950,7 +950,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       const u32 prow = pid == r_id ? nrow : load_row(pid != INV ? pid : pad);  // a fresh f*: its list now
       // an entry already at its home slot of the visited table is not fresh: its row is not requested (one
       // read-only LDS probe; the visit proper still runs at the top of the next expansion)
-      const bool seen = !A.no_seen && in_row && prow != INV && vtab[vhash(prow, vshift)] == prow;
+      const bool seen = in_row && prow != INV && vtab[vhash(prow, vshift)] == prow;
       issue_list<D, E, P>(X, vec, seen ? INV : prow, pad, g4, c4);
 
       // ---- merge (:456-465 over the whole list at once) ----------------------------------------------------------
