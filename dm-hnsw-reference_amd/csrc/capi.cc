@@ -534,7 +534,13 @@ LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef) {
   return sh;
 }
 
-LaunchShape pick_shape(uint32_t nq, uint32_t ef, int mode) {
+// Fallback pass of fast mode: visited bitmap in HBM and a 16 KiB LDS share, so its workgroups fit beside the main
+// pass's wavefronts of another batch in flight (a whole-CU share would wait for a CU to drain even when the pass
+// has no work, which serialised the batches).  next_candidates holds (16 KiB - top - 512 B) / 8 entries (>= 1,470
+// at ef <= 512; the largest queue met on the bench's index is far below: DESIGN.md §4).
+constexpr uint64_t kLightFixupLds = 16384;
+
+LaunchShape pick_shape(uint32_t nq, uint32_t ef, int mode, bool light = false) {
   LaunchShape sh{};
   const uint64_t top_bytes = align16(8ull * ef);
   uint32_t wpc = 1;
@@ -547,7 +553,7 @@ LaunchShape pick_shape(uint32_t nq, uint32_t ef, int mode) {
   } else {
     sh.vis_cap = mode == 1 ? 16384 : 0;  // mode 2: visited bitmap in HBM
   }
-  const uint64_t budget = (kLdsPerCu / wpc) & ~15u;
+  const uint64_t budget = light ? kLightFixupLds : (kLdsPerCu / wpc) & ~15u;
   const int64_t cap = (static_cast<int64_t>(budget) - static_cast<int64_t>(top_bytes) - 4ll * sh.vis_cap - 512) / 8;
   sh.cap = static_cast<uint32_t>(std::max<int64_t>(cap & ~1ll, 2));
   if (mode == 0) sh.cap = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_DEBUG_CAP", sh.cap)));  // test hook
@@ -595,9 +601,14 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   if (timed) HIP_TRY(hipEventRecord(R.ev0, s));
   const int start = static_cast<int>(env_int("SHINE_DEBUG_START_MODE", 0));  // test hook: exercise modes 1, 2
   const bool fast_mode = h->search_mode == SHINE_MODE_FAST;
+  // fast mode: the sorted-list pass, then one light fallback pass (HBM visited bitmap) for the queries whose
+  // visited table filled; exact mode: three passes with growing LDS shares
+  const bool light_chain = fast_mode && start == 0 && ef <= kFastMaxEf;
+  int prev = -1;  // the pass whose overflow list feeds this one
   for (int mode = start; mode <= 2; ++mode) {
+    if (light_chain && mode == 1) continue;
     const bool fast = fast_mode && mode == 0 && ef <= kFastMaxEf;
-    const LaunchShape sh = fast ? pick_fast_shape(nq, ef) : pick_shape(nq, ef, mode);
+    const LaunchShape sh = fast ? pick_fast_shape(nq, ef) : pick_shape(nq, ef, mode, light_chain && mode == 2);
     if (mode == 2) {
       if (int rc = ensure_bitmaps(h, S, s, sh.grid)) return rc;
     }
@@ -622,9 +633,9 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     a.counter = S.counter.p + mode;
     a.fast = fast ? 1u : 0u;
     a.sort_out = fast_mode ? 1u : 0u;
-    if (mode > start) {
-      a.in_list = S.ovf.p + static_cast<size_t>(mode - 1) * nq;
-      a.in_count = S.counter.p + 3 + (mode - 1);
+    if (prev >= 0) {
+      a.in_list = S.ovf.p + static_cast<size_t>(prev) * nq;
+      a.in_count = S.counter.p + 3 + prev;
     }
     if (mode == 0 && env_int("SHINE_PHASE_PROFILE", 0)) {
       if (int rc = R.prof.grow(24)) return rc;
@@ -636,6 +647,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     }
     hipError_t e = launch_search(h->dim, h->metric, h->elem, sh.grid, a, s);
     if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("search launch: ") + hipGetErrorString(e));
+    prev = mode;
   }
   if (timed) HIP_TRY(hipEventRecord(R.ev1, s));
   return 0;
