@@ -106,7 +106,7 @@ def parse():
     p.add_argument("--mode", choices=["fast", "exact", "both"], default="both",
                    help="search mode(s); the first one measured gives `value` (fast, then exact with 'both')")
     p.add_argument("--cache", default=os.environ.get("SHINE_BENCH_CACHE", "/tmp/shine_bench"))
-    p.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r01" / "bench_fast_v5_pmc.json"),
+    p.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r01" / "bench_fast_v6_pmc.json"),
                    help="per-launch HBM bytes of the search kernel measured by rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                         "passes of this bench (tools/pmc.py; tools/gpu_round.sh)")
     return p.parse_args()
