@@ -490,7 +490,8 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
 // Launch shapes.  Each query keeps top_candidates, next_candidates and its visited table in LDS; the batch is
 // spread so that enough wavefronts are resident (one per query up to 16 per CU) and the rest of the CU's
 // 160 KiB go to the queues.  A query that outgrows them is re-run alone per CU with the whole LDS (mode 1),
-// then with the visited set in HBM (mode 2); only then does it fail with SHINE_ERR_OVERFLOW.
+// then with the visited set in HBM (mode 2); only then does it fail with SHINE_ERR_OVERFLOW.  Fast mode goes from
+// its sorted-list pass straight to a light mode 2 (16 KiB LDS share, see kLightFixupLds).
 struct LaunchShape {
   uint32_t cap, grid, vis_cap, vis_limit;
 };
