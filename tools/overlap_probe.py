@@ -1,7 +1,8 @@
 """Diagnostics: does a second batch in flight hide the fast kernel's tail?
 
 Times K batches of the bench workload (SIFT1M-shaped, ef=128, batch 1024, fast mode) issued on one stream, then
-the same K batches alternating over S streams of the same index handle (per-stream device scratch).  Prints QPS per configuration and the per-query expansion-count distribution.
+the same K batches alternating over S streams of the same index handle (per-stream device scratch).  Prints QPS
+per configuration and the per-query expansion-count distribution.
 """
 import os
 import sys
