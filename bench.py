@@ -13,9 +13,16 @@ own batches (queries split id % G, read_data.hh:57-58) — weak scaling, no data
 the index once and shares the dump files; the max over ranks of the timed wall time gives `value`.
 
 Also reported: `roofline` for the search kernel (algorithmic bytes of the K launches / their GPU span from HIP
-events vs 8 TB/s; `avg_launch_ms` is the per-launch event time, which rocprofv3's average duration matches)
-and `cpu_baseline` (the CPU oracle — a C++ restatement of the reference's knn — on the host cores, bounded
-sample, rank 0 at N=1 only).
+events vs 8 TB/s; `avg_launch_ms` is the per-launch event time, which rocprofv3's average duration matches),
+`value_host_to_host` (SURVEY §8d's query phase: pinned host queries → H2D → knn → D2H of the ids, pipelined on
+the same streams, K steps; `value_host_api` is the synchronous C-ABI host call shine_knn_batch, one batch at a time)
+and `cpu_baseline` (the CPU oracle — a C++ restatement of the reference's knn — built with the reference's flags on
+the host that runs it, on the host cores, bounded sample, rank 0 at N=1 only).
+
+--placement sharded (one process, not torchrun) runs the cfg-4-shaped sharded leg instead: a DEEP-shaped 96-d L2
+index as 8 memory-node dumps over --slots GPU slots (slot s on GPU s % device_count; memory node m on slot m % S),
+every batch split id % S over the slots, and reports the share of reads that left a slot's stripe (xGMI) and the
+bandwidth bound that share implies.
 """
 from __future__ import annotations
 
@@ -109,11 +116,17 @@ def parse():
     p.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r01" / "bench_fast_v6_pmc.json"),
                    help="per-launch HBM bytes of the search kernel measured by rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                         "passes of this bench (tools/pmc.py; tools/gpu_round.sh)")
+    p.add_argument("--no-host", action="store_true", help="skip the host-to-host and host-API legs")
+    p.add_argument("--placement", choices=["replica", "sharded"], default="replica")
+    p.add_argument("--slots", type=int, default=0, help="sharded leg: GPU slots (default --gpus)")
+    p.add_argument("--cache-frac", type=float, default=0.0, help="sharded leg: share of other stripes cached locally")
     return p.parse_args()
 
 
 def main():
     a = parse()
+    if a.placement == "sharded":
+        return run_sharded(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -154,7 +167,7 @@ def main():
     qd = torch.from_numpy(q).cuda()
     ids = torch.empty((a.nbatches, a.batch, a.k), dtype=torch.int32, device="cuda")
     dists = torch.empty((a.nbatches, a.batch, a.k), dtype=torch.float32, device="cuda")
-    qs = torch.zeros((a.nbatches, a.batch, 8), dtype=torch.int32, device="cuda")
+    qs = torch.zeros((a.nbatches, a.batch, shine_amd.QS_WORDS), dtype=torch.int32, device="cuda")
     # real streams (the C ABI reads a NULL stream as "the handle's own stream"); the index keeps device scratch per
     # stream, so batches on different streams run concurrently
     if a.nbatches < a.inflight:
@@ -172,16 +185,7 @@ def main():
         if rec is not None:
             rec[1].record(stream)
 
-    # ground truth on the GPU (exact: integer-valued data keep every f32 partial sum < 2^24)
-    bt = torch.from_numpy(base).cuda()
-    bn = (bt * bt).sum(1)
-    gt = []
-    for s in range(0, nq_rank, 256):
-        qq = qd[s:s + 256]
-        dd = (qq * qq).sum(1)[:, None] + bn[None, :] - 2.0 * (qq @ bt.T)
-        gt.append(torch.topk(dd, a.k, largest=False).indices.cpu().numpy())
-    del bt, bn
-    gt = np.concatenate(gt)
+    gt = ground_truth(torch, base, q, a.k, 0)
 
     def run_mode(mode):
         """Validation pass over every batch (status, recall, algorithmic bytes), warmup, then exactly K timed
@@ -190,7 +194,7 @@ def main():
         for i in range(a.nbatches):
             step(i)
         torch.cuda.synchronize()
-        qs_h = qs.cpu().numpy().view(np.uint32).reshape(-1, 8).copy()
+        qs_h = qs.cpu().numpy().view(np.uint32).reshape(-1, shine_amd.QS_WORDS).copy()
         n_bad = int((qs_h[:, 6] != 0).sum())
         if n_bad:
             raise SystemExit(f"{n_bad} queries did not complete (status {np.unique(qs_h[:, 6])})")
@@ -220,8 +224,63 @@ def main():
         return dict(elapsed=elapsed, kern_ms=kern_ms, span_ms=span_ms, bytes_steps=bytes_steps, recall=recall,
                     qs=qs_h, ids=res)
 
+    def host_legs(mode):
+        """SURVEY §8d's query phase, host to host: pinned host queries → H2D → knn → D2H of ids and distances, all
+        on the step's stream (two batches in flight), K steps between barriers; then the synchronous C-ABI host
+        call (shine_knn_batch: pinned staging inside the library), one batch at a time."""
+        idx.set_search_mode(mode)
+        q_host = torch.from_numpy(q).pin_memory()
+        ids_host = torch.empty((a.nbatches, a.batch, a.k), dtype=torch.int32).pin_memory()
+        d_host = torch.empty((a.nbatches, a.batch, a.k), dtype=torch.float32).pin_memory()
+        qbuf = [torch.empty((a.batch, a.dim), dtype=torch.float32, device="cuda") for _ in streams]
+
+        def hstep(i):
+            b, si = i % a.nbatches, i % len(streams)
+            st = streams[si]
+            with torch.cuda.stream(st):
+                qbuf[si].copy_(q_host[b * a.batch:(b + 1) * a.batch], non_blocking=True)
+                idx.knn_device(qbuf[si].data_ptr(), a.batch, a.k, a.ef, ids[b].data_ptr(), dists[b].data_ptr(),
+                               qs[b].data_ptr(), stream=st.cuda_stream)
+                ids_host[b].copy_(ids[b], non_blocking=True)
+                d_host[b].copy_(dists[b], non_blocking=True)
+
+        for i in range(a.warmup):
+            hstep(i)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            hstep(a.warmup + i)
+        torch.cuda.synchronize()
+        el = max_over_ranks(time.perf_counter() - t0, dist, "cuda")
+        got = ids_host.numpy().view(np.uint32).reshape(-1, a.k)
+        rec = D.recall_at_k(got[:a.batch * min(a.nbatches, a.steps + a.warmup)], gt, a.k)
+        out = {"value_host_to_host": a.steps * a.batch * world / el, "ms_per_step_host_to_host": el * 1e3 / a.steps,
+               "recall_at_10_host_to_host": rec}
+        # the synchronous host API (no batches in flight: it returns when the batch's results are on the host)
+        steps_api = max(1, min(a.steps, 20))
+        for i in range(2):
+            idx.knn(q[:a.batch], a.k, a.ef)
+        if dist:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for i in range(steps_api):
+            b = i % a.nbatches
+            idx.knn(q[b * a.batch:(b + 1) * a.batch], a.k, a.ef)
+        el = max_over_ranks(time.perf_counter() - t0, dist, "cuda")
+        out["value_host_api"] = steps_api * a.batch * world / el
+        out["ms_per_step_host_api"] = el * 1e3 / steps_api
+        log(f"host legs: host-to-host {out['value_host_to_host'] / 1e6:.2f}M QPS (recall {rec:.4f}), "
+            f"shine_knn_batch {out['value_host_api'] / 1e6:.2f}M QPS")
+        return out
+
+    if a.nbatches % max(1, a.inflight) != 0:
+        raise SystemExit("--nbatches must be a multiple of --inflight (a batch's buffers stay on one stream)")
     modes = ["fast", "exact"] if a.mode == "both" else [a.mode]
     runs = {m: run_mode(shine_amd.MODE_FAST if m == "fast" else shine_amd.MODE_EXACT) for m in modes}
+    host = None if a.no_host else host_legs(shine_amd.MODE_FAST if modes[0] == "fast" else shine_amd.MODE_EXACT)
     head = runs[modes[0]]
     elapsed, kern_ms, bytes_steps, recall, qs_h = (head[x] for x in ("elapsed", "kern_ms", "bytes_steps", "recall", "qs"))
     # launches overlap when batches are in flight on several streams: the rate is the K launches' algorithmic bytes
@@ -252,7 +311,7 @@ def main():
             for i in range(a.nbatches):
                 step(i, ef=ef)
             torch.cuda.synchronize()
-            qs_e = qs.cpu().numpy().view(np.uint32).reshape(-1, 8)
+            qs_e = qs.cpu().numpy().view(np.uint32).reshape(-1, shine_amd.QS_WORDS)
             if (qs_e[:, 6] != 0).any():
                 raise SystemExit(f"ef={ef}: queries did not complete")
             rec_e = D.recall_at_k(ids.cpu().numpy().view(np.uint32).reshape(-1, a.k).copy(), gt, a.k)
@@ -299,6 +358,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic SIFT-shaped (integer-valued f32, 1M x 128), random-seeded; index built in-run",
             "recall_at_10": recall,
+            **(host or {}),
             "search_mode": modes[0],
             "modes": mode_report,
             "ef_sweep": sweep or None,
@@ -325,12 +385,173 @@ def main():
         dist.destroy_process_group()
 
 
+def run_sharded(a):
+    """cfg-4-shaped sharded leg: one process drives S GPU slots of one index in the sharded placement
+    (include/shine_gpu.h SHINE_PLACE_SHARDED): memory node m lives on slot m % S only, every slot reads the others'
+    stripes through its own virtual view (xGMI when the slots are distinct GPUs), queries split id % S.  Reports
+    QPS, recall, the share of the algorithmic bytes that left the answering slot's stripe (qstats words 8-11) and the
+    xGMI bound that share implies (7 links x 153 GB/s inbound per GPU)."""
+    import torch
+    import shine_amd
+    from shine_amd import datasets as D
+    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+        raise SystemExit("--placement sharded runs as one process driving every GPU slot (not under torchrun)")
+    ndev = torch.cuda.device_count()
+    S = a.slots or a.gpus
+    gpus = [s % ndev for s in range(S)]
+    phys = len(set(gpus))
+    dim, M, efc, ef, shards = 96, 16, 200, 128, 8
+    key = hashlib.sha1(f"{a.n}-{dim}-{M}-{efc}-{shards}-deep_like-l2-v1".encode()).hexdigest()[:12]
+    cache = Path(a.cache) / key
+    base = D.deep_like(a.n, seed=1, d=dim)
+    paths = [cache / "dump" / shine_amd.dump_name(M, efc, i, shards) for i in range(shards)]
+
+    def build():
+        t0 = time.time()
+        dumps, _ = shine_amd.build(base, M, efc, shine_amd.METRIC_L2, shards, seed=1234, threads=host_threads())
+        log(f"built sharded index: {sum(d.size for d in dumps) / 2**20:.0f} MiB in {time.time() - t0:.1f}s")
+        return dumps
+
+    prepare_dumps(paths, 0, None, build)
+    idx = shine_amd.Index.open(paths, dim, M, shine_amd.METRIC_L2, gpus=gpus, placement="sharded", cache=a.cache_frac)
+    info = idx.info()
+    log(f"sharded index: {info['num_nodes']} nodes over {S} slots ({phys} GPUs), id space {info['id_space']}, "
+        f"{info['device_bytes'] / 2**20:.0f} MiB per GPU, cache fraction {info['cache_fraction']:.3f}")
+    nb, B, k = a.nbatches, a.batch, a.k
+    q = D.deep_like(B * nb, seed=2, d=dim)
+    gt = ground_truth(torch, base, q, k, 0)
+    rows = [[np.arange(b * B, (b + 1) * B)[np.arange(B) % S == s] for s in range(S)] for b in range(nb)]
+    qd, ids, qs, streams = [], [], [], []
+    for s in range(S):
+        dev = torch.device("cuda", gpus[s])
+        qd.append([torch.from_numpy(np.ascontiguousarray(q[rows[b][s]])).to(dev) for b in range(nb)])
+        ids.append([torch.empty((len(rows[b][s]), k), dtype=torch.int32, device=dev) for b in range(nb)])
+        qs.append([torch.zeros((len(rows[b][s]), shine_amd.QS_WORDS), dtype=torch.int32, device=dev)
+                   for b in range(nb)])
+        with torch.cuda.device(dev):
+            streams.append([torch.cuda.Stream(device=dev) for _ in range(max(1, a.inflight))])
+
+    def step(i):
+        b = i % nb
+        for s in range(S):
+            n = len(rows[b][s])
+            if n:
+                idx.knn_device(qd[s][b].data_ptr(), n, k, ef, ids[s][b].data_ptr(), None, qs[s][b].data_ptr(),
+                               stream=streams[s][i % len(streams[s])].cuda_stream, gpu_slot=s)
+
+    def sync():
+        for d in sorted(set(gpus)):
+            torch.cuda.synchronize(d)
+
+    lines = []
+    for mode_name, mode in (("fast", shine_amd.MODE_FAST), ("exact", shine_amd.MODE_EXACT)):
+        if a.mode != "both" and a.mode != mode_name:
+            continue
+        idx.set_search_mode(mode)
+        for i in range(nb):
+            step(i)
+        sync()
+        res = np.zeros((B * nb, k), np.uint32)
+        st = np.zeros((B * nb, shine_amd.QS_WORDS), np.uint32)
+        for b in range(nb):
+            for s in range(S):
+                res[rows[b][s]] = ids[s][b].cpu().numpy().view(np.uint32)
+                st[rows[b][s]] = qs[s][b].cpu().numpy().view(np.uint32)
+        if (st[:, 6] != 0).any():
+            raise SystemExit(f"{int((st[:, 6] != 0).sum())} queries failed")
+        recall = D.recall_at_k(res, gt, k)
+        for i in range(a.warmup):
+            step(i)
+        sync()
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            step(a.warmup + i)
+        sync()
+        el = time.perf_counter() - t0
+        algo = idx.algorithmic_bytes(st) / st.shape[0]
+        remote = (st[:, 8].astype(np.float64) * dim * 4 + st[:, 9].astype(np.float64) * 4 * 2 * M).mean()
+        hits, misses = st[:, 10:12].sum(), st[:, 8:10].sum()
+        qps = a.steps * B / el
+        xgmi_in = 7 * 153e9
+        line = {
+            "metric": "QPS at recall@10, cfg4-shaped sharded index (DEEP-like 96-d L2, 8 memory-node dumps)",
+            "value": qps, "unit": "queries/s", "n_gpus": phys, "gpu_slots": S, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": el * 1e3 / a.steps, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "f32", "search_mode": mode_name, "recall_at_10": recall,
+            "data": f"synthetic DEEP-shaped (L2-normalised f32, {a.n} x 96; N reduced from 100M), index built in-run",
+            "config": {"workload": "cfg4-shaped sharded knn, M=16 efC=200 ef=128 k=10", "n": a.n, "dim": dim,
+                       "M": M, "efc": efc, "ef": ef, "k": k, "shards": shards, "batch": B, "placement": "sharded",
+                       "gpus": gpus, "cache_fraction": info["cache_fraction"],
+                       "batches_in_flight": max(1, a.inflight)},
+            "reads": {"algorithmic_bytes_per_query": algo, "off_stripe_bytes_per_query": remote,
+                      "off_stripe_share": remote / algo, "cache_hit_rate": hits / max(1, hits + misses),
+                      "cache_hits": int(hits), "cache_misses": int(misses)},
+            "bounds": {"hbm_qps": phys * HBM_PEAK_GBPS * 1e9 / algo,
+                       "xgmi_qps": (phys * xgmi_in / remote) if phys > 1 and remote > 0 else None,
+                       "note": "xgmi_qps: every GPU's off-stripe reads at 7 x 153 GB/s inbound; with repeated slots "
+                               "on one GPU all reads are local HBM and only the accounting is exercised"},
+        }
+        log(json.dumps(line))
+        lines.append(line)
+    idx.close()
+    print(json.dumps(lines[0]), flush=True)
+
+
+def ground_truth(torch, base, q, k, metric):
+    """Exact top-k on the GPU in float64 (no reduced-precision GEMM path can reorder near neighbours)."""
+    bt = torch.from_numpy(base).cuda().double()
+    bn = (bt * bt).sum(1)
+    qd = torch.from_numpy(q).cuda().double()
+    out = []
+    for s in range(0, q.shape[0], 256):
+        qq = qd[s:s + 256]
+        ip = qq @ bt.T
+        dd = (qq * qq).sum(1)[:, None] + bn[None, :] - 2.0 * ip if metric == 0 else 1.0 - ip
+        out.append(torch.topk(dd, k, largest=False).indices.cpu().numpy())
+    del bt, bn, qd
+    torch.cuda.empty_cache()
+    return np.concatenate(out)
+
+
+def host_cpu_info():
+    """nproc and lscpu's socket / core counts of the host that runs the CPU baseline."""
+    import subprocess
+    info = {"nproc": os.cpu_count()}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+        for line in out.splitlines():
+            key, _, val = line.partition(":")
+            key, val = key.strip(), val.strip()
+            if key in ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core", "CPU(s)"):
+                info[{"Model name": "model", "Socket(s)": "sockets", "Core(s) per socket": "cores_per_socket",
+                      "Thread(s) per core": "threads_per_core", "CPU(s)": "cpus"}[key]] = val
+    except Exception as e:  # lscpu absent: report what os gives
+        info["lscpu_error"] = str(e)
+    return info
+
+
+def native_oracle():
+    """Build the oracle with the reference's flags for THIS host (-march=native must target the CPU being timed).
+    Returns True if the native build is usable, else the portable checker build is timed instead."""
+    import subprocess
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as O
+    try:
+        subprocess.run(["make", "-s", "-B", "-C", str(ROOT / "oracle"), "native"], check=True, capture_output=True,
+                       timeout=300)
+        return O.NATIVE_PATH.exists()
+    except Exception as e:
+        log(f"native oracle build failed ({e}); timing the portable build")
+        return False
+
+
 def cpu_baseline(paths, q, a, gpu_recall):
     """The oracle (C++ restatement of the reference's knn) on this host's cores, same dump, same queries."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle as O
+    native = native_oracle()
     dumps = [np.fromfile(p, dtype=np.uint8) for p in paths]
-    I = O.OracleIndex(dumps, a.dim, a.M, 0)
+    I = O.OracleIndex(dumps, a.dim, a.M, 0, native=native)
     th = host_threads()
     n = min(q.shape[0], 512)
     t0 = time.perf_counter()
@@ -345,10 +566,14 @@ def cpu_baseline(paths, q, a, gpu_recall):
         done += n
     el = time.perf_counter() - t0
     I.close()
-    log(f"cpu baseline: {done} queries in {el:.1f}s on {th} threads")
+    hw = host_cpu_info()
+    log(f"cpu baseline: {done} queries in {el:.1f}s on {th} threads ({hw})")
     return {"value": done / el, "unit": "queries/s", "cores": th, "kind": "port",
+            "flags": O.NATIVE_FLAGS if native else "-O3 -march=x86-64-v3 -ffp-contract=off (portable checker build)",
+            "host": hw, "pinned": False,
+            "label": "reference-equivalent CPU path (restated), not the RDMA deployment",
             "sample": f"{done} queries (batches of {n} from the bench's query set, k={a.k}, ef={a.ef}) on the "
-                      f"same dump, {th} threads, ~{a.cpu_seconds:.0f}s"}
+                      f"same dump, {th} threads (this job's CPU share of the host), ~{a.cpu_seconds:.0f}s"}
 
 
 if __name__ == "__main__":

@@ -27,8 +27,9 @@ using namespace shine;
 namespace {
 
 constexpr uint32_t kLogCap = 32768;          // visited ids remembered per slot for O(visited) clearing
-constexpr uint32_t kLdsPerCu = 160 * 1024;   // gfx950
-constexpr uint32_t kCus = 256;
+constexpr uint64_t kBitmapBudget = 1ull << 30;  // HBM for the fallback passes' visited bitmaps, per stream
+constexpr uint32_t kGlobalNextCap = 131072;  // next_candidates capacity of the global-heap pass (1 MiB per slot)
+constexpr uint32_t kGlobalSlots = 64;        // persistent slots of the global-heap pass (it sees few queries)
 
 #define HIP_TRY(expr)                                                                              \
   do {                                                                                             \
@@ -37,6 +38,28 @@ constexpr uint32_t kCus = 256;
       return set_error(_e == hipErrorOutOfMemory ? SHINE_ERR_NOMEM : SHINE_ERR_HIP,                \
                        std::string(#expr) + ": " + hipGetErrorString(_e));                         \
   } while (0)
+
+// Pinned host staging (shine_knn_batch): asynchronous copies, no pageable bounce.
+template <class T>
+struct HostBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  int grow(size_t want) {
+    if (want <= n) return 0;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(want, 1) * sizeof(T), hipHostMallocDefault);
+    if (e != hipSuccess) return set_error(SHINE_ERR_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    n = want;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
 
 template <class T>
 struct DevBuf {
@@ -104,9 +127,11 @@ struct ShardedArray {
 // stream a caller enqueues on gets its own, so batches on different streams run concurrently on one GPU.
 struct Scratch {
   DevBuf<uint32_t> visited, vlog, counter, ovf, qs;
+  DevBuf<unsigned long long> heaps;  // global-heap pass
   uint32_t slots = 0;
   void release() {
     for (auto* b : {&visited, &vlog, &counter, &ovf, &qs}) b->release();
+    heaps.release();
     slots = 0;
   }
 };
@@ -114,6 +139,8 @@ struct Scratch {
 struct Replica {
   int device = 0;
   uint32_t slot = 0;
+  uint32_t cus = 256;                 // compute units of the device (hipDeviceProp_t, queried at open)
+  uint32_t lds_per_cu = 160 * 1024;   // LDS bytes per CU
   uint32_t pad_node = 0;  // a node of this slot's own stripe (sharded) for the unconditional loads of empty slots
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -125,6 +152,8 @@ struct Replica {
   // staging for the host-pointer API
   DevBuf<float> q, d;
   DevBuf<uint32_t> ids;
+  HostBuf<float> hq, hd;
+  HostBuf<uint32_t> hids, hqs;
   DevBuf<unsigned long long> prof;  // SHINE_PHASE_PROFILE diagnostics
 };
 
@@ -142,6 +171,8 @@ struct shine_index {
   int placement = SHINE_PLACE_REPLICA;
   uint64_t id_space = 0;       // device ids are < id_space (sharded: slot o owns [o * ids_per_slot, ...))
   uint64_t ids_per_slot = 0;
+  uint64_t cached_rows = 0;    // sharded: rows of every stripe other slots keep local copies of
+  uint32_t div_magic = 0, div_shift = 0;  // id / ids_per_slot = umulhi(id, div_magic) >> div_shift
   ShardedArray svec, sadj0;    // sharded: level-0 vectors and lists
   double cache_fraction = 0;
   Regions regions;             // SHINE_PLACE_SHARDED_REGIONS: slot o owns (and is routed) region o
@@ -168,7 +199,32 @@ DevGraph dev_graph(const shine_index* h, const Replica& r) {
   g.ep = h->ep;
   g.ep_level = h->ep_level;
   g.lists_unique = h->lists_unique;
+  g.sharded = h->placement != SHINE_PLACE_REPLICA && h->reps.size() > 1 ? 1u : 0u;
+  g.slot = r.slot;
+  g.stripe_ids = static_cast<uint32_t>(h->ids_per_slot);
+  g.cached_rows = static_cast<uint32_t>(h->cached_rows);
+  g.div_magic = h->div_magic;
+  g.div_shift = h->div_shift;
   return g;
+}
+
+// Division by the stripe size on the device: for x < 2^31, x / U == umulhi(x, m) >> (l - 1) with l = ceil(log2 U),
+// m = floor(2^(31 + l) / U) + 1 (round-up reciprocal; m < 2^32 for U >= 2).  Checked on the host at every stripe
+// boundary the id space has.
+bool stripe_divider(uint64_t U, uint64_t slots, uint32_t& magic, uint32_t& shift) {
+  if (U < 2 || U * slots > 0x80000000ull) return false;
+  uint32_t l = 0;
+  while ((1ull << l) < U) ++l;
+  const unsigned __int128 m = ((static_cast<unsigned __int128>(1) << (31 + l)) / U) + 1;
+  if (m >> 32) return false;
+  magic = static_cast<uint32_t>(m);
+  shift = l - 1;
+  auto q = [&](uint64_t x) { return static_cast<uint32_t>((x * magic) >> 32) >> shift; };
+  for (uint64_t o = 0; o < slots; ++o) {
+    const uint64_t lo = o * U, hi = lo + U - 1;
+    if (q(lo) != o || q(hi) != o) return false;
+  }
+  return true;
 }
 
 template <class T>
@@ -180,19 +236,22 @@ int upload(DevBuf<T>& dst, const T* src, size_t n, hipStream_t s) {
 
 void release_index(shine_index* h) {
   for (auto& R : h->reps) {
+    // The whole device drains: a caller stream may already be destroyed (include/shine_gpu.h: stream lifetime), so
+    // its handle is never touched here.
     (void)hipSetDevice(R.device);
-    if (R.stream) (void)hipStreamSynchronize(R.stream);
+    (void)hipDeviceSynchronize();
     for (auto* b : {&R.adj0, &R.uid, &R.up_base, &R.adjU, &R.inv_uid, &R.ids}) b->release();
-    for (auto& e : R.by_stream) {
-      (void)hipStreamSynchronize(e.first);
-      e.second->release();
-    }
+    for (auto& e : R.by_stream) e.second->release();
     R.by_stream.clear();
     R.main.release();
     R.prof.release();
     R.vec.release();
     R.q.release();
     R.d.release();
+    R.hq.release();
+    R.hd.release();
+    R.hids.release();
+    R.hqs.release();
     if (R.ev0) (void)hipEventDestroy(R.ev0);
     if (R.ev1) (void)hipEventDestroy(R.ev1);
     if (R.stream) (void)hipStreamDestroy(R.stream);
@@ -294,6 +353,26 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
   for (int d : devs)
     if (d < 0 || d >= ndev) return set_error(SHINE_ERR_ARG, "gpu id " + std::to_string(d) + " out of range");
   const bool sharded = placement != SHINE_PLACE_REPLICA;
+  // device shape from the runtime (CU count and LDS per CU size the launches; partitioned modes change both)
+  std::vector<hipDeviceProp_t> props(devs.size());
+  for (size_t i = 0; i < devs.size(); ++i) {
+    HIP_TRY(hipGetDeviceProperties(&props[i], devs[i]));
+    if (std::strncmp(props[i].gcnArchName, "gfx950", 6) != 0)
+      return set_error(SHINE_ERR_HIP, "GPU " + std::to_string(devs[i]) + " is " + props[i].gcnArchName +
+                                          "; the kernels are built for gfx950 (MI355X) only");
+  }
+  if (sharded) {  // every slot dereferences every other slot's stripe: each ordered pair needs a peer path (xGMI)
+    for (int a : devs)
+      for (int b : devs) {
+        if (a == b) continue;
+        int can = 0;
+        HIP_TRY(hipDeviceCanAccessPeer(&can, a, b));
+        if (!can)
+          return set_error(SHINE_ERR_HIP, "GPU " + std::to_string(a) + " cannot access GPU " + std::to_string(b) +
+                                              "'s memory (no peer path): the sharded placement needs all-to-all "
+                                              "peer access");
+      }
+  }
 
   std::unique_ptr<shine_index> h(new shine_index);
   struct Guard {  // a failed open releases what it had already placed on the devices
@@ -352,6 +431,8 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
     U = std::max<uint64_t>(unit, (most + unit - 1) / unit * unit);
     if (U * slots >= 0x80000000ull)
       return set_error(SHINE_ERR_ARG, "sharded id space of " + std::to_string(U * slots) + " ids exceeds 2^31");
+    if (!stripe_divider(U, slots, h->div_magic, h->div_shift))
+      return set_error(SHINE_ERR_ARG, "no exact 32-bit divider for " + std::to_string(U) + " ids per stripe");
   }
   const uint64_t id_space = sharded ? U * slots : G.N;
   h->id_space = id_space;
@@ -436,6 +517,10 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
     Replica& R = h->reps[r];
     R.device = devs[r];
     R.slot = r;
+    R.cus = static_cast<uint32_t>(std::max(1, props[r].multiProcessorCount));
+    R.lds_per_cu = static_cast<uint32_t>(props[r].maxSharedMemoryPerMultiProcessor > 0
+                                             ? props[r].maxSharedMemoryPerMultiProcessor
+                                             : props[r].sharedMemPerBlock);
     R.pad_node = sharded && owned[r] > 0 ? static_cast<uint32_t>(r * U) : pad_default;
     HIP_TRY(hipSetDevice(R.device));
     HIP_TRY(hipStreamCreateWithFlags(&R.stream, hipStreamNonBlocking));
@@ -460,6 +545,7 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
     while ((step * vrow) % gran != 0 || (step * arow) % gran != 0) step <<= 1;
     crows = std::min<uint64_t>(U, (crows + step - 1) / step * step);
     h->cache_fraction = static_cast<double>(crows) / static_cast<double>(U);
+    h->cached_rows = slots > 1 ? crows : 0;
     if (int rc = map_sharded(h->svec, U * vrow, crows * vrow, devs, gran)) return rc;
     if (int rc = map_sharded(h->sadj0, U * arow, crows * arow, devs, gran)) return rc;
     std::vector<uint8_t> vb;
@@ -487,11 +573,17 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
   return SHINE_OK;
 }
 
-// Launch shapes.  Each query keeps top_candidates, next_candidates and its visited table in LDS; the batch is
-// spread so that enough wavefronts are resident (one per query up to 16 per CU) and the rest of the CU's
-// 160 KiB go to the queues.  A query that outgrows them is re-run alone per CU with the whole LDS (mode 1),
-// then with the visited set in HBM (mode 2); only then does it fail with SHINE_ERR_OVERFLOW.  Fast mode goes from
-// its sorted-list pass straight to a light mode 2 (16 KiB LDS share, see kLightFixupLds).
+// Launch shapes and the pass chain.  Each search runs as up to three passes enqueued back to back on one stream,
+// every pass handing the queries it could not hold to the next through a device list (no host round trip):
+//   main    fast mode: the sorted-list kernel, visited table in LDS (PASS_FAST); exact mode: both std heaps and
+//           the visited table in LDS, one wavefront per query up to 16 per CU (PASS_LDS).
+//   light   visited set as a bitmap in HBM, heaps in a 16 KiB LDS share (kLightFixupLds), so its workgroups fit
+//           beside the main pass of another batch in flight instead of waiting for a drained CU.
+//   global  visited bitmap and both heaps in HBM: no capacity limit short of kGlobalNextCap entries, slow per
+//           heap operation, sized for the few queries the light pass cannot hold.
+// The whole-CU pass (16K-entry LDS table, PASS_WHOLE_CU) is reachable only through SHINE_DEBUG_START_MODE=1.
+enum PassKind { PASS_LDS = 0, PASS_WHOLE_CU = 1, PASS_LIGHT = 2, PASS_GLOBAL = 3, PASS_FAST = 4 };
+
 struct LaunchShape {
   uint32_t cap, grid, vis_cap, vis_limit;
 };
@@ -507,18 +599,15 @@ int64_t env_int(const char* name, int64_t dflt) {
   return e ? std::atoll(e) : dflt;
 }
 
-// mode 0: one wavefront per query up to 16 per CU; top / next / visited table in the wave's LDS share.
-// mode 1: one wavefront per CU with the whole 160 KiB: 16K-entry visited table, larger next queue (fixup).
-// mode 2: one wavefront per CU, visited bitmap in HBM, next queue takes the LDS (fixup).
-// fast (mode 0 of SHINE_MODE_FAST): the sorted list lives in VGPRs, LDS holds only the visited table.
-//   The table is sized for concurrency first: as large as the LDS share of the wavefronts that hold the whole
-//   batch (up to 16 per CU), never below pow2(24·ef) (a query visits ~5-20·ef nodes; one that fills 7/8 of the
-//   table is re-run exactly by the fixup passes) and never above pow2(48·ef).
-LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef) {
+// Fast mode: the sorted list lives in VGPRs, LDS holds only the visited table.  The table is sized for concurrency
+// first: as large as the LDS share of the wavefronts that hold the whole batch (up to 16 per CU), never below
+// pow2(24·ef) (a query visits ~5-20·ef nodes; one that fills 7/8 of the table goes to the light pass) and never
+// above pow2(48·ef).
+LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds_per_cu) {
   LaunchShape sh{};
   {
-    const uint32_t want = std::max<uint32_t>(1, std::min<uint32_t>(16, (nq + kCus - 1) / kCus));
-    const int64_t budget = static_cast<int64_t>(kLdsPerCu / want) - static_cast<int64_t>(search_fast_lds_bytes(0, ef));
+    const uint32_t want = std::max<uint32_t>(1, std::min<uint32_t>(16, (nq + cus - 1) / cus));
+    const int64_t budget = static_cast<int64_t>(lds_per_cu / want) - static_cast<int64_t>(search_fast_lds_bytes(0, ef));
     uint32_t fit = 1024;
     while (static_cast<int64_t>(fit) * 2 * 4 <= budget) fit *= 2;
     const uint32_t lo = std::min<uint32_t>(8192, std::max<uint32_t>(2048, pow2_at_least(24 * ef)));
@@ -527,39 +616,57 @@ LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef) {
   }
   sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
   const uint64_t need = search_fast_lds_bytes(sh.vis_cap, ef);
-  const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(kLdsPerCu / need));
-  const uint32_t wpc = std::max<uint32_t>(1, std::min<uint32_t>({(nq + kCus - 1) / kCus, 16u, fit}));
+  const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(lds_per_cu / need));
+  const uint32_t wpc = std::max<uint32_t>(1, std::min<uint32_t>({(nq + cus - 1) / cus, 16u, fit}));
   sh.cap = 0;
   sh.vis_limit = sh.vis_cap / 8 * 7;
-  sh.grid = std::max<uint32_t>(1, std::min<uint32_t>(nq, kCus * wpc));
+  sh.grid = std::max<uint32_t>(1, std::min<uint32_t>(nq, cus * wpc));
   return sh;
 }
 
-// Fallback pass of fast mode: visited bitmap in HBM and a 16 KiB LDS share, so its workgroups fit beside the main
-// pass's wavefronts of another batch in flight (a whole-CU share would wait for a CU to drain even when the pass
-// has no work, which serialised the batches).  next_candidates holds (16 KiB - top - 512 B) / 8 entries (>= 1,470
-// at ef <= 512; the largest queue met on the bench's index is far below: DESIGN.md §4).
+// LDS share of the light pass.  next_candidates holds (16 KiB - top - 512 B) / 8 entries (>= 1,470 at ef <= 512);
+// a query that outgrows it goes on to the global-heap pass.
 constexpr uint64_t kLightFixupLds = 16384;
 
-LaunchShape pick_shape(uint32_t nq, uint32_t ef, int mode, bool light = false) {
+// Visited-bitmap slots the fallback passes may use on this index (kBitmapBudget of HBM per stream).
+uint32_t bitmap_slot_cap(const shine_index* h) {
+  const uint64_t per = std::max<uint64_t>(1, h->words_per_slot * 4);
+  return static_cast<uint32_t>(std::max<uint64_t>(kGlobalSlots, std::min<uint64_t>(1u << 20, kBitmapBudget / per)));
+}
+
+LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint32_t ef, int pass) {
   LaunchShape sh{};
   const uint64_t top_bytes = align16(8ull * ef);
+  const uint32_t cus = R.cus, lds = R.lds_per_cu;
+  if (pass == PASS_GLOBAL) {
+    sh.vis_cap = 0;
+    sh.cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_GLOBAL_CAP", kGlobalNextCap));  // test hook
+    sh.grid = std::max<uint32_t>(1, std::min<uint32_t>({nq, kGlobalSlots, bitmap_slot_cap(h)}));
+    return sh;
+  }
   uint32_t wpc = 1;
-  if (mode == 0) {
+  uint64_t budget = lds;
+  if (pass == PASS_LDS) {
     sh.vis_cap = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(48 * ef)));
     const uint64_t need = search_lds_bytes(ef, 4 * ef, sh.vis_cap);
-    const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(kLdsPerCu / need));
-    wpc = std::max<uint32_t>(1, std::min<uint32_t>({(nq + kCus - 1) / kCus, 16u, fit}));
+    const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(lds / need));
+    wpc = std::max<uint32_t>(1, std::min<uint32_t>({(nq + cus - 1) / cus, 16u, fit}));
     sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
-  } else {
-    sh.vis_cap = mode == 1 ? 16384 : 0;  // mode 2: visited bitmap in HBM
+    budget = (lds / wpc) & ~15u;
+  } else if (pass == PASS_WHOLE_CU) {
+    sh.vis_cap = 16384;
+  } else {  // PASS_LIGHT: as many slots as the LDS shares allow, capped by the HBM its bitmaps take
+    sh.vis_cap = 0;
+    budget = kLightFixupLds;
+    wpc = std::max<uint32_t>(1, static_cast<uint32_t>(lds / kLightFixupLds));
   }
-  const uint64_t budget = light ? kLightFixupLds : (kLdsPerCu / wpc) & ~15u;
   const int64_t cap = (static_cast<int64_t>(budget) - static_cast<int64_t>(top_bytes) - 4ll * sh.vis_cap - 512) / 8;
   sh.cap = static_cast<uint32_t>(std::max<int64_t>(cap & ~1ll, 2));
-  if (mode == 0) sh.cap = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_DEBUG_CAP", sh.cap)));  // test hook
+  if (pass == PASS_LDS) sh.cap = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_DEBUG_CAP", sh.cap)));
+  if (pass == PASS_LIGHT) sh.cap = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_DEBUG_LIGHT_CAP", sh.cap)));
   sh.vis_limit = sh.vis_cap / 8 * 7;  // linear probing stays short; >= 64 free slots for one expansion
-  sh.grid = std::max<uint32_t>(1, std::min<uint32_t>(nq, kCus * wpc));
+  sh.grid = std::max<uint32_t>(1, std::min<uint32_t>(nq, cus * wpc));
+  if (pass == PASS_LIGHT) sh.grid = std::min(sh.grid, bitmap_slot_cap(h));
   return sh;
 }
 
@@ -585,38 +692,44 @@ int ensure_bitmaps(shine_index* h, Scratch& S, hipStream_t s, uint32_t slots) {
   return 0;
 }
 
-// Enqueue the three search passes on stream s: pass 0 over the whole batch; passes 1 and 2 (more LDS per
-// wavefront, then the visited set in HBM) over the compact lists of queries the previous pass could not hold.
-// Everything stays on the device, so the call is asynchronous and still exact.
+// Enqueue the pass chain on stream s (see PassKind).  Counter words of the call: queue head of pass i at [i],
+// size of the list pass i hands on at [4 + i].  Everything stays on the device: asynchronous and still exact.
 int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, uint32_t k, uint32_t ef,
-                   uint32_t* d_ids, float* d_dists, uint32_t* d_qs, hipStream_t s, bool timed) {
+                   uint32_t* d_ids, float* d_dists, uint32_t* d_qs, hipStream_t s, bool timed,
+                   uint32_t* d_access = nullptr) {
   Scratch& S = scratch_for(R, s);
   if (int rc = S.counter.grow(8)) return rc;
-  if (S.ovf.n < 2ull * nq) HIP_TRY(hipStreamSynchronize(s));  // a reallocation must not pull the list from under
-  if (int rc = S.ovf.grow(2ull * nq)) return rc;                // an earlier call on this stream
-  HIP_TRY(hipMemsetAsync(S.counter.p, 0, 8 * sizeof(uint32_t), s));  // 3 queue heads + 2 list counts
-  if (env_int("SHINE_PHASE_PROFILE", 0)) {
-    if (int rc = R.prof.grow(24)) return rc;
-    HIP_TRY(hipMemsetAsync(R.prof.p, 0, 24 * sizeof(unsigned long long), s));
-  }
+  if (S.ovf.n < 3ull * nq) HIP_TRY(hipStreamSynchronize(s));  // a reallocation must not pull the list from under
+  if (int rc = S.ovf.grow(3ull * nq)) return rc;                // an earlier call on this stream
+  HIP_TRY(hipMemsetAsync(S.counter.p, 0, 8 * sizeof(uint32_t), s));
   if (timed) HIP_TRY(hipEventRecord(R.ev0, s));
-  const int start = static_cast<int>(env_int("SHINE_DEBUG_START_MODE", 0));  // test hook: exercise modes 1, 2
+  const int start = static_cast<int>(env_int("SHINE_DEBUG_START_MODE", 0));  // test hook: the fallback passes alone
   const bool fast_mode = h->search_mode == SHINE_MODE_FAST;
-  // fast mode: the sorted-list pass, then one light fallback pass (HBM visited bitmap) for the queries whose
-  // visited table filled; exact mode: three passes with growing LDS shares
-  const bool light_chain = fast_mode && start == 0 && ef <= kFastMaxEf;
-  int prev = -1;  // the pass whose overflow list feeds this one
-  for (int mode = start; mode <= 2; ++mode) {
-    if (light_chain && mode == 1) continue;
-    const bool fast = fast_mode && mode == 0 && ef <= kFastMaxEf;
-    const LaunchShape sh = fast ? pick_fast_shape(nq, ef) : pick_shape(nq, ef, mode, light_chain && mode == 2);
-    if (mode == 2) {
-      if (int rc = ensure_bitmaps(h, S, s, sh.grid)) return rc;
-    }
+  const bool fast_kernel = fast_mode && ef <= kFastMaxEf && h->M0 <= 64;
+  int chain[3], n_pass = 0;
+  if (start <= 0) chain[n_pass++] = fast_kernel ? PASS_FAST : PASS_LDS;
+  else if (start == 1) chain[n_pass++] = PASS_WHOLE_CU;
+  if (start <= 2) chain[n_pass++] = PASS_LIGHT;
+  chain[n_pass++] = PASS_GLOBAL;
+  for (int i = 0; i < n_pass; ++i) {
+    const int pass = chain[i];
+    const LaunchShape sh = pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu) : pick_shape(h, R, nq, ef, pass);
     SearchArgs a{};
     a.g = dev_graph(h, R);
     if (!a.g.vec || !a.g.adj0 || !a.g.uid || !a.g.up_base)
       return set_error(SHINE_ERR_HIP, "search launch: an index array is missing on this GPU slot");
+    if (pass == PASS_LIGHT || pass == PASS_GLOBAL) {
+      const uint32_t need = std::max(pick_shape(h, R, nq, ef, PASS_LIGHT).grid, pick_shape(h, R, nq, ef, PASS_GLOBAL).grid);
+      if (int rc = ensure_bitmaps(h, S, s, need)) return rc;
+    }
+    if (pass == PASS_GLOBAL) {
+      a.heap_stride = align16(8ull * ef) / 8 + sh.cap;
+      const size_t want = static_cast<size_t>(sh.grid) * a.heap_stride;
+      if (S.heaps.n < want) HIP_TRY(hipStreamSynchronize(s));
+      if (int rc = S.heaps.grow(want)) return rc;
+      a.heaps = S.heaps.p;
+      a.global_heaps = 1;
+    }
     a.queries = d_q;
     a.nq = nq;
     a.k = k;
@@ -631,24 +744,25 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     a.words_per_slot = h->words_per_slot;
     a.vlog = S.vlog.p;
     a.log_cap = kLogCap;
-    a.counter = S.counter.p + mode;
-    a.fast = fast ? 1u : 0u;
+    a.counter = S.counter.p + i;
+    a.fast = pass == PASS_FAST ? 1u : 0u;
     a.sort_out = fast_mode ? 1u : 0u;
-    if (prev >= 0) {
-      a.in_list = S.ovf.p + static_cast<size_t>(prev) * nq;
-      a.in_count = S.counter.p + 3 + prev;
+    a.access = d_access;
+    if (i > 0) {
+      a.in_list = S.ovf.p + static_cast<size_t>(i - 1) * nq;
+      a.in_count = S.counter.p + 4 + (i - 1);
     }
-    if (mode == 0 && env_int("SHINE_PHASE_PROFILE", 0)) {
+    if (i == 0 && env_int("SHINE_PHASE_PROFILE", 0)) {
       if (int rc = R.prof.grow(24)) return rc;
+      HIP_TRY(hipMemsetAsync(R.prof.p, 0, 24 * sizeof(unsigned long long), s));
       a.prof = R.prof.p;
     }
-    if (mode < 2) {
-      a.out_list = S.ovf.p + static_cast<size_t>(mode) * nq;
-      a.out_count = S.counter.p + 3 + mode;
+    if (i + 1 < n_pass) {
+      a.out_list = S.ovf.p + static_cast<size_t>(i) * nq;
+      a.out_count = S.counter.p + 4 + i;
     }
     hipError_t e = launch_search(h->dim, h->metric, h->elem, sh.grid, a, s);
     if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("search launch: ") + hipGetErrorString(e));
-    prev = mode;
   }
   if (timed) HIP_TRY(hipEventRecord(R.ev1, s));
   return 0;
@@ -686,13 +800,29 @@ int validate_views(shine_index* h) {
   return 0;
 }
 
-void route_batch(const shine_index* h, const float* q, uint32_t nq, uint32_t* out) {
+void route_batch(const shine_index* h, const float* q, const uint32_t* ids, uint32_t nq, uint32_t* out) {
   const uint32_t G = static_cast<uint32_t>(h->reps.size());
   if (h->placement == SHINE_PLACE_SHARDED_REGIONS && G > 1) {
     route_queries(h->regions, q, nq, 0.25, out);  // per-batch limits, query_router.hh:359-372
     return;
   }
-  for (uint32_t i = 0; i < nq; ++i) out[i] = i % G;
+  for (uint32_t i = 0; i < nq; ++i) out[i] = (ids ? ids[i] : i) % G;
+}
+
+void print_phase_profile(const shine_index* h, const Replica& R) {  // SHINE_PHASE_PROFILE diagnostics
+  unsigned long long ph[24];
+  if (hipMemcpy(ph, R.prof.p, sizeof(ph), hipMemcpyDeviceToHost) != hipSuccess) return;
+  std::fprintf(stderr, "SHINE_PHASE_PROFILE entries:");
+  for (int i = 12; i < 24; ++i) std::fprintf(stderr, " %llu", ph[i]);
+  std::fprintf(stderr, "\n");
+  if (h->search_mode == SHINE_MODE_FAST)  // entry counts 9..11: next = runner-up / fresh, mispredicted
+    std::fprintf(stderr, "SHINE_PHASE_PROFILE cycles: setup %llu greedy %llu pick %llu - %llu predict+issue %llu "
+                         "dist %llu merge %llu out %llu visited %llu\n",
+                 ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6], ph[7], ph[8]);
+  else
+    std::fprintf(stderr, "SHINE_PHASE_PROFILE cycles: setup %llu greedy %llu pop %llu adj+visited %llu dist %llu "
+                         "predict %llu accept-loop %llu out %llu next-push %llu top-pop %llu top-push %llu trim %llu\n",
+                 ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6], ph[7], ph[8], ph[9], ph[10], ph[11]);
 }
 
 uint64_t bq_bytes(const shine_index* h, const uint32_t* qs) {  // B_q
@@ -800,15 +930,15 @@ int shine_knn_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_qu
   uint32_t* qs = d_qstats;
   if (!qs) {
     Scratch& S = scratch_for(R, s);
-    if (S.qs.n < static_cast<size_t>(nq) * SHINE_QS_WORDS) HIP_TRY(hipStreamSynchronize(s));
-    if (int rc = S.qs.grow(static_cast<size_t>(nq) * SHINE_QS_WORDS)) return rc;
+    if (S.qs.n < static_cast<size_t>(nq) * kQsWords) HIP_TRY(hipStreamSynchronize(s));
+    if (int rc = S.qs.grow(static_cast<size_t>(nq) * kQsWords)) return rc;
     qs = S.qs.p;
   }
   return enqueue_search(h, R, d_queries, nq, k, ef, d_out_ids, d_out_dists, qs, s, false);
 }
 
-int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t k, uint32_t ef, uint32_t* out_ids,
-                    float* out_dists, uint32_t* qstats, shine_stats* stats) {
+int shine_knn_batch(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
+                    uint32_t ef, uint32_t* out_ids, float* out_dists, uint32_t* qstats, shine_stats* stats) {
   if (int rc = check_knn_args(h, k, ef)) return rc;
   if (stats) std::memset(stats, 0, sizeof(*stats));
   if (nq == 0) return SHINE_OK;
@@ -816,29 +946,39 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
   std::lock_guard<std::mutex> lk(h->mu);
   const uint32_t G = static_cast<uint32_t>(h->reps.size());
   const size_t d = h->dim;
-  // queries are split over the slots round-robin by position, as compute nodes split them by id
-  // (read_data.hh:57-58: id % num_clients == client_id); a region-placed index routes them to their region instead
   if (env_int("SHINE_DEBUG_VALIDATE", 0))
     if (int rc = validate_views(h)) return rc;
+  // queries are split over the slots as compute nodes split them, by id (read_data.hh:57-58: id % num_clients ==
+  // client_id; the position stands in for the id when query_ids is NULL); a region-placed index routes them to
+  // their region instead
   std::vector<uint32_t> dest(nq);
-  route_batch(h, queries, nq, dest.data());
+  route_batch(h, queries, query_ids, nq, dest.data());
   std::vector<std::vector<uint32_t>> part(G);
   for (uint32_t i = 0; i < nq; ++i) part[dest[i]].push_back(i);
-  std::vector<std::vector<float>> qbuf(G);
-  std::vector<std::vector<uint32_t>> ibuf(G), sbuf(G);
-  std::vector<std::vector<float>> dbuf(G);
+  // every slot's batch is staged through pinned host memory and enqueued (H2D, passes, D2H) before any wait
   for (uint32_t r = 0; r < G; ++r) {
     const uint32_t n = static_cast<uint32_t>(part[r].size());
     if (n == 0) continue;
     Replica& R = h->reps[r];
     HIP_TRY(hipSetDevice(R.device));
-    qbuf[r].resize(n * d);
-    for (uint32_t j = 0; j < n; ++j) std::memcpy(&qbuf[r][j * d], queries + part[r][j] * d, d * sizeof(float));
-    if (int rc = upload(R.q, qbuf[r].data(), qbuf[r].size(), R.stream)) return rc;
+    if (int rc = R.q.grow(n * d)) return rc;
     if (int rc = R.ids.grow(static_cast<size_t>(n) * k)) return rc;
     if (int rc = R.d.grow(static_cast<size_t>(n) * k)) return rc;
-    if (int rc = R.main.qs.grow(static_cast<size_t>(n) * SHINE_QS_WORDS)) return rc;
+    if (int rc = R.main.qs.grow(static_cast<size_t>(n) * kQsWords)) return rc;
+    if (int rc = R.hq.grow(n * d)) return rc;
+    if (int rc = R.hids.grow(static_cast<size_t>(n) * k)) return rc;
+    if (int rc = R.hd.grow(static_cast<size_t>(n) * k)) return rc;
+    if (int rc = R.hqs.grow(static_cast<size_t>(n) * kQsWords + 8)) return rc;
+    for (uint32_t j = 0; j < n; ++j)
+      std::memcpy(R.hq.p + j * d, queries + static_cast<size_t>(part[r][j]) * d, d * sizeof(float));
+    HIP_TRY(hipMemcpyAsync(R.q.p, R.hq.p, n * d * sizeof(float), hipMemcpyHostToDevice, R.stream));
     if (int rc = enqueue_search(h, R, R.q.p, n, k, ef, R.ids.p, R.d.p, R.main.qs.p, R.stream, true)) return rc;
+    HIP_TRY(hipMemcpyAsync(R.hids.p, R.ids.p, static_cast<size_t>(n) * k * 4, hipMemcpyDeviceToHost, R.stream));
+    HIP_TRY(hipMemcpyAsync(R.hd.p, R.d.p, static_cast<size_t>(n) * k * 4, hipMemcpyDeviceToHost, R.stream));
+    HIP_TRY(hipMemcpyAsync(R.hqs.p, R.main.qs.p, static_cast<size_t>(n) * kQsWords * 4, hipMemcpyDeviceToHost,
+                           R.stream));
+    HIP_TRY(hipMemcpyAsync(R.hqs.p + static_cast<size_t>(n) * kQsWords, R.main.counter.p, 8 * 4,
+                           hipMemcpyDeviceToHost, R.stream));
   }
   double kernel_ms = 0;
   uint64_t retries = 0;
@@ -847,44 +987,24 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
     if (n == 0) continue;
     Replica& R = h->reps[r];
     HIP_TRY(hipSetDevice(R.device));
-    sbuf[r].resize(static_cast<size_t>(n) * SHINE_QS_WORDS);
-    HIP_TRY(hipMemcpyAsync(sbuf[r].data(), R.main.qs.p, sbuf[r].size() * 4, hipMemcpyDeviceToHost, R.stream));
     HIP_TRY(hipStreamSynchronize(R.stream));
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, R.ev0, R.ev1));
     kernel_ms = std::max(kernel_ms, static_cast<double>(ms));
-    if (env_int("SHINE_PHASE_PROFILE", 0) && R.prof.p) {
-      unsigned long long ph[24];
-      HIP_TRY(hipMemcpy(ph, R.prof.p, sizeof(ph), hipMemcpyDeviceToHost));
-      std::fprintf(stderr, "SHINE_PHASE_PROFILE entries:");
-      for (int i = 12; i < 24; ++i) std::fprintf(stderr, " %llu", ph[i]);
-      std::fprintf(stderr, "\n");
-      if (h->search_mode == SHINE_MODE_FAST)  // entry counts 9..11: next = runner-up / fresh, mispredicted
-        std::fprintf(stderr, "SHINE_PHASE_PROFILE cycles: setup %llu greedy %llu pick %llu - %llu predict+issue %llu "
-                             "dist %llu merge %llu out %llu visited %llu\n",
-                     ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6], ph[7], ph[8]);
-      else
-        std::fprintf(stderr, "SHINE_PHASE_PROFILE cycles: setup %llu greedy %llu pop %llu adj+visited %llu dist %llu "
-                             "predict %llu accept-loop %llu out %llu next-push %llu top-pop %llu top-push %llu trim %llu\n",
-                     ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6], ph[7], ph[8], ph[9], ph[10], ph[11]);
-    }
-    uint32_t ovf_counts[2] = {0, 0};  // queries handed to the fixup passes
-    HIP_TRY(hipMemcpy(ovf_counts, R.main.counter.p + 3, sizeof(ovf_counts), hipMemcpyDeviceToHost));
-    retries += ovf_counts[0] + ovf_counts[1];
-    ibuf[r].resize(static_cast<size_t>(n) * k);
-    dbuf[r].resize(static_cast<size_t>(n) * k);
-    HIP_TRY(hipMemcpyAsync(ibuf[r].data(), R.ids.p, ibuf[r].size() * 4, hipMemcpyDeviceToHost, R.stream));
-    HIP_TRY(hipMemcpyAsync(dbuf[r].data(), R.d.p, dbuf[r].size() * 4, hipMemcpyDeviceToHost, R.stream));
-    HIP_TRY(hipStreamSynchronize(R.stream));
+    const uint32_t* cnt = R.hqs.p + static_cast<size_t>(n) * kQsWords;
+    retries += cnt[4] + cnt[5] + cnt[6];  // queries handed on by each pass
+    if (env_int("SHINE_PHASE_PROFILE", 0) && R.prof.p) print_phase_profile(h, R);
   }
   int rc = SHINE_OK;
   shine_stats agg{};
+  const uint64_t e = h->elem == SHINE_ELEM_F16 ? 2 : 4;
   for (uint32_t r = 0; r < G; ++r) {
+    const Replica& R = h->reps[r];
     for (size_t j = 0; j < part[r].size(); ++j) {
       const uint32_t qi = part[r][j];
-      std::memcpy(out_ids + static_cast<size_t>(qi) * k, &ibuf[r][j * k], k * 4);
-      if (out_dists) std::memcpy(out_dists + static_cast<size_t>(qi) * k, &dbuf[r][j * k], k * 4);
-      const uint32_t* qs = &sbuf[r][j * SHINE_QS_WORDS];
+      std::memcpy(out_ids + static_cast<size_t>(qi) * k, R.hids.p + j * k, k * 4);
+      if (out_dists) std::memcpy(out_dists + static_cast<size_t>(qi) * k, R.hd.p + j * k, k * 4);
+      const uint32_t* qs = R.hqs.p + j * kQsWords;
       if (qstats) std::memcpy(qstats + static_cast<size_t>(qi) * SHINE_QS_WORDS, qs, SHINE_QS_WORDS * 4);
       if (qs[SHINE_QS_STATUS] != 0 && rc == SHINE_OK)
         rc = set_error(static_cast<int>(qs[SHINE_QS_STATUS]),
@@ -897,6 +1017,9 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
       agg.visited_neighborlists_l0 += qs[SHINE_QS_LISTS_L0];
       agg.rdma_reads_in_bytes += ref_read_bytes(h, qs);
       agg.algorithmic_bytes += bq_bytes(h, qs);
+      agg.remote_reads_in_bytes += qs[SHINE_QS_REMOTE_VEC] * h->dim * e + qs[SHINE_QS_REMOTE_LIST] * 4ull * h->M0;
+      agg.cache_hits += qs[SHINE_QS_CACHED_VEC] + qs[SHINE_QS_CACHED_LIST];
+      agg.cache_misses += qs[SHINE_QS_REMOTE_VEC] + qs[SHINE_QS_REMOTE_LIST];
     }
   }
   agg.overflow_retries = retries;
@@ -905,11 +1028,29 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
   return rc;
 }
 
+int shine_release_stream(shine_index_t h, void* stream) {
+  if (!h) return set_error(SHINE_ERR_ARG, "index handle is NULL");
+  if (!stream) return SHINE_OK;  // the handle's own streams live as long as the handle
+  std::lock_guard<std::mutex> lk(h->mu);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  for (auto& R : h->reps) {
+    for (auto it = R.by_stream.begin(); it != R.by_stream.end(); ++it) {
+      if (it->first != s) continue;
+      HIP_TRY(hipSetDevice(R.device));
+      HIP_TRY(hipStreamSynchronize(s));
+      it->second->release();
+      R.by_stream.erase(it);
+      break;
+    }
+  }
+  return SHINE_OK;
+}
+
 int shine_route(shine_index_t h, const float* queries, uint32_t nq, uint32_t* out_slot) {
   if (!h) return set_error(SHINE_ERR_ARG, "index handle is NULL");
   if (nq == 0) return SHINE_OK;
   if (!queries || !out_slot) return set_error(SHINE_ERR_ARG, "NULL host pointer");
-  route_batch(h, queries, nq, out_slot);
+  route_batch(h, queries, nullptr, nq, out_slot);
   return SHINE_OK;
 }
 
@@ -929,6 +1070,23 @@ int shine_plan_regions(const uint8_t* const* dumps, const uint64_t* sizes, uint3
       region_of_uid[G.uid[g]] = region[g];
     }
   }
+  return SHINE_OK;
+}
+
+int shine_graph_stats_buffers(const uint8_t* const* dumps, const uint64_t* sizes, uint32_t n_dumps, uint32_t dim,
+                              uint32_t M, shine_graph_stats* out) {
+  if (!dumps || !sizes || !out) return set_error(SHINE_ERR_ARG, "NULL argument");
+  HostGraph G;
+  if (int rc = parse_dumps(dumps, sizes, n_dumps, dim, M, SHINE_METRIC_L2, 0, G)) return rc;
+  const GraphReach r = graph_reach(G);
+  std::memset(out, 0, sizeof(*out));
+  out->num_nodes = r.num_nodes;
+  out->reachable_l0 = r.reachable_l0;
+  out->reachable_any = r.reachable_any;
+  out->zero_indegree_l0 = r.zero_indegree_l0;
+  out->full_lists_l0 = r.full_lists_l0;
+  out->mean_degree_l0 = r.mean_degree_l0;
+  out->max_level = r.max_level;
   return SHINE_OK;
 }
 

@@ -188,4 +188,57 @@ int parse_dumps(const u8* const* bufs, const u64* sizes, u32 n, u32 dim, u32 M, 
   return 0;
 }
 
+// Reachability of the parsed graph from the entry point (diagnostic for shine_graph_stats).  A level-0 search
+// starts at the node the greedy descent ends on (hnsw.hh:279-294) and follows level-0 lists only
+// (hnsw.hh:436-438), so a record no level-0 path from the entry point reaches can never be returned.
+GraphReach graph_reach(const HostGraph& G) {
+  GraphReach r;
+  const u32 M0 = 2 * G.L.M, MU = G.L.M;
+  r.num_nodes = G.N;
+  std::vector<u8> seen(G.N, 0);
+  std::vector<u32> stack;
+  auto bfs = [&](bool all_levels) {
+    std::fill(seen.begin(), seen.end(), 0);
+    stack.assign(1, G.ep);
+    seen[G.ep] = 1;
+    u64 cnt = 1;
+    while (!stack.empty()) {
+      const u32 g = stack.back();
+      stack.pop_back();
+      auto visit = [&](u32 x) {
+        if (x != kInvalid && !seen[x]) {
+          seen[x] = 1;
+          ++cnt;
+          stack.push_back(x);
+        }
+      };
+      for (u32 j = 0; j < M0; ++j) visit(G.adj0[static_cast<u64>(g) * M0 + j]);
+      if (all_levels)
+        for (u32 l = 1; l <= G.level[g]; ++l)
+          for (u32 j = 0; j < MU; ++j) visit(G.adjU[(static_cast<u64>(G.up_base[g]) + l - 1) * MU + j]);
+    }
+    return cnt;
+  };
+  r.reachable_l0 = bfs(false);
+  r.reachable_any = bfs(true);
+  std::vector<u32> indeg(G.N, 0);
+  u64 edges = 0;
+  for (u64 g = 0; g < G.N; ++g) {
+    u32 c = 0;
+    for (u32 j = 0; j < M0; ++j) {
+      const u32 x = G.adj0[g * M0 + j];
+      if (x == kInvalid) continue;
+      ++c;
+      ++indeg[x];
+    }
+    edges += c;
+    if (c == M0) ++r.full_lists_l0;
+  }
+  for (u64 g = 0; g < G.N; ++g)
+    if (indeg[g] == 0 && g != G.ep) ++r.zero_indegree_l0;
+  r.mean_degree_l0 = G.N ? static_cast<double>(edges) / static_cast<double>(G.N) : 0.0;
+  r.max_level = G.ep_level;
+  return r;
+}
+
 }  // namespace shine

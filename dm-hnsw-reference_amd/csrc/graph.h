@@ -64,4 +64,11 @@ int parse_dumps(const u8* const* bufs, const u64* sizes, u32 n, u32 dim, u32 M, 
 
 int read_file(const std::string& path, std::vector<u8>& out);
 
+struct GraphReach {
+  u64 num_nodes = 0, reachable_l0 = 0, reachable_any = 0, zero_indegree_l0 = 0, full_lists_l0 = 0;
+  double mean_degree_l0 = 0;
+  u32 max_level = 0;
+};
+GraphReach graph_reach(const HostGraph& G);
+
 }  // namespace shine

@@ -17,7 +17,15 @@ struct DevGraph {
   uint32_t inv_size;
   uint32_t N, M0, MU, ep, ep_level, lists_unique;
   uint32_t pad_node;      // a node local to this GPU: unconditional loads of empty list slots read it
+  // Sharded placements: where a device id's record lives, for the per-query read accounting (qstats words 8-11,
+  // the rdma_reads_in_bytes analogue, rdma_reads.hh:12,46).  Id x belongs to stripe x / stripe_ids (computed as
+  // umulhi(x, div_magic) >> div_shift, exact for x < 2^31); it is local when the stripe is `slot`, a cached copy
+  // when x % stripe_ids < cached_rows, otherwise an xGMI read.  sharded = 0: every read is local (replica).
+  uint32_t sharded, slot, stripe_ids, cached_rows, div_magic, div_shift;
 };
+
+// Per-query counter words (u32) written by the search kernels; include/shine_gpu.h SHINE_QS_*.
+constexpr uint32_t kQsWords = 12;
 
 struct SearchArgs {
   DevGraph g;
@@ -38,9 +46,13 @@ struct SearchArgs {
   const uint32_t* in_count;
   uint32_t* out_list;        // queries that overflow here are appended for the next pass (nullable)
   uint32_t* out_count;
+  unsigned long long* heaps; // global-heap pass: per-slot top / next heaps in HBM, heap_stride entries each
+  uint64_t heap_stride;
+  uint32_t* access;          // cache warmup (nullable): per device id, reads of the record (vector or list)
   unsigned long long* prof; // diagnostics (nullable): per-phase shader-clock totals, PROF kernel variant only
   uint32_t fast;            // 1: sorted-list kernel (SHINE_MODE_FAST; ef <= kFastMaxEf, vis_cap > 0)
   uint32_t sort_out;        // heap kernel writes ascending order (fast-mode fixup passes)
+  uint32_t global_heaps;    // 1: heap kernel with both heaps in HBM (last fallback pass; vis_cap must be 0)
 };
 
 struct DistArgs {

@@ -401,6 +401,50 @@ __device__ __forceinline__ void dist_list(const E* __restrict__ vec, const Query
 __device__ __forceinline__ u32 vhash(u32 key, u32 shift) { return (key * 0x9E3779B1u) >> shift; }
 
 // ------------------------------------------------------------------------------------------------------------
+// Read accounting (qstats words 8-11): the reads a search makes of records outside its GPU's own stripe, split
+// into those served by the local copies (cache hits) and those that cross xGMI — the analogue of the
+// reference's rdma_reads_in_bytes / cache_hits / cache_misses (rdma_reads.hh:12,46; statistics.hh:148-175).
+// Counted per wave step with ballots; a replica index (sharded = 0) skips it on a uniform branch.  With
+// A.access set (cache warmup), every record read is also counted per device id for the admission ranking.
+// ------------------------------------------------------------------------------------------------------------
+struct ReadCount {
+  u32 vec_remote = 0, list_remote = 0, vec_cached = 0, list_cached = 0;
+};
+
+__device__ __forceinline__ u32 read_class(const DevGraph& g, u32 x) {  // 0 own stripe, 1 cached copy, 2 xGMI
+  const u32 s = __umulhi(x, g.div_magic) >> g.div_shift;
+  const u32 r = x - s * g.stripe_ids;
+  return s == g.slot ? 0u : (r < g.cached_rows ? 1u : 2u);
+}
+
+// vector reads of the lanes with `active` set (each reads record x)
+__device__ __forceinline__ void count_vec_reads(const SearchArgs& A, ReadCount& rc, bool active, u32 x) {
+  if (A.g.sharded) {
+    const u32 c = active ? read_class(A.g, x) : 0u;
+    rc.vec_remote += __popcll(__ballot(c == 2u));
+    rc.vec_cached += __popcll(__ballot(c == 1u));
+  }
+  if (A.access && active) atomicAdd(&A.access[x], 1u);
+}
+
+// one neighbour-list read of record x (x uniform over the wave)
+__device__ __forceinline__ void count_list_read(const SearchArgs& A, ReadCount& rc, u32 x, int lane) {
+  if (A.g.sharded) {
+    const u32 c = read_class(A.g, x);
+    rc.list_remote += c == 2u ? 1u : 0u;
+    rc.list_cached += c == 1u ? 1u : 0u;
+  }
+  if (A.access && lane == 0) atomicAdd(&A.access[x], 1u);
+}
+
+__device__ __forceinline__ void write_read_counts(u32* qs, const ReadCount& rc) {
+  qs[8] = rc.vec_remote;
+  qs[9] = rc.list_remote;
+  qs[10] = rc.vec_cached;
+  qs[11] = rc.list_cached;
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // Wave-wide minimum on DPP: row_shr 1/2/4/8 inside each 16-lane row, then row_bcast15 / row_bcast31 — six VALU
 // steps instead of a ds_bpermute butterfly.  Lanes that hold nothing must pass +inf; NaN never wins.
 // ------------------------------------------------------------------------------------------------------------
@@ -433,9 +477,10 @@ template <int D, int METRIC, typename E>
 __device__ __forceinline__ void entry_and_descent(const SearchArgs& A, const E* __restrict__ vec,
                                                   const QueryRegs<D>& Q, u32* sc_ids, float* sc_d, int lane,
                                                   u32& nn, float& closest, u32& st_dist, u32& st_vup, u32& st_vl0,
-                                                  u32& st_lup, u32& status) {
+                                                  u32& st_lup, u32& status, ReadCount& rc) {
   const u32 ep = A.g.ep;
   if (lane == 0) sc_ids[0] = ep;
+  count_vec_reads(A, rc, lane == 0, ep);
   wave_sync();
   dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, 1, lane);
   wave_sync();
@@ -459,6 +504,7 @@ __device__ __forceinline__ void entry_and_descent(const SearchArgs& A, const E* 
       st_vup += cnt;
       st_dist += cnt;
       if (valid) sc_ids[lane] = e;
+      count_vec_reads(A, rc, valid, e);  // upper-level lists are replicated: only the vectors can be remote
       wave_sync();
       dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, cnt, lane);
       wave_sync();
@@ -525,6 +571,9 @@ struct PhaseClock<true> {  // lane i accumulates phase i: one compare and one 64
 #define PHASE(i) clk.mark(i);
 #define EVENT(i) clk.event(i);
 
+//   VIS   0: visited table in LDS; 1: visited bitmap in HBM; 2: visited bitmap and both heaps in HBM (the last
+//         fallback pass: no capacity limit but the heap stride, ~µs per heap operation).  Heaps in HBM are
+//         written by some lanes and read by others: a workgroup-scope fence orders every heap operation.
 template <int D, int METRIC, typename E, int VIS, bool PROF = false>
 __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
   PhaseClock<PROF> clk;
@@ -532,18 +581,23 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int ef = static_cast<int>(A.ef), cap = static_cast<int>(A.cap);
   const size_t top_b = align16(8ull * ef), next_b = align16(8ull * cap);
-  u64* top = reinterpret_cast<u64*>(smem);                     // MaxHeap top_candidates
-  u64* nxt = reinterpret_cast<u64*>(smem + top_b);             // MinHeap next_candidates
-  u32* vtab = reinterpret_cast<u32*>(smem + top_b + next_b);   // visited table            (VIS = 0)
+  u64* const gheap = VIS == 2 ? reinterpret_cast<u64*>(A.heaps) + static_cast<u64>(blockIdx.x) * A.heap_stride
+                              : nullptr;
+  u64* top = VIS == 2 ? gheap : reinterpret_cast<u64*>(smem);                   // MaxHeap top_candidates
+  u64* nxt = VIS == 2 ? gheap + top_b / 8 : reinterpret_cast<u64*>(smem + top_b);  // MinHeap next_candidates
+  u32* vtab = reinterpret_cast<u32*>(VIS == 2 ? smem : smem + top_b + next_b);  // visited table (VIS = 0)
   u32* sc_ids = vtab + (VIS == 0 ? A.vis_cap : 0u);            // fresh neighbours
   float* sc_d = reinterpret_cast<float*>(sc_ids + 64);
+  auto hfence = []() {
+    if constexpr (VIS == 2) __threadfence_block();
+  };
 
   const int lane = threadIdx.x;
   const E* __restrict__ vec = static_cast<const E*>(A.g.vec);
   const u32 M0 = A.g.M0;
   const u32 vmask = A.vis_cap - 1, vshift = 32 - (31 - __clz(static_cast<int>(A.vis_cap > 1 ? A.vis_cap : 2)));
-  u32* __restrict__ vis = A.visited + (VIS == 1 ? static_cast<u64>(blockIdx.x) * A.words_per_slot : 0ull);
-  u32* __restrict__ vlog = A.vlog + (VIS == 1 ? static_cast<u64>(blockIdx.x) * A.log_cap : 0ull);
+  u32* __restrict__ vis = A.visited + (VIS >= 1 ? static_cast<u64>(blockIdx.x) * A.words_per_slot : 0ull);
+  u32* __restrict__ vlog = A.vlog + (VIS >= 1 ? static_cast<u64>(blockIdx.x) * A.log_cap : 0ull);
   const u64 below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));  // lanes < this one
 
   const u32 n_items = A.in_count ? *A.in_count : A.nq;
@@ -563,12 +617,14 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
     }
 
     u32 st_dist = 0, st_vup = 0, st_vl0 = 0, st_lup = 0, st_ll0 = 0, st_maxnext = 0, status = 0;
+    ReadCount rc;
 
     // ---- entry point + greedy descent (hnsw.hh:256-287) ---------------------------------------------------
     PHASE(1)
     u32 nn;
     float closest;
-    entry_and_descent<D, METRIC, E>(A, vec, Q, sc_ids, sc_d, lane, nn, closest, st_dist, st_vup, st_vl0, st_lup, status);
+    entry_and_descent<D, METRIC, E>(A, vec, Q, sc_ids, sc_d, lane, nn, closest, st_dist, st_vup, st_vl0, st_lup, status,
+                                    rc);
 
     // ---- top_candidates.push({nn, dist(q, nn)}) (hnsw.hh:285-286) ---------------------------------------
     ++st_dist;
@@ -590,6 +646,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
       }
       logpos = 1;
       st_maxnext = 1;
+      hfence();
       wave_sync();
 
       u32 pre_id = INV;  // candidate whose adjacency row is in flight in pre_e
@@ -601,12 +658,14 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         const float ck = key(nroot), farthest0 = key(troot);  // next_candidates.top(); pop()  (:418-421)
         const u32 cid = eid(nroot);
         nroot = nan_keys ? heap_pop_any<false>(nxt, nnext, lane) : heap_pop<false>(nxt, nnext, lane);
+        hfence();
         --nnext;
         if (ck > farthest0) break;  // :421-426
 
         // neighbour list of the candidate at level 0 (:436-438)
         PHASE(3)
         ++st_ll0;
+        count_list_read(A, rc, cid, lane);
         u32 e = INV;
         if (cid == pre_id) {
           e = pre_e;
@@ -637,17 +696,18 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         }
         const u64 fm = __ballot(fresh);
         const int nf = __popcll(fm);
+        count_vec_reads(A, rc, fresh, e);
         if (fresh) {
           const int r = __popcll(fm & below);
           sc_ids[r] = e;
-          if (VIS == 1) {
+          if (VIS >= 1) {
             const u32 lp = logpos + r;
             if (lp < A.log_cap) vlog[lp] = e;
           }
         }
         logpos += nf;
         nvis += nf;
-        if (VIS == 1 && logpos > A.log_cap) log_overflow = true;
+        if (VIS >= 1 && logpos > A.log_cap) log_overflow = true;
         st_vl0 += nf;
         st_dist += nf;
         if (VIS == 0 && nvis > A.vis_limit) { status = ST_OVERFLOW; break; }
@@ -689,15 +749,19 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
             const u64 en = mk(d, id);
             PHASE(8)
             nroot = heap_push<false>(nxt, nnext, en, nroot, lane);
+            hfence();
             if (ntop < ef) {  // heap.hh:34-41 push_k
               PHASE(10)
               troot = heap_push<true>(top, ntop, en, troot, lane);
+              hfence();
               ++ntop;
             } else {  // d < top().distance holds: it is the accept test with the top full
               PHASE(9)
               troot = nan_keys ? heap_pop_any<true>(top, ntop, lane) : heap_pop<true>(top, ntop, lane);
+              hfence();
               PHASE(10)
               troot = heap_push<true>(top, ntop - 1, en, troot, lane);
+              hfence();
             }
             PHASE(6)
             ++nnext;
@@ -714,6 +778,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         while (ntop > static_cast<int>(A.k)) {
           if (nan_keys) heap_pop_any<true>(top, ntop, lane);
           else heap_pop<true>(top, ntop, lane);
+          hfence();
           --ntop;
         }
       }
@@ -742,7 +807,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
     }
     if (status == ST_OVERFLOW && A.out_list && lane == 0) A.out_list[atomicAdd(A.out_count, 1u)] = qi;
     if (A.qstats && lane == 0) {
-      u32* qs = A.qstats + static_cast<u64>(qi) * 8;
+      u32* qs = A.qstats + static_cast<u64>(qi) * kQsWords;
       qs[0] = st_dist;
       qs[1] = st_vup;
       qs[2] = st_vl0;
@@ -751,9 +816,10 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
       qs[5] = A.sort_out ? 0u : st_maxnext;  // fast-mode fixup: exact, so no tie can have changed the set
       qs[6] = status;
       qs[7] = status == 0 ? static_cast<u32>(ntop < static_cast<int>(A.k) ? ntop : A.k) : 0u;
+      write_read_counts(qs, rc);
     }
 
-    if (VIS == 1) {  // visited_nodes.clear() (:475): clear exactly the words this query touched
+    if (VIS >= 1) {  // visited_nodes.clear() (:475): clear exactly the words this query touched
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (!log_overflow) {
         for (u32 i = lane; i < logpos; i += 64) {
@@ -849,10 +915,12 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       for (u32 i = lane; i < A.vis_cap / 4; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
     }
     u32 st_dist = 0, st_vup = 0, st_vl0 = 0, st_lup = 0, st_ll0 = 0, ties = 0, status = 0;
+    ReadCount rc;
     PHASE(1)
     u32 nn;
     float closest;
-    entry_and_descent<D, METRIC, E>(A, vec, Q, sc_ids, sc_d, lane, nn, closest, st_dist, st_vup, st_vl0, st_lup, status);
+    entry_and_descent<D, METRIC, E>(A, vec, Q, sc_ids, sc_d, lane, nn, closest, st_dist, st_vup, st_vl0, st_lup, status,
+                                    rc);
     ++st_dist;  // top_candidates.push({nn, dist(q, nn)}) (hnsw.hh:285-286)
 
     float ck[R];  // candidate keys, ascending; +inf beyond the size
@@ -883,9 +951,11 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
     float r_key = INF;
     u32 nid = nn;
     u32 nrow = load_row(nn);
+    u32 cur = nn;  // the candidate whose list `e` is
 
     while (status == 0) {
       ++st_ll0;  // read_neighborlist (:436-438)
+      count_list_read(A, rc, cur, lane);
       PHASE(8)
       bool cand = in_row && e != INV;
       if (!A.g.lists_unique) {  // first occurrence in list order wins (visited.insert order, :443)
@@ -906,6 +976,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       }
       const u64 fm = __ballot(fresh);
       const int nf = __popcll(fm);
+      count_vec_reads(A, rc, fresh, e);
       nvis += nf;
       st_vl0 += nf;
       st_dist += nf;
@@ -1055,6 +1126,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       nid = c2 != INV ? c2 : c;
       nrow = load_row(nid);  // unconditional: always the youngest load
       e = erow;
+      cur = c;
       r_id = c2;
       r_key = k2;
     }
@@ -1083,7 +1155,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
     }
     if (status == ST_OVERFLOW && A.out_list && lane == 0) A.out_list[atomicAdd(A.out_count, 1u)] = qi;
     if (A.qstats && lane == 0) {
-      u32* qs = A.qstats + static_cast<u64>(qi) * 8;
+      u32* qs = A.qstats + static_cast<u64>(qi) * kQsWords;
       qs[0] = st_dist;
       qs[1] = st_vup;
       qs[2] = st_vl0;
@@ -1092,6 +1164,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       qs[5] = ties;
       qs[6] = status;
       qs[7] = status == 0 ? static_cast<u32>(cs < static_cast<int>(A.k) ? cs : A.k) : 0u;
+      write_read_counts(qs, rc);
     }
   }
   clk.flush(A.prof, lane);
@@ -1210,6 +1283,11 @@ hipError_t launch_search_t(uint32_t grid, const SearchArgs& a, hipStream_t s) {
   }
   if constexpr (D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
     if (a.prof && a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0, true>);
+  }
+  if (a.global_heaps) {  // both heaps in HBM: only the scratch ids / distances stay in LDS
+    if (a.vis_cap != 0 || !a.heaps || a.heap_stride < align16(8ull * a.ef) / 8 + a.cap) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((search_kernel<D, METRIC, E, 2>), dim3(grid), dim3(64), 64 * 4 * 2, s, a);
+    return hipGetLastError();
   }
   if (a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0>);
   return run(search_kernel<D, METRIC, E, 1>);

@@ -18,7 +18,8 @@ OK, ERR_ARG, ERR_IO, ERR_FORMAT, ERR_HIP, ERR_NOMEM, ERR_OVERFLOW = range(7)
 METRIC_L2, METRIC_IP = 0, 1
 ELEM_F32, ELEM_F16 = 0, 1
 QS_DISTCOMPS, QS_VISITED_UPPER, QS_VISITED_L0, QS_LISTS_UPPER, QS_LISTS_L0, QS_MAX_NEXT, QS_STATUS, QS_NRESULT = range(8)
-QS_WORDS = 8
+QS_REMOTE_VEC, QS_REMOTE_LIST, QS_CACHED_VEC, QS_CACHED_LIST = range(8, 12)
+QS_WORDS = 12
 QS_TIES = 5  # fast mode's meaning of word 5
 MODE_EXACT, MODE_FAST = 0, 1
 PLACE_REPLICA, PLACE_SHARDED, PLACE_SHARDED_REGIONS = 0, 1, 2
@@ -41,6 +42,9 @@ class Stats(C.Structure):
         ("rdma_reads_in_bytes", C.c_uint64),
         ("algorithmic_bytes", C.c_uint64),
         ("overflow_retries", C.c_uint64),
+        ("remote_reads_in_bytes", C.c_uint64),
+        ("cache_hits", C.c_uint64),
+        ("cache_misses", C.c_uint64),
         ("kernel_ms", C.c_double),
     ]
 
@@ -71,6 +75,22 @@ class IndexInfo(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class GraphStats(C.Structure):
+    _fields_ = [
+        ("num_nodes", C.c_uint64),
+        ("reachable_l0", C.c_uint64),
+        ("reachable_any", C.c_uint64),
+        ("zero_indegree_l0", C.c_uint64),
+        ("full_lists_l0", C.c_uint64),
+        ("mean_degree_l0", C.c_double),
+        ("max_level", C.c_uint32),
+        ("reserved0", C.c_uint32),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved0"}
+
+
 P = C.c_void_p
 U32, U64, I32 = C.c_uint32, C.c_uint64, C.c_int
 PU8 = C.POINTER(C.c_uint8)
@@ -84,7 +104,8 @@ PROTOTYPES = {
                             C.POINTER(P)]),
     "shine_open_buffers_ex": (I32, [C.POINTER(PU8), C.POINTER(U64), U32, U32, U32, I32, I32, C.POINTER(I32), U32, I32,
                                     C.c_double, C.POINTER(P)]),
-    "shine_knn_batch": (I32, [P, P, U32, U32, U32, P, P, P, C.POINTER(Stats)]),
+    "shine_knn_batch": (I32, [P, P, P, U32, U32, U32, P, P, P, C.POINTER(Stats)]),
+    "shine_release_stream": (I32, [P, P]),
     "shine_knn_batch_device": (I32, [P, U32, P, U32, U32, U32, P, P, P, P]),
     "shine_distance_batch_device": (I32, [P, U32, P, U32, P, U32, P, P]),
     "shine_route": (I32, [P, P, U32, P]),
@@ -95,6 +116,7 @@ PROTOTYPES = {
     "shine_close": (I32, [P]),
     "shine_selftest_heap": (I32, [I32, P, P, P, U32, U32, P, P, P]),
     "shine_last_error": (C.c_char_p, []),
+    "shine_graph_stats_buffers": (I32, [C.POINTER(PU8), C.POINTER(U64), U32, U32, U32, C.POINTER(GraphStats)]),
     "shine_build": (I32, [P, U64, U32, U32, U32, I32, U32, U32, U32, C.POINTER(P)]),
     "shine_build_dump_size": (U64, [P, U32]),
     "shine_build_dump_data": (P, [P, U32]),
@@ -113,6 +135,7 @@ def lib() -> C.CDLL:
         if not LIB_PATH.exists():
             raise ShineError(ERR_HIP, f"{LIB_PATH} not built: run __graft_entry__.build() (make -C "
                                       f"dm-hnsw-reference_amd/csrc)")
+        _one_hip_runtime()
         L = C.CDLL(str(LIB_PATH))
         for name, (res, args) in PROTOTYPES.items():
             fn = getattr(L, name)
@@ -120,6 +143,17 @@ def lib() -> C.CDLL:
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+def _one_hip_runtime() -> None:
+    """One HIP runtime per process.  torch's ROCm libraries name the runtime `libamdhip64.so` (resolved in torch/lib),
+    this library names `libamdhip64.so.7`: loaded first, ours would make torch load a second runtime next to it,
+    and whichever initialises second finds no device.  Importing torch first lets the loader match our soname to
+    torch's copy.  Without torch (e.g. the C façade) /opt/rocm's runtime is the only one."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
 
 
 def check(rc: int) -> None:

@@ -47,7 +47,7 @@ def _placement(p) -> int:
 class KnnResult:
     ids: np.ndarray      # (nq, k) uint32 uids, reference result order (heap-array order)
     dists: np.ndarray    # (nq, k) float32
-    qstats: np.ndarray   # (nq, 8) uint32, SHINE_QS_* layout
+    qstats: np.ndarray   # (nq, QS_WORDS) uint32, SHINE_QS_* layout
     stats: dict          # aggregates (statistics.hh names)
 
 
@@ -114,17 +114,26 @@ class Index:
         self.mode = mode
 
     # ---- queries -----------------------------------------------------------------------------------------
-    def knn(self, queries: np.ndarray, k: int, ef: int) -> KnnResult:
+    def knn(self, queries: np.ndarray, k: int, ef: int, query_ids: np.ndarray | None = None) -> KnnResult:
+        """shine_knn_batch: query i is answered on GPU slot query_ids[i] % n_gpus (position when None)."""
         q = np.ascontiguousarray(queries, dtype=np.float32)
         if q.ndim != 2 or q.shape[1] != self.dim:
             raise ValueError(f"queries must be (nq, {self.dim})")
         nq = q.shape[0]
+        qid = None if query_ids is None else np.ascontiguousarray(query_ids, dtype=np.uint32)
+        if qid is not None and qid.shape != (nq,):
+            raise ValueError("query_ids must hold one id per query")
         ids = np.empty((nq, k), dtype=np.uint32)
         dists = np.empty((nq, k), dtype=np.float32)
         qs = np.empty((nq, L.QS_WORDS), dtype=np.uint32)
         st = L.Stats()
-        L.check(L.lib().shine_knn_batch(self._h, _ptr(q), nq, k, ef, _ptr(ids), _ptr(dists), _ptr(qs), C.byref(st)))
+        L.check(L.lib().shine_knn_batch(self._h, _ptr(q), _ptr(qid), nq, k, ef, _ptr(ids), _ptr(dists), _ptr(qs),
+                                        C.byref(st)))
         return KnnResult(ids, dists, qs, st.as_dict())
+
+    def release_stream(self, stream: int) -> None:
+        """shine_release_stream: wait for `stream` and drop the handle's scratch for it."""
+        L.check(L.lib().shine_release_stream(self._h, C.c_void_p(stream)))
 
     def knn_device(self, q_ptr: int, nq: int, k: int, ef: int, ids_ptr: int, dists_ptr: int | None,
                    qstats_ptr: int | None, stream: int | None = None, gpu_slot: int = 0) -> None:
@@ -178,6 +187,14 @@ def plan_regions(dumps, dim: int, M: int, metric: int, k: int) -> tuple[np.ndarr
     region = np.full(n_uid, 0xFFFFFFFF, dtype=np.uint32)
     L.check(L.lib().shine_plan_regions(ptrs, sizes, len(dumps), dim, M, metric, k, _ptr(region), n_uid, _ptr(cent)))
     return cent, region
+
+
+def graph_stats(dumps, dim: int, M: int) -> dict:
+    """Host-only reachability diagnostics of an index (shine_graph_stats_buffers)."""
+    dumps, ptrs, sizes = _dump_arrays(dumps)
+    st = L.GraphStats()
+    L.check(L.lib().shine_graph_stats_buffers(ptrs, sizes, len(dumps), dim, M, C.byref(st)))
+    return st.as_dict()
 
 
 def _max_uid(dumps, dim: int, M: int) -> int:

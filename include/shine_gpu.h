@@ -45,7 +45,14 @@ extern "C" {
 #define SHINE_QS_TIES 5          /* fast mode: equal-key events met (0 = result identical to exact mode) */
 #define SHINE_QS_STATUS 6        /* 0 = ok, otherwise the SHINE_ERR_* that stopped this query */
 #define SHINE_QS_NRESULT 7       /* number of ids written (< k only if the graph has fewer nodes) */
-#define SHINE_QS_WORDS 8
+/* Reads of records outside the answering GPU's own stripe (sharded placements; 0 for a replica): the analogue of
+ * rdma_reads_in_bytes / cache_hits / cache_misses (rdma_reads.hh:12,46; statistics.hh:148-175).  "remote" reads
+ * cross xGMI, "cached" reads are served by this GPU's local copies of other stripes' hot records. */
+#define SHINE_QS_REMOTE_VEC 8    /* vector reads over xGMI */
+#define SHINE_QS_REMOTE_LIST 9   /* level-0 neighbour-list reads over xGMI */
+#define SHINE_QS_CACHED_VEC 10   /* vector reads served by the local copies (cache hits) */
+#define SHINE_QS_CACHED_LIST 11  /* level-0 list reads served by the local copies */
+#define SHINE_QS_WORDS 12
 
 typedef struct shine_index* shine_index_t;
 
@@ -60,6 +67,9 @@ typedef struct shine_stats {
   uint64_t rdma_reads_in_bytes;   /* bytes the reference would READ from memory nodes for the same search */
   uint64_t algorithmic_bytes;     /* roofline basis B_q summed over the batch */
   uint64_t overflow_retries;      /* queries re-run with a larger candidate-queue capacity */
+  uint64_t remote_reads_in_bytes; /* bytes read over xGMI from other GPUs' stripes (device layout) */
+  uint64_t cache_hits;            /* cache.hits_total: off-stripe record reads served by local copies */
+  uint64_t cache_misses;          /* cache.misses_total: off-stripe record reads that crossed xGMI */
   double kernel_ms;               /* device time of the search launch(es), HIP events */
 } shine_stats;
 
@@ -122,11 +132,14 @@ int shine_open_buffers_ex(const uint8_t* const* dumps, const uint64_t* sizes, ui
 
 /* knn over a batch of host-resident queries (replaces the WorkerPool::process_queries → hnsw::schedule →
  * HNSW::knn loop, worker_pool.hh:78-89, scheduler.hh:19-102, hnsw.hh:253-307).  queries: nq × dim row-major.
+ * query_ids (nullable): the queries' ids (HNSW::knn's q_id); query i is answered on GPU slot query_ids[i] % n_gpus
+ * (the compute-node split, read_data.hh:57-58), or on slot i % n_gpus when NULL.
  * out_ids: nq × k uids, in the reference's result order (top_candidates heap-array order, hnsw.hh:300-303).
  * out_dists (nullable): nq × k.  qstats (nullable): nq × SHINE_QS_WORDS.  stats (nullable): aggregates.
- * Requires ef >= k (hnsw.hh:36).  Synchronous. */
-int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t k, uint32_t ef,
-                    uint32_t* out_ids, float* out_dists, uint32_t* qstats, shine_stats* stats);
+ * Requires ef >= k (hnsw.hh:36).  Synchronous: every slot's batch is staged through pinned host memory and enqueued
+ * (H2D, search passes, D2H) before the call waits. */
+int shine_knn_batch(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
+                    uint32_t ef, uint32_t* out_ids, float* out_dists, uint32_t* qstats, shine_stats* stats);
 
 /* Same with device-resident inputs/outputs on GPU `gpu_slot` of the handle, enqueued on `stream`
  * (hipStream_t; NULL = the handle's stream).  Asynchronous: returns after enqueue.  qstats (device,
@@ -134,9 +147,15 @@ int shine_knn_batch(shine_index_t h, const float* queries, uint32_t nq, uint32_t
  * shine_knn_batch (or check qstats) when exactness under overflow must be guaranteed.
  * Batches enqueued on different streams run concurrently: the handle keeps its search scratch (work-queue
  * heads, fixup lists, visited bitmaps) per stream, so a serving loop may keep several batches in flight
- * (bench.py keeps two).  Calls on one stream are ordered as usual. */
+ * (bench.py keeps two).  Calls on one stream are ordered as usual.
+ * Stream lifetime: the handle keeps per-stream scratch keyed by the stream; a caller stream must stay valid until
+ * shine_release_stream(h, stream) or shine_close(h), and must be released before it is destroyed if its handle
+ * value may be reused while h is open. */
 int shine_knn_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_queries, uint32_t nq, uint32_t k,
                            uint32_t ef, uint32_t* d_out_ids, float* d_out_dists, uint32_t* d_qstats, void* stream);
+
+/* Wait for the work enqueued on `stream` and free the handle's scratch for it (every GPU slot). */
+int shine_release_stream(shine_index_t h, void* stream);
 
 /* The GPU slot each query of a batch is answered on: id % n_gpus, or for SHINE_PLACE_SHARDED_REGIONS the slot of
  * the query's nearest region that still has room in this batch (QueryRouter::run_routing, query_router.hh:280-387).
@@ -177,6 +196,22 @@ int shine_selftest_heap(int is_max, const int32_t* ops, const float* vals, const
                         uint32_t k, float* out_d, uint32_t* out_ids, uint32_t* out_n);
 
 const char* shine_last_error(void);
+
+/* Host-only graph diagnostics over dump images (no device needed): how much of the index a search can reach.
+ * A level-0 search follows level-0 lists only (hnsw.hh:436-438) from where the greedy descent ends, so a record
+ * outside reachable_l0 can never be returned, whatever ef.  Used to tell an index property from a search bug. */
+typedef struct shine_graph_stats {
+  uint64_t num_nodes;
+  uint64_t reachable_l0;     /* records reachable from the entry point along level-0 lists */
+  uint64_t reachable_any;    /* ... along the lists of every level */
+  uint64_t zero_indegree_l0; /* records no level-0 list names (entry point excluded) */
+  uint64_t full_lists_l0;    /* records whose level-0 list holds 2M entries */
+  double mean_degree_l0;
+  uint32_t max_level;
+  uint32_t reserved0;
+} shine_graph_stats;
+int shine_graph_stats_buffers(const uint8_t* const* dumps, const uint64_t* sizes, uint32_t n_dumps, uint32_t dim,
+                              uint32_t M, shine_graph_stats* out);
 
 /* ----------------------------------------------------------------------------------------------------------
  * Build path: a parallel CPU restatement of HNSW::insert (hnsw.hh:40-251) writing the

@@ -11,16 +11,20 @@ import numpy as np
 
 ORACLE_DIR = Path(__file__).resolve().parent
 LIB_PATH = ORACLE_DIR / "liboracle.so"
+# The same restatement built with the reference's flags (-O3 -march=native -ffast-math -mavx2, CMakeLists.txt:16)
+# for the CPU baseline only: -march=native must target the host that times it, so bench.py builds it there
+# (`make -C oracle native`).  Its distances may differ in the last bit (contraction / reassociation): never a checker.
+NATIVE_PATH = ORACLE_DIR / "liboracle_native.so"
+NATIVE_FLAGS = "-O3 -march=native -ffast-math -mavx2"
 QS_WORDS = 8
-_lib = None
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not LIB_PATH.exists():
-            raise RuntimeError(f"{LIB_PATH} missing: run `make -C oracle`")
-        L = C.CDLL(str(LIB_PATH))
+def lib(path: Path = LIB_PATH):
+    if path not in _libs:
+        if not path.exists():
+            raise RuntimeError(f"{path} missing: run `make -C oracle`")
+        L = C.CDLL(str(path))
         P, U32, I32 = C.c_void_p, C.c_uint32, C.c_int
         L.oracle_draw_levels.argtypes = [U32, U32, U32, U32, P, P]
         L.oracle_build.restype = P
@@ -42,8 +46,8 @@ def lib():
         L.oracle_distance.argtypes = [I32, P, P, U32]
         L.oracle_selftest_heap.restype = I32
         L.oracle_selftest_heap.argtypes = [I32, P, P, P, U32, U32, P, P, P]
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return _libs[path]
 
 
 def _p(a):
@@ -73,11 +77,13 @@ def build(base: np.ndarray, M: int, efc: int, metric: int = 0, n_shards: int = 1
 
 
 class OracleIndex:
-    def __init__(self, dumps, dim, M, metric=0):
+    def __init__(self, dumps, dim, M, metric=0, native=False):
+        """native=True: the reference-flags build (CPU baseline timing only)."""
+        self._lib = lib(NATIVE_PATH if native else LIB_PATH)
         self._dumps = [np.ascontiguousarray(d, dtype=np.uint8) for d in dumps]
         ptrs = (C.c_void_p * len(dumps))(*[d.ctypes.data for d in self._dumps])
         sizes = (C.c_uint64 * len(dumps))(*[d.size for d in self._dumps])
-        self._h = lib().oracle_open(ptrs, sizes, len(dumps), dim, M, metric)
+        self._h = self._lib.oracle_open(ptrs, sizes, len(dumps), dim, M, metric)
         self.dim = dim
 
     def knn(self, queries, k, ef, threads=1):
@@ -86,14 +92,14 @@ class OracleIndex:
         ids = np.empty((nq, k), np.uint32)
         dd = np.empty((nq, k), np.float32)
         qs = np.empty((nq, QS_WORDS), np.uint32)
-        rc = lib().oracle_knn(self._h, _p(q), nq, k, ef, _p(ids), _p(dd), _p(qs), threads)
+        rc = self._lib.oracle_knn(self._h, _p(q), nq, k, ef, _p(ids), _p(dd), _p(qs), threads)
         if rc != 0:
             raise RuntimeError(f"oracle_knn failed: {rc}")
         return ids, dd, qs
 
     def close(self):
         if self._h:
-            lib().oracle_free(self._h)
+            self._lib.oracle_free(self._h)
             self._h = None
 
     def __del__(self):

@@ -36,6 +36,40 @@ def test_parallel_build_is_a_valid_index_with_high_recall():
     assert sum(int(np.frombuffer(d[:8], np.uint64)[0]) for d in dumps) == sum(d.size for d in dumps)
 
 
+@pytest.mark.parametrize("threads,metric,gen,dim", [(1, 0, D.sift_like, 128), (8, 0, D.sift_like, 128),
+                                                    (8, 1, D.deep_like, 96)])
+def test_parallel_build_reaches_every_record(threads, metric, gen, dim):
+    """Reachability from the entry point along level-0 lists (shine_graph_stats_buffers): a race in the parallel
+    insert (lost list updates, a list published before its node) would leave records no search can return."""
+    base = gen(30000, seed=8, d=dim)
+    dumps, _ = shine_amd.build(base, 16, 100, metric, 2, seed=2, threads=threads)
+    st = shine_amd.graph_stats(dumps, dim, 16)
+    assert st["num_nodes"] == 30000
+    assert st["reachable_l0"] >= 30000 - 3, st
+    assert st["reachable_any"] >= st["reachable_l0"]
+    assert 8.0 <= st["mean_degree_l0"] <= 32.0
+
+
+def test_graph_stats_sees_a_cut_graph():
+    """Emptying the entry point's level-0 list (and every upper list) leaves only the entry point reachable."""
+    base = D.sift_like(300, seed=9)
+    dumps, _, _ = O.build(base, 4, 16, 0, 1, seed=1)
+    d = dumps[0].copy()
+    free = int(np.frombuffer(d[:8].tobytes(), np.uint64)[0])
+    off = 16
+    while off < free:  # zero every list count (node.hh:10-19 record walk)
+        level = int(np.frombuffer(d[off + 12:off + 16].tobytes(), np.uint32)[0])
+        lo = off + 16 + 4 * 128
+        d[lo:lo + 4] = 0
+        for l in range(1, level + 1):
+            p = lo + 4 + 8 * 8 + (l - 1) * (4 + 8 * 4)
+            d[p:p + 4] = 0
+        size = 16 + 4 * 128 + 4 + 8 * 8 + level * (4 + 8 * 4)
+        off += size + (-size) % 8
+    st = shine_amd.graph_stats([d], 128, 4)
+    assert st["reachable_l0"] == 1 and st["reachable_any"] == 1 and st["zero_indegree_l0"] == 299
+
+
 def test_build_write_uses_reference_dump_names(tmp_path):
     import ctypes as C
     base = D.sift_like(500, seed=7)

@@ -50,8 +50,9 @@ FAST_CASES = [
     # name, generator, n, nq, dim, M, efc, metric, shards, k, ef
     ("deep_l2_d96_ef64", D.deep_like, 5000, 200, 96, 16, 100, 0, 1, 10, 64),
     ("deep_ip_d96_ef100", D.deep_like, 5000, 150, 96, 16, 100, 1, 2, 10, 100),
-    ("sift_l2_ef128", D.sift_like, 6000, 200, 128, 16, 100, 0, 1, 10, 128),
-    ("sift_l2_ef256_3shards", D.sift_like, 5000, 100, 128, 8, 64, 0, 3, 10, 256),
+    ("sift_l2_ef128", D.sift_like, 6000, 1000, 128, 16, 100, 0, 1, 10, 128),
+    ("sift_bench_shape_m16_efc200_ef128", D.sift_like, 20000, 1000, 128, 16, 200, 0, 1, 10, 128),
+    ("sift_l2_ef256_3shards", D.sift_like, 5000, 1000, 128, 8, 64, 0, 3, 10, 256),
     ("tti_ip_d200_ef40", D.tti_like, 3000, 100, 200, 16, 80, 1, 1, 10, 40),
     ("m32_ef200", D.deep_like, 3000, 100, 128, 32, 100, 0, 1, 10, 200),
     ("k_eq_ef", D.deep_like, 2000, 64, 128, 16, 64, 0, 1, 20, 20),
@@ -67,14 +68,16 @@ def test_fast_mode_matches_oracle(case, gpu_available):
     base = gen(n, seed=101, d=dim)
     q = gen(nq, seed=202, d=dim)
     dumps, _, _ = O.build(base, M, efc, metric, shards, seed=5)
-    ref = O.OracleIndex(dumps, dim, M, metric).knn(q, k, ef)
+    ref = O.OracleIndex(dumps, dim, M, metric).knn(q, k, ef, threads=8)
     r = _fast_knn(dumps, dim, M, metric, q, k, ef)
-    # float-valued data (deep/tti) rarely ties (IP keys 1 - x can round equal): nearly every query is exact
-    need = 0.95 if gen is not D.sift_like else 0.2
+    # float-valued data (deep/tti) rarely ties (IP keys 1 - x can round equal): nearly every query is exact;
+    # integer-valued SIFT-like data ties on half the queries or more (72 % at ef=256), so >= 250 of the 1000 are
+    # checked bitwise
+    need = 0.95 if gen is not D.sift_like else 0.25
     _check_tie_free_exact(r, ref, need)
     gt, _ = D.brute_force_knn(base, q, k, metric=metric)
-    assert abs(D.recall_at_k(r.ids, gt, k) - D.recall_at_k(ref[0], gt, k)) <= 1e-3 + 1.0 / (nq * k) * (
-        (r.qstats[:, L.QS_TIES] > 0).sum())
+    # the north-star bar over the whole batch, ties included: |recall_fast - recall_ref| <= 1e-3
+    assert abs(D.recall_at_k(r.ids, gt, k) - D.recall_at_k(ref[0], gt, k)) <= 1e-3
 
 
 def test_fast_mode_ties_are_counted(gpu_available):
@@ -107,6 +110,34 @@ def test_fast_mode_overflow_fixups_are_exact(gpu_available, monkeypatch):
     assert clean.all()
 
 
+def test_fast_mode_light_pass_at_ef512_is_exact(gpu_available, monkeypatch):
+    """ef=512 with a 1,024-entry visited table: nearly every query fills it and goes to the light pass (HBM
+    bitmap, 16 KiB LDS share); none may fail, and all are exact (heap kernel, ascending output)."""
+    base = D.deep_like(6000, seed=91, d=96)
+    q = D.deep_like(96, seed=92, d=96)
+    dumps, _, _ = O.build(base, 16, 100, 1, 1, seed=4)
+    ref = O.OracleIndex(dumps, 96, 16, 1).knn(q, 10, 512)
+    monkeypatch.setenv("SHINE_DEBUG_VISCAP", "1024")
+    r = _fast_knn(dumps, 96, 16, 1, q, 10, 512)
+    assert r.stats["overflow_retries"] >= 48
+    clean = _check_tie_free_exact(r, ref, 0.95)
+    assert clean.mean() >= 0.95
+
+
+def test_fast_mode_light_pass_overflow_goes_to_global_heaps(gpu_available, monkeypatch):
+    """A light pass whose next_candidates holds only 8 entries hands its queries on to the global-heap pass (both
+    heaps in HBM): the batch still completes, exactly."""
+    base = D.deep_like(4000, seed=93, d=96)
+    q = D.deep_like(48, seed=94, d=96)
+    dumps, _, _ = O.build(base, 16, 100, 0, 1, seed=4)
+    ref = O.OracleIndex(dumps, 96, 16, 0).knn(q, 10, 128)
+    monkeypatch.setenv("SHINE_DEBUG_VISCAP", "1024")
+    monkeypatch.setenv("SHINE_DEBUG_LIGHT_CAP", "8")
+    r = _fast_knn(dumps, 96, 16, 0, q, 10, 128)
+    assert r.stats["overflow_retries"] > 0  # counted once per pass a query is handed on by
+    _check_tie_free_exact(r, ref, 1.0)
+
+
 def test_fast_mode_device_entry_and_mode_switch(gpu_available):
     import torch
     base = D.deep_like(3000, seed=51, d=96)
@@ -116,7 +147,7 @@ def test_fast_mode_device_entry_and_mode_switch(gpu_available):
     s_ids, _ = _sorted_ref(ref_ids, ref_d)
     q = torch.from_numpy(qn).cuda()
     ids = torch.empty((128, 10), dtype=torch.int32, device="cuda")
-    qs = torch.empty((128, 8), dtype=torch.int32, device="cuda")
+    qs = torch.empty((128, L.QS_WORDS), dtype=torch.int32, device="cuda")
     with shine_amd.Index.from_buffers(dumps, 96, 16, 0, gpus=[0]) as idx:
         for mode, want in [(L.MODE_FAST, s_ids), (L.MODE_EXACT, ref_ids), (L.MODE_FAST, s_ids)]:
             idx.set_search_mode(mode)
@@ -153,7 +184,7 @@ def test_concurrent_batches_on_streams_share_one_handle(mode, gpu_available, mon
         assert (want.qstats[:, L.QS_STATUS] == 0).all()
         streams = [torch.cuda.Stream() for _ in range(4)]
         ids = torch.full((nb, bs, 10), -1, dtype=torch.int32, device="cuda")
-        qs = torch.zeros((nb, bs, 8), dtype=torch.int32, device="cuda")
+        qs = torch.zeros((nb, bs, L.QS_WORDS), dtype=torch.int32, device="cuda")
         for rep in range(2):
             for b in range(nb):
                 s = streams[b % 4]
@@ -161,5 +192,5 @@ def test_concurrent_batches_on_streams_share_one_handle(mode, gpu_available, mon
                                qs[b].data_ptr(), stream=s.cuda_stream)
             torch.cuda.synchronize()
             np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32).reshape(-1, 10), want.ids)
-            np.testing.assert_array_equal(qs.cpu().numpy().view(np.uint32).reshape(-1, 8)[:, :5],
+            np.testing.assert_array_equal(qs.cpu().numpy().view(np.uint32).reshape(-1, L.QS_WORDS)[:, :5],
                                           want.qstats[:, :5])

@@ -59,7 +59,7 @@ def test_knn_device_entry(case, gpu_available):
     nq, k = q.shape[0], case["k"]
     ids = torch.empty((nq, k), dtype=torch.int32, device="cuda")
     dd = torch.empty((nq, k), dtype=torch.float32, device="cuda")
-    qs = torch.empty((nq, 8), dtype=torch.int32, device="cuda")
+    qs = torch.empty((nq, shine_amd.QS_WORDS), dtype=torch.int32, device="cuda")
     with shine_amd.Index.from_buffers(case["dumps"], case["dim"], case["M"], case["metric"], gpus=[0]) as idx:
         idx.knn_device(q.data_ptr(), nq, k, case["ef"], ids.data_ptr(), dd.data_ptr(), qs.data_ptr(),
                        stream=torch.cuda.current_stream().cuda_stream)
@@ -218,9 +218,12 @@ def test_device_heaps_match_libstdcxx(is_max, ties, general, gpu_available):
 
 
 @pytest.mark.parametrize("env", [{"SHINE_DEBUG_VISCAP": "1024"}, {"SHINE_DEBUG_START_MODE": "1"},
-                                 {"SHINE_DEBUG_START_MODE": "2"}])
+                                 {"SHINE_DEBUG_START_MODE": "2"}, {"SHINE_DEBUG_START_MODE": "3"},
+                                 {"SHINE_DEBUG_VISCAP": "1024", "SHINE_DEBUG_LIGHT_CAP": "16"}])
 def test_visited_modes(env, gpu_available, monkeypatch):
-    """Visited table overflow → re-run with the whole LDS; and the HBM-bitmap variant: identical results."""
+    """Every pass of the chain alone or handed overflowing queries: the whole-CU LDS pass (start mode 1), the
+    light pass (HBM visited bitmap, 16 KiB LDS heaps; start mode 2), the global-heap pass (bitmap and both heaps in
+    HBM; start mode 3), and a light pass too small for most queries: identical results."""
     base = D.sift_like(8000, seed=71)
     q = D.sift_like(128, seed=72)
     dumps, _, _ = O.build(base, 16, 100, 0, 1, seed=3)
@@ -233,6 +236,20 @@ def test_visited_modes(env, gpu_available, monkeypatch):
             assert r.stats["overflow_retries"] > 0
         _check_same(r, *ref)
         _check_same(idx.knn(q, 10, 200), *ref)
+
+
+def test_global_heap_capacity_overflow_is_reported(gpu_available, monkeypatch):
+    """The last pass's capacity is the only hard limit: a query that outgrows it fails with SHINE_ERR_OVERFLOW in
+    its status word and shine_knn_batch returns that status (no silent truncation)."""
+    base = D.sift_like(3000, seed=95)
+    q = D.sift_like(8, seed=96)
+    dumps, _, _ = O.build(base, 8, 40, 0, 1, seed=2)
+    monkeypatch.setenv("SHINE_DEBUG_START_MODE", "3")
+    monkeypatch.setenv("SHINE_DEBUG_GLOBAL_CAP", "4")
+    with shine_amd.Index.from_buffers(dumps, 128, 8, 0, gpus=[0]) as idx:
+        with pytest.raises(shine_amd.ShineError) as e:
+            idx.knn(q, 10, 64)
+    assert e.value.code == shine_amd._lib.ERR_OVERFLOW
 
 
 def test_nan_distances_follow_reference(gpu_available):

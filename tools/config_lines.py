@@ -64,16 +64,21 @@ class Heartbeat:
 
 
 def ground_truth(torch, base_t, q_t, k, metric):
+    """Exact top-k on the GPU in float64.  The round-1 version multiplied in float32, and torch's f32 GEMM on this
+    stack does not give exact f32 products: on the 10M DEEP-like index its "ground truth" agreed with the exact one
+    at recall 0.875 only (tools/cfg3_reach.py, profiles/r02/cfg3_10m.jsonl), which was the cfg-3 plateau."""
     out = []
-    bn = (base_t * base_t).sum(1) if metric == 0 else None
+    b64 = base_t.double()
+    bn = (b64 * b64).sum(1) if metric == 0 else None
     for s in range(0, q_t.shape[0], 256):
-        qq = q_t[s:s + 256]
-        dot = qq @ base_t.T
+        qq = q_t[s:s + 256].double()
+        dot = qq @ b64.T
         if metric == 0:
             d = (qq * qq).sum(1)[:, None] + bn[None, :] - 2.0 * dot
             out.append(torch.topk(d, k, largest=False).indices.cpu().numpy())
         else:
             out.append(torch.topk(dot, k, largest=True).indices.cpu().numpy())
+    del b64
     return np.concatenate(out)
 
 
@@ -114,7 +119,7 @@ def run(name, a):
     torch.cuda.empty_cache()
     ids = torch.empty((nb, batch, a.k), dtype=torch.int32, device="cuda")
     dists = torch.empty((nb, batch, a.k), dtype=torch.float32, device="cuda")
-    qs = torch.zeros((nb, batch, 8), dtype=torch.int32, device="cuda")
+    qs = torch.zeros((nb, batch, shine_amd.QS_WORDS), dtype=torch.int32, device="cuda")
     # a.inflight batches in flight per slot (step i on stream set i % inflight), as bench.py does
     streams = [[torch.cuda.Stream() for _ in range(slots)] for _ in range(a.inflight)]
     per = batch // slots  # slot s answers rows [s*per, (s+1)*per) of each batch (id % G in the host API)
@@ -140,7 +145,7 @@ def run(name, a):
         for i in range(nb):
             step(i)
         torch.cuda.synchronize()
-        qs_h = qs.cpu().numpy().view(np.uint32).reshape(-1, 8).copy()
+        qs_h = qs.cpu().numpy().view(np.uint32).reshape(-1, shine_amd.QS_WORDS).copy()
         bad = int((qs_h[:, 6] != 0).sum())
         res = ids.cpu().numpy().view(np.uint32).reshape(-1, a.k)
         recall = D.recall_at_k(res, gt, a.k)

@@ -32,7 +32,7 @@ idx.set_search_mode(shine_amd.MODE_FAST)
 streams = [torch.cuda.Stream() for _ in range(S)]
 ids = torch.empty((nb, 1024, 10), dtype=torch.int32, device="cuda")
 dd = torch.empty((nb, 1024, 10), dtype=torch.float32, device="cuda")
-qs = torch.zeros((nb, 1024, 8), dtype=torch.int32, device="cuda")
+qs = torch.zeros((nb, 1024, 12), dtype=torch.int32, device="cuda")
 
 
 def run(ns):
