@@ -158,7 +158,7 @@ def main():
     idx = shine_amd.Index.open(paths, a.dim, a.M, shine_amd.METRIC_L2, gpus=[local])
     info = idx.info()
     log(f"rank {rank}: index on GPU {local}: {info['num_nodes']} nodes, max level {info['max_level']}, "
-        f"{info['device_bytes'] / 2**20:.0f} MiB")
+        f"{info['device_bytes'] / 2**20:.0f} MiB; device {info['cus']} CUs, {info['lds_per_cu']} B LDS per CU")
 
     # queries: rank r takes ids ≡ r (mod G) of a common pool (read_data.hh:57-58)
     nq_rank = a.batch * a.nbatches

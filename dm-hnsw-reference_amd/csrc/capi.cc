@@ -51,6 +51,7 @@ struct HostBuf {
     n = 0;
     hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(want, 1) * sizeof(T), hipHostMallocDefault);
     if (e != hipSuccess) return set_error(SHINE_ERR_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    std::memset(p, 0, std::max<size_t>(want, 1) * sizeof(T));
     n = want;
     return 0;
   }
@@ -128,10 +129,12 @@ struct ShardedArray {
 struct Scratch {
   DevBuf<uint32_t> visited, vlog, counter, ovf, qs;
   DevBuf<unsigned long long> heaps;  // global-heap pass
+  HostBuf<uint32_t> seen;  // pinned copy of the last call's hand-on counts (sizes the next light pass; may be stale)
   uint32_t slots = 0;
   void release() {
     for (auto* b : {&visited, &vlog, &counter, &ovf, &qs}) b->release();
     heaps.release();
+    seen.release();
     slots = 0;
   }
 };
@@ -159,7 +162,8 @@ struct Replica {
 
 }  // namespace
 
-struct shine_index {
+// Everything a handle holds but its lock: shine_cache_warmup builds a new layout into a second state and moves it in.
+struct IndexState {
   uint32_t dim = 0, M = 0, M0 = 0;
   int metric = 0, elem = 0;
   uint64_t N = 0, upper_rows = 0;
@@ -177,6 +181,13 @@ struct shine_index {
   double cache_fraction = 0;
   Regions regions;             // SHINE_PLACE_SHARDED_REGIONS: slot o owns (and is routed) region o
   std::vector<Replica> reps;
+  // sharded placements: the host graph and its device ids, kept to re-rank the stripes after a cache warmup
+  HostGraph host;
+  std::vector<uint32_t> dev_of;  // dev_of[g] = device id of graph node g
+  std::vector<int> devs;
+};
+
+struct shine_index : IndexState {
   std::mutex mu;
 };
 
@@ -234,7 +245,7 @@ int upload(DevBuf<T>& dst, const T* src, size_t n, hipStream_t s) {
   return 0;
 }
 
-void release_index(shine_index* h) {
+void release_state(IndexState* h) {
   for (auto& R : h->reps) {
     // The whole device drains: a caller stream may already be destroyed (include/shine_gpu.h: stream lifetime), so
     // its handle is never touched here.
@@ -258,6 +269,11 @@ void release_index(shine_index* h) {
   }
   h->svec.release();
   h->sadj0.release();
+  h->reps.clear();
+}
+
+void release_index(shine_index* h) {
+  release_state(h);
   delete h;
 }
 
@@ -334,8 +350,9 @@ int fill_copies(ShardedArray& A, const std::vector<int>& devs) {
   return 0;
 }
 
-int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus, int placement, double cache_fraction,
-               shine_index_t* out) {
+// heat (nullable, indexed by graph node): warmup read counts that rank each stripe's level-0 records for the cache
+int make_index(HostGraph G, int elem, const int* gpu_ids, uint32_t n_gpus, int placement, double cache_fraction,
+               shine_index_t* out, const std::vector<uint32_t>* heat = nullptr) {
   if (!out) return set_error(SHINE_ERR_ARG, "out is NULL");
   if (elem != SHINE_ELEM_F32 && elem != SHINE_ELEM_F16) return set_error(SHINE_ERR_ARG, "elem must be 0 (f32) or 1 (f16)");
   if (placement != SHINE_PLACE_REPLICA && placement != SHINE_PLACE_SHARDED && placement != SHINE_PLACE_SHARDED_REGIONS)
@@ -446,7 +463,8 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
     newid.resize(G.N);
     for (uint32_t o = 0; o < slots; ++o) {
       std::stable_sort(order[o].begin(), order[o].end(), [&](uint32_t a, uint32_t b) {
-        if (G.level[a] != G.level[b]) return G.level[a] > G.level[b];
+        if (G.level[a] != G.level[b]) return G.level[a] > G.level[b];  // upper levels always admitted
+        if (heat && (*heat)[a] != (*heat)[b]) return (*heat)[a] > (*heat)[b];  // warmup reads, most first
         return indeg[a] > indeg[b];
       });
       for (size_t i = 0; i < order[o].size(); ++i) newid[order[o][i]] = static_cast<uint32_t>(o * U + i);
@@ -569,6 +587,11 @@ int make_index(const HostGraph& G, int elem, const int* gpu_ids, uint32_t n_gpus
   } else {
     h->device_bytes = vlen + 4 * G.adj0.size() + replicated;
   }
+  if (sharded) {
+    h->dev_of = std::move(newid);
+    h->host = std::move(G);
+    h->devs = devs;
+  }
   *out = h.release();
   return SHINE_OK;
 }
@@ -634,7 +657,11 @@ uint32_t bitmap_slot_cap(const shine_index* h) {
   return static_cast<uint32_t>(std::max<uint64_t>(kGlobalSlots, std::min<uint64_t>(1u << 20, kBitmapBudget / per)));
 }
 
-LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint32_t ef, int pass) {
+// handed: queries the main pass handed on in an earlier call on this stream.  The light pass gets slots for twice
+// that (at least one per CU, at most what LDS shares and bitmap memory allow): its workgroups of a call with few
+// overflows exit at once, and a launch of thousands of them delays the stream's next batch (-7 % QPS at ef = 32).
+LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint32_t ef, int pass,
+                       uint32_t handed = 0xFFFFFFFFu) {
   LaunchShape sh{};
   const uint64_t top_bytes = align16(8ull * ef);
   const uint32_t cus = R.cus, lds = R.lds_per_cu;
@@ -658,7 +685,7 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
   } else {  // PASS_LIGHT: as many slots as the LDS shares allow, capped by the HBM its bitmaps take
     sh.vis_cap = 0;
     budget = kLightFixupLds;
-    wpc = std::max<uint32_t>(1, static_cast<uint32_t>(lds / kLightFixupLds));
+    wpc = static_cast<uint32_t>(env_int("SHINE_DEBUG_LIGHT_WPC", std::max<uint32_t>(1, static_cast<uint32_t>(lds / kLightFixupLds))));
   }
   const int64_t cap = (static_cast<int64_t>(budget) - static_cast<int64_t>(top_bytes) - 4ll * sh.vis_cap - 512) / 8;
   sh.cap = static_cast<uint32_t>(std::max<int64_t>(cap & ~1ll, 2));
@@ -666,7 +693,11 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
   if (pass == PASS_LIGHT) sh.cap = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_DEBUG_LIGHT_CAP", sh.cap)));
   sh.vis_limit = sh.vis_cap / 8 * 7;  // linear probing stays short; >= 64 free slots for one expansion
   sh.grid = std::max<uint32_t>(1, std::min<uint32_t>(nq, cus * wpc));
-  if (pass == PASS_LIGHT) sh.grid = std::min(sh.grid, bitmap_slot_cap(h));
+  if (pass == PASS_LIGHT) {
+    sh.grid = std::min(sh.grid, bitmap_slot_cap(h));
+    const uint64_t want = std::max<uint64_t>(cus, (2ull * handed + 63) / 64 * 64);
+    sh.grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(sh.grid, want)));
+  }
   return sh;
 }
 
@@ -706,14 +737,17 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   const int start = static_cast<int>(env_int("SHINE_DEBUG_START_MODE", 0));  // test hook: the fallback passes alone
   const bool fast_mode = h->search_mode == SHINE_MODE_FAST;
   const bool fast_kernel = fast_mode && ef <= kFastMaxEf && h->M0 <= 64;
+  if (int rc = S.seen.grow(4)) return rc;
+  const uint32_t handed = S.seen.p[3] ? S.seen.p[0] : 0;  // [3] = 1 once a call has written the counts
   int chain[3], n_pass = 0;
   if (start <= 0) chain[n_pass++] = fast_kernel ? PASS_FAST : PASS_LDS;
   else if (start == 1) chain[n_pass++] = PASS_WHOLE_CU;
   if (start <= 2) chain[n_pass++] = PASS_LIGHT;
-  chain[n_pass++] = PASS_GLOBAL;
+  if (!env_int("SHINE_DEBUG_NO_GLOBAL", 0)) chain[n_pass++] = PASS_GLOBAL;  // measurement hook
   for (int i = 0; i < n_pass; ++i) {
     const int pass = chain[i];
-    const LaunchShape sh = pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu) : pick_shape(h, R, nq, ef, pass);
+    const LaunchShape sh =
+        pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu) : pick_shape(h, R, nq, ef, pass, handed);
     SearchArgs a{};
     a.g = dev_graph(h, R);
     if (!a.g.vec || !a.g.adj0 || !a.g.uid || !a.g.up_base)
@@ -765,6 +799,8 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("search launch: ") + hipGetErrorString(e));
   }
   if (timed) HIP_TRY(hipEventRecord(R.ev1, s));
+  HIP_TRY(hipMemcpyAsync(S.seen.p, S.counter.p + 4, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  S.seen.p[3] = 1;
   return 0;
 }
 
@@ -850,7 +886,7 @@ int shine_open_buffers_ex(const uint8_t* const* dumps, const uint64_t* sizes, ui
   if (metric != SHINE_METRIC_L2 && metric != SHINE_METRIC_IP) return set_error(SHINE_ERR_ARG, "metric must be 0 or 1");
   HostGraph G;
   if (int rc = parse_dumps(dumps, sizes, n_dumps, dim, M, metric, 0, G)) return rc;
-  return make_index(G, elem, gpu_ids, n_gpus, placement, cache_fraction, out);
+  return make_index(std::move(G), elem, gpu_ids, n_gpus, placement, cache_fraction, out);
 }
 
 int shine_open_ex(const char* const* dump_paths, uint32_t n_dumps, uint32_t dim, uint32_t M, int metric, int elem,
@@ -907,6 +943,10 @@ int shine_index_get_info(shine_index_t h, shine_index_info* o) {
   o->placement = static_cast<uint32_t>(h->placement);
   o->id_space = h->id_space;
   o->cache_fraction = h->cache_fraction;
+  if (!h->reps.empty()) {
+    o->cus = h->reps[0].cus;
+    o->lds_per_cu = h->reps[0].lds_per_cu;
+  }
   return SHINE_OK;
 }
 
@@ -937,13 +977,14 @@ int shine_knn_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_qu
   return enqueue_search(h, R, d_queries, nq, k, ef, d_out_ids, d_out_dists, qs, s, false);
 }
 
-int shine_knn_batch(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
-                    uint32_t ef, uint32_t* out_ids, float* out_dists, uint32_t* qstats, shine_stats* stats) {
-  if (int rc = check_knn_args(h, k, ef)) return rc;
-  if (stats) std::memset(stats, 0, sizeof(*stats));
-  if (nq == 0) return SHINE_OK;
-  if (!queries || !out_ids) return set_error(SHINE_ERR_ARG, "NULL host pointer");
-  std::lock_guard<std::mutex> lk(h->mu);
+}  // extern "C"
+
+namespace {
+
+// shine_knn_batch with the handle locked.  access (nullable): per-slot device counters of record reads (warmup).
+int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k, uint32_t ef,
+             uint32_t* out_ids, float* out_dists, uint32_t* qstats, shine_stats* stats,
+             std::vector<DevBuf<uint32_t>>* access) {
   const uint32_t G = static_cast<uint32_t>(h->reps.size());
   const size_t d = h->dim;
   if (env_int("SHINE_DEBUG_VALIDATE", 0))
@@ -972,7 +1013,9 @@ int shine_knn_batch(shine_index_t h, const float* queries, const uint32_t* query
     for (uint32_t j = 0; j < n; ++j)
       std::memcpy(R.hq.p + j * d, queries + static_cast<size_t>(part[r][j]) * d, d * sizeof(float));
     HIP_TRY(hipMemcpyAsync(R.q.p, R.hq.p, n * d * sizeof(float), hipMemcpyHostToDevice, R.stream));
-    if (int rc = enqueue_search(h, R, R.q.p, n, k, ef, R.ids.p, R.d.p, R.main.qs.p, R.stream, true)) return rc;
+    if (int rc = enqueue_search(h, R, R.q.p, n, k, ef, R.ids.p, R.d.p, R.main.qs.p, R.stream, true,
+                                access ? (*access)[r].p : nullptr))
+      return rc;
     HIP_TRY(hipMemcpyAsync(R.hids.p, R.ids.p, static_cast<size_t>(n) * k * 4, hipMemcpyDeviceToHost, R.stream));
     HIP_TRY(hipMemcpyAsync(R.hd.p, R.d.p, static_cast<size_t>(n) * k * 4, hipMemcpyDeviceToHost, R.stream));
     HIP_TRY(hipMemcpyAsync(R.hqs.p, R.main.qs.p, static_cast<size_t>(n) * kQsWords * 4, hipMemcpyDeviceToHost,
@@ -1026,6 +1069,67 @@ int shine_knn_batch(shine_index_t h, const float* queries, const uint32_t* query
   agg.kernel_ms = kernel_ms;
   if (stats) *stats = agg;
   return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int shine_knn_batch(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
+                    uint32_t ef, uint32_t* out_ids, float* out_dists, uint32_t* qstats, shine_stats* stats) {
+  if (int rc = check_knn_args(h, k, ef)) return rc;
+  if (stats) std::memset(stats, 0, sizeof(*stats));
+  if (nq == 0) return SHINE_OK;
+  if (!queries || !out_ids) return set_error(SHINE_ERR_ARG, "NULL host pointer");
+  std::lock_guard<std::mutex> lk(h->mu);
+  return knn_host(h, queries, query_ids, nq, k, ef, out_ids, out_dists, qstats, stats, nullptr);
+}
+
+int shine_cache_warmup(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
+                       uint32_t ef) {
+  if (int rc = check_knn_args(h, k, ef)) return rc;
+  if (nq == 0) return SHINE_OK;
+  if (!queries) return set_error(SHINE_ERR_ARG, "NULL host pointer");
+  std::lock_guard<std::mutex> lk(h->mu);
+  const uint32_t G = static_cast<uint32_t>(h->reps.size());
+  if (h->placement == SHINE_PLACE_REPLICA || G < 2 || h->cached_rows == 0) return SHINE_OK;  // nothing is cached
+  if (h->host.N == 0 || h->dev_of.size() != h->host.N)
+    return set_error(SHINE_ERR_ARG, "the index's host graph is gone (an earlier warmup failed): reopen it");
+  // 1. the warmup split, with every record read counted per slot (the reference's warmup run, compute_node.cc:116-131)
+  std::vector<DevBuf<uint32_t>> access(G);
+  auto free_access = [&]() {
+    for (uint32_t r = 0; r < G; ++r) {
+      (void)hipSetDevice(h->reps[r].device);
+      access[r].release();
+    }
+  };
+  for (uint32_t r = 0; r < G; ++r) {
+    HIP_TRY(hipSetDevice(h->reps[r].device));
+    if (int rc = access[r].grow(h->id_space)) return free_access(), rc;
+    HIP_TRY(hipMemsetAsync(access[r].p, 0, h->id_space * 4, h->reps[r].stream));
+  }
+  std::vector<uint32_t> ids(static_cast<size_t>(nq) * k);
+  if (int rc = knn_host(h, queries, query_ids, nq, k, ef, ids.data(), nullptr, nullptr, nullptr, &access))
+    return free_access(), rc;
+  // 2. admission ranking: reads summed over the slots, per graph node
+  std::vector<uint32_t> part(h->id_space), heat(h->host.N, 0);
+  for (uint32_t r = 0; r < G; ++r) {
+    HIP_TRY(hipSetDevice(h->reps[r].device));
+    HIP_TRY(hipMemcpy(part.data(), access[r].p, h->id_space * 4, hipMemcpyDeviceToHost));
+    for (uint64_t g = 0; g < h->host.N; ++g) heat[g] += part[h->dev_of[g]];
+  }
+  free_access();
+  // 3. the same stripes re-laid out hottest first (a new layout beside the old one, then moved in)
+  shine_index_t nh = nullptr;
+  const std::vector<int> devs = h->devs;
+  if (int rc = make_index(std::move(h->host), h->elem, devs.data(), static_cast<uint32_t>(devs.size()), h->placement,
+                          h->cache_fraction, &nh, &heat))
+    return rc;
+  nh->search_mode = h->search_mode;
+  release_state(h);
+  static_cast<IndexState&>(*h) = std::move(static_cast<IndexState&>(*nh));
+  delete nh;  // its state was moved out: nothing left to release
+  return SHINE_OK;
 }
 
 int shine_release_stream(shine_index_t h, void* stream) {

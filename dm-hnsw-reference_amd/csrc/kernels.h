@@ -36,7 +36,7 @@ struct SearchArgs {
   uint32_t vis_limit;     // entries allowed in the LDS table before the query is re-run with more LDS
   uint32_t* out_ids;      // [nq_total][k]
   float* out_dists;       // [nq_total][k] (nullable)
-  uint32_t* qstats;       // [nq_total][8] (nullable)
+  uint32_t* qstats;       // [nq_total][kQsWords] (nullable)
   uint32_t* visited;      // [slots][words_per_slot] bitmaps, all-zero between queries
   uint64_t words_per_slot;
   uint32_t* vlog;         // [slots][log_cap] ids whose visited bit is set (for clearing)
@@ -94,6 +94,15 @@ __host__ __device__ inline uint32_t permuted_index(uint32_t dim, uint32_t i) {
 }
 
 bool dim_supported(uint32_t dim, int elem);
+
+// The compiled vector dimensions: one translation unit each (kernels_dim.hip built with -DSHINE_DIM=D), so the
+// kernel instantiations compile in parallel.  fp16 records (config 5) exist for 96, 128 and 200.
+#define SHINE_DIMS(X) X(16) X(32) X(64) X(96) X(100) X(128) X(200) X(256)
+#define SHINE_DECLARE_DIM(DD)                                                                                       \
+  hipError_t launch_search_d##DD(int metric, int elem, uint32_t grid, const SearchArgs& a, hipStream_t s);          \
+  hipError_t launch_distance_d##DD(int metric, int elem, const DistArgs& a, hipStream_t s);
+SHINE_DIMS(SHINE_DECLARE_DIM)
+#undef SHINE_DECLARE_DIM
 
 // Returns hipSuccess or the launch error.  grid = number of persistent search slots (one wavefront each).
 hipError_t launch_search(uint32_t dim, int metric, int elem, uint32_t grid, const SearchArgs& a, hipStream_t s);

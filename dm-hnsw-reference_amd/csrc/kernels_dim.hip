@@ -1,0 +1,35 @@
+// One vector dimension's kernel instantiations (built once per dimension with -DSHINE_DIM=D; see kernels.h).
+#include "kernels_impl.h"
+
+#ifndef SHINE_DIM
+#error "build with -DSHINE_DIM=<dimension>"
+#endif
+
+#define SHINE_CAT2(a, b) a##b
+#define SHINE_CAT(a, b) SHINE_CAT2(a, b)
+
+namespace shine {
+
+hipError_t SHINE_CAT(launch_search_d, SHINE_DIM)(int metric, int elem, uint32_t grid, const SearchArgs& a,
+                                                 hipStream_t s) {
+  if (elem == 0)
+    return metric == 0 ? launch_search_t<SHINE_DIM, 0, float>(grid, a, s) : launch_search_t<SHINE_DIM, 1, float>(grid, a, s);
+#if SHINE_DIM == 96 || SHINE_DIM == 128 || SHINE_DIM == 200
+  if (elem == 1)
+    return metric == 0 ? launch_search_t<SHINE_DIM, 0, __half>(grid, a, s)
+                       : launch_search_t<SHINE_DIM, 1, __half>(grid, a, s);
+#endif
+  return hipErrorInvalidValue;
+}
+
+hipError_t SHINE_CAT(launch_distance_d, SHINE_DIM)(int metric, int elem, const DistArgs& a, hipStream_t s) {
+  if (elem == 0)
+    return metric == 0 ? launch_distance_t<SHINE_DIM, 0, float>(a, s) : launch_distance_t<SHINE_DIM, 1, float>(a, s);
+#if SHINE_DIM == 96 || SHINE_DIM == 128 || SHINE_DIM == 200
+  if (elem == 1)
+    return metric == 0 ? launch_distance_t<SHINE_DIM, 0, __half>(a, s) : launch_distance_t<SHINE_DIM, 1, __half>(a, s);
+#endif
+  return hipErrorInvalidValue;
+}
+
+}  // namespace shine

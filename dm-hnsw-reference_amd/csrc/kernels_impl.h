@@ -1,0 +1,1325 @@
+// gfx950 (CDNA4) kernels of the SHINE compute-node query path (device code and launch templates; included by
+// kernels.hip and by one kernels_dim.hip translation unit per vector dimension, compiled in parallel).
+//
+//   search_kernel   HNSW::knn (src/hnsw/hnsw.hh:253-307): greedy descent search_for_one (:331-393) and the
+//                   level-0 best-first beam search search_level (:406-476), one query per wavefront,
+//                   persistent workgroups pulling queries from a device work queue.
+//   distance_kernel Distance::dist (src/hnsw/distance.hh:153-161) over gathered (query, node) pairs.
+//   heap_replay     diagnostics: the device heap routines driven by an op list (tests pin them to libstdc++).
+//
+// Exactness.  Distances are evaluated in exactly the oracle's floating-point order (oracle/oracle.cc): eight
+// lanes of a wavefront play the eight AVX2 accumulators of L2SqrSIMD16ExtAVX / InnerProductSIMD16ExtAVX
+// (distance.hh:11-76) — lane a owns elements i ≡ a (mod 8) of the 16-aligned prefix and runs the same fmaf
+// chain — the eight partial sums are added left to right, then the scalar tail.  The two candidate queues are
+// the reference's std::vector heaps (heap.hh) kept in LDS and updated with exactly the libstdc++ algorithms
+// (bits/stl_heap.h: __push_heap, __adjust_heap, __pop_heap), so ties between equal distances are broken as on
+// the CPU and results come out in the same heap-array order (hnsw.hh:300-303).
+//
+// Wave-parallel heap operations (one query = one wavefront, all 64 lanes cooperate on each operation):
+//   push   the ancestors of the new slot are loaded in one LDS round, each lane compares its ancestor with the
+//          new key, and the length of the run of moves (a ballot + ctz) fixes the final slot; the moved
+//          ancestors are stored in one more round.  (std::__push_heap walks the same chain one level at a time.)
+//   pop    std::__adjust_heap's hole walks from the root to a leaf always taking the child the comparator
+//          prefers, independently of the value being re-inserted.  The walk is resolved five levels per LDS
+//          round: 62 lanes load the 5-level subtree under the hole, 31 lanes compare sibling pairs, and the
+//          ballot of "right child wins" bits is walked with scalar bit tests.  The final std::__push_heap of the
+//          last element climbs back up that same path, so its stopping point is one more ballot, and all moves
+//          are written in one round.
+// Expansion step (search_level): pop the closest candidate; its 2M-entry adjacency row is one coalesced
+// 128-/256-byte load (one u32 per lane), issued speculatively during the previous step's accept phase for the
+// predicted next candidate; the visited test-and-set is an exact open-addressing hash table in LDS (CAS per
+// lane); fresh neighbours' vectors are gathered 8 per wave-instruction group and reduced; the accept / push /
+// push_k sequence (:456-465) is replayed in list order with the parallel heap operations.
+#pragma once
+
+#include "kernels.h"
+
+#include <hip/hip_fp16.h>
+
+#include <type_traits>
+
+namespace shine {
+namespace {
+
+using u32 = uint32_t;
+using u64 = uint64_t;
+constexpr u32 INV = 0xFFFFFFFFu;
+constexpr u32 ST_OVERFLOW = 6;  // SHINE_ERR_OVERFLOW
+constexpr u32 ST_FORMAT = 3;    // SHINE_ERR_FORMAT
+
+__device__ __forceinline__ float key(u64 e) { return __uint_as_float(static_cast<u32>(e)); }
+__device__ __forceinline__ u32 eid(u64 e) { return static_cast<u32>(e >> 32); }
+__device__ __forceinline__ u64 mk(float d, u32 id) { return (static_cast<u64>(id) << 32) | __float_as_uint(d); }
+
+__device__ __forceinline__ u32 bcast(u32 v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ u64 bcast64(u64 v) {
+  return (static_cast<u64>(bcast(static_cast<u32>(v >> 32))) << 32) | bcast(static_cast<u32>(v));
+}
+// Cross-lane LDS hand-off inside one wavefront: DS instructions of a wave execute in order, so only compiler
+// code motion has to be stopped.
+__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(__half x) { return __half2float(x); }
+
+// ------------------------------------------------------------------------------------------------------------
+// Heaps of packed {dist, id} entries in LDS.
+//   MAXH = true : heap::MaxHeapCompare (lhs.distance < rhs.distance), heap.hh:15-17
+//   MAXH = false: heap::MinHeapCompare (lhs.distance > rhs.distance), heap.hh:19-21
+// ------------------------------------------------------------------------------------------------------------
+template <bool MAXH>
+__device__ __forceinline__ bool hcmp(float a, float b) {
+  return MAXH ? (a < b) : (a > b);
+}
+
+// push_back(v) + std::push_heap on h[0..n]  ≡  std::__push_heap(h, n, 0, v).  Returns the new root given the
+// old one (root0; ignored when n == 0).
+template <bool MAXH>
+__device__ __forceinline__ u64 heap_push(u64* h, int n, u64 v, u64 root0, int lane) {
+  const float vd = key(v);
+  const int L = 31 - __clz(n + 1);  // ancestors of slot n
+  u64 ent = 0;
+  bool c = false;
+  if (lane < L) {  // lane t holds ancestor t+1
+    ent = h[((n + 1) >> (lane + 1)) - 1];
+    c = hcmp<MAXH>(key(ent), vd);  // parent moves down while comp(parent, value)
+  }
+  const u64 C = __ballot(c);
+  const int s = static_cast<int>(__builtin_ctzll(~C));  // moves happen for the first s ancestors
+  if (lane < s) h[lane == 0 ? n : ((n + 1) >> lane) - 1] = ent;
+  const int fin = s == 0 ? n : ((n + 1) >> s) - 1;
+  if (lane == 0) h[fin] = v;
+  wave_sync();
+  return fin == 0 ? v : root0;
+}
+
+// General form (any keys, NaN included): the value's landing slot is found bottom-up like std::__push_heap.
+// std::pop_heap on h[0..n) followed by pop_back  ≡  std::__adjust_heap(h, 0, n-1, h[n-1]).  Returns the new
+// root (meaningless when n <= 1).
+//
+// The hole's walk is resolved six levels per LDS round: lane i plays internal node i+1 (1-based) of the
+// 63-node window below the hole, reads both children's keys (adjacent slots: one ds_read2_b32) and votes
+// "right child wins"; the walk then follows the ballot with scalar bit tests.
+template <bool MAXH>
+__device__ __forceinline__ u64 heap_pop_any(u64* h, int n, int lane) {
+  if (n <= 1) return 0;
+  const int len = n - 1;
+  const u64 value = h[len];
+  const float vk = key(value);
+  const int lim = (len - 1) / 2;  // the hole has two children while hole < lim
+  const u32* hk = reinterpret_cast<const u32*>(h);
+  const int j1 = lane + 1;
+  const int lj = 31 - __clz(j1);
+  const int oj = j1 - (1 << lj);
+  int pos = 0, L = 0, my_child = 0;  // lane t: the path's (t+1)-th node
+  while (pos < lim) {
+    const int a = ((pos + 1) << lj) - 1 + oj;  // this lane's node
+    const int c1 = 2 * a + 1;
+    bool right = false;
+    if (lane < 63 && c1 + 1 < len) {
+      const float lk = __uint_as_float(hk[2 * c1]);
+      const float rk = __uint_as_float(hk[2 * c1 + 2]);
+      right = !hcmp<MAXH>(rk, lk);  // libstdc++ takes the left child iff comp(right, left)
+    }
+    const u64 W = __ballot(right);
+    int r1 = 1;
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      if (pos >= lim) break;
+      const int b = static_cast<int>((W >> (r1 - 1)) & 1ull);
+      const int child = 2 * pos + 1 + b;
+      if (lane == L) my_child = child;
+      ++L;
+      pos = child;
+      r1 = 2 * r1 + b;
+    }
+  }
+  if ((len & 1) == 0 && pos == (len - 2) / 2) {  // lone left child
+    const int child = 2 * pos + 1;
+    if (lane == L) my_child = child;
+    ++L;
+    pos = child;
+  }
+  // std::__push_heap(h, hole = path end, 0, value) climbs the same path
+  u64 ent = 0;
+  bool c = false;
+  if (lane < L) {
+    ent = h[my_child];
+    c = hcmp<MAXH>(key(ent), vk);
+  }
+  const u64 C = __ballot(c);
+  const u64 stay = ~C & (L >= 64 ? ~0ull : ((1ull << L) - 1));
+  const int j = stay ? 64 - __clzll(stay) : 0;  // value lands on the path's j-th node
+  const int pj = j == 0 ? 0 : __shfl(my_child, j - 1);
+  if (lane < j) h[(my_child - 1) >> 1] = ent;  // path nodes above the landing slot shift up
+  if (lane == 0) h[pj] = value;
+  wave_sync();
+  return j == 0 ? value : bcast64(ent);  // lane 0 holds the path's first node
+}
+
+// Fast form for NaN-free heaps.  Along any root-to-leaf path of a heap the keys are monotone, so the
+// comparisons std::__push_heap makes on its way back up are false on a prefix of the path and true below it:
+// every path node whose winning child the comparator does not rank past the value shifts up, the first one
+// that does marks the landing slot.  Each 6-level window costs one LDS round trip: lane i plays window node
+// i+1 (1-based), reads both children entries (adjacent slots: one ds_read2_b64) and votes for the right
+// child; the walk follows the ballot on SGPRs; the on-path lanes then shift their winner up in place.
+template <bool MAXH>
+__device__ __forceinline__ u64 heap_pop(u64* h, int n, int lane) {
+  if (n <= 1) return 0;
+  const int len = n - 1;
+  const u64 value = h[len];
+  const float vk = key(value);
+  const int lim = (len - 1) / 2;  // the hole has two children while hole < lim
+  const int j1 = lane + 1;        // window node (1-based) of this lane
+  const int lj = 31 - __clz(j1);
+  const int oj = j1 - (1 << lj);
+  int P1 = 1;  // window root, 1-based heap index
+  u64 root = value;
+  for (int round = 0;; ++round) {
+    const int a1 = (P1 << lj) + oj;  // this lane's node, 1-based
+    const int c1 = 2 * a1 - 1;       // its left child, 0-based
+    u64 le = 0, re = 0;
+    if (lane < 63 && c1 < len) {
+      le = h[c1];
+      re = h[c1 + 1];
+    }
+    const bool right = lane < 63 && c1 + 1 < len && !hcmp<MAXH>(key(re), key(le));
+    const u64 we = right ? re : le;  // the child the hole would move into
+    const u64 W = __ballot(right);
+    int P = P1, r1 = 1, steps = 0;
+    while (steps < 6 && P - 1 < lim) {
+      const int b = static_cast<int>((W >> (r1 - 1)) & 1ull);
+      r1 = 2 * r1 + b;
+      P = 2 * P + b;
+      ++steps;
+    }
+    const bool lone = (len & 1) == 0 && P - 1 == (len - 2) / 2;  // a last node with only a left child
+    bool more = steps == 6 && (P - 1 < lim || lone);
+    if (!more && lone) {
+      r1 = 2 * r1;
+      P = 2 * P;
+      ++steps;
+    }
+    const bool onp = lane < 63 && lj < steps && (r1 >> (steps - lj)) == j1;
+    const bool up = onp && !hcmp<MAXH>(key(we), vk);  // no move back down: the winner stays shifted up
+    const int k = __popcll(__ballot(up));
+    if (up) h[a1 - 1] = we;
+    if (round == 0) root = k == 0 ? value : bcast64(we);  // lane 0 is the root
+    if (k < steps) {
+      if (lane == 0) h[(P >> (steps - k)) - 1] = value;
+      break;
+    }
+    if (!more) {
+      if (lane == 0) h[P - 1] = value;
+      break;
+    }
+    P1 = P;
+  }
+  wave_sync();
+  return root;
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Distance evaluation in the oracle's FP order.  A "pass" evaluates 16 vectors: lane l of the wavefront belongs
+// to group g = l >> 2 (the vector, or slot) and plays the two AVX2 accumulators 2c and 2c+1, c = l & 3, as the
+// two halves of a packed-FP32 register pair: each half runs the scalar fmaf chain of its accumulator
+// (distance.hh:11-76), so v_pk_fma_f32 does two accumulators per instruction.  Rows are stored in the device
+// layout of kernels.h (permuted_index): one 16-byte load (f32; 8 bytes for f16) brings elements t and t+1 of
+// both of the lane's accumulators, already paired, and the 4 lanes of a group read 64 contiguous bytes.  The
+// eight partial sums are folded left to right, ((((a0 + a1) + a2) ... ) + a7), by a 3-step DPP row_shr:1 chain
+// that ends in the group's lane c = 3, which then adds the scalar tail.
+// ------------------------------------------------------------------------------------------------------------
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int D, typename E>
+struct Lay {
+  static constexpr int DB = D >> 4 << 4;  // elements handled by the SIMD16 kernel (qty16 << 4)
+  static constexpr int PER = DB / 8;      // elements per accumulator
+  static constexpr int NCH = PER / 2;     // 4-element chunks per lane
+  static constexpr int TAIL = D - DB;     // scalar tail (distance.hh:112-115, 136-139)
+  static constexpr int TAILA = TAIL > 0 ? TAIL : 1;
+  static_assert(DB >= 16, "dimension must be >= 16");
+};
+
+template <int D>
+struct QueryRegs {
+  f32x2 q2[D / 16 * 2];  // {q[2c + 8t], q[2c + 1 + 8t]}, t < PER
+  float qt[(D & 15) > 0 ? (D & 15) : 1];
+};
+
+template <int D>
+__device__ __forceinline__ void load_query(const float* __restrict__ q, int lane, QueryRegs<D>& Q) {
+  constexpr int DB = D >> 4 << 4, PER = DB / 8, TAIL = D - DB;
+  const int c2 = 2 * (lane & 3);
+#pragma unroll
+  for (int t = 0; t < PER; ++t) Q.q2[t] = f32x2{q[c2 + 8 * t], q[c2 + 1 + 8 * t]};
+#pragma unroll
+  for (int t = 0; t < TAIL; ++t) Q.qt[t] = q[DB + t];
+}
+
+// One chunk = elements (t, t+1) of accumulators (2c, 2c+1): f32 → 4 floats, f16 → 4 halves in 2 words.
+template <typename E>
+struct ChunkT {
+  using type = f32x4;
+};
+template <>
+struct ChunkT<__half> {
+  using type = uint2;
+};
+
+// The neighbour vectors of P passes (16 slots each) in VGPRs.
+template <int D, typename E, int P>
+struct NbrBuf {
+  using L = Lay<D, E>;
+  typename ChunkT<E>::type x[P][L::NCH];
+  float xt[P][L::TAILA];  // scalar tail, lane c = 3 only
+};
+
+// Issue the loads of pass p: this lane's group evaluates node `id` (INV: nothing to load).
+template <int D, typename E, int P>
+__device__ __forceinline__ void issue_pass(NbrBuf<D, E, P>& B, int p, const E* __restrict__ vec, u32 id, int c4) {
+  using L = Lay<D, E>;
+  using C = typename ChunkT<E>::type;
+  if (id != INV) {
+    const E* row = vec + static_cast<u64>(id) * D;
+#pragma unroll
+    for (int u = 0; u < L::NCH; ++u) B.x[p][u] = *reinterpret_cast<const C*>(row + u * 16 + c4 * 4);
+    if (c4 == 3) {
+#pragma unroll
+      for (int t = 0; t < L::TAIL; ++t) B.xt[p][t] = to_f32(row[L::DB + t]);
+    }
+  }
+}
+
+// Unconditional form: always the same number of load instructions (an INV slot reads the local node `pad` and is
+// ignored), so that the compiler's vmcnt bookkeeping stays exact across the software pipeline of search_fast_kernel.
+template <int D, typename E, int P>
+__device__ __forceinline__ void issue_pass_u(NbrBuf<D, E, P>& B, int p, const E* __restrict__ vec, u32 id, u32 pad,
+                                             int c4) {
+  using L = Lay<D, E>;
+  using C = typename ChunkT<E>::type;
+  const E* row = vec + static_cast<u64>(id == INV ? pad : id) * D;
+#pragma unroll
+  for (int u = 0; u < L::NCH; ++u) B.x[p][u] = *reinterpret_cast<const C*>(row + u * 16 + c4 * 4);
+#pragma unroll
+  for (int t = 0; t < L::TAIL; ++t) B.xt[p][t] = to_f32(row[L::DB + t]);
+}
+
+__device__ __forceinline__ f32x2 half2_to_f32x2(u32 w) {
+  return f32x2{__half2float(__ushort_as_half(static_cast<unsigned short>(w & 0xFFFFu))),
+               __half2float(__ushort_as_half(static_cast<unsigned short>(w >> 16)))};
+}
+
+// Left fold of a group's 8 accumulators (lane c holds 2c, 2c+1) into its lane c = 3.
+__device__ __forceinline__ float fold8(f32x2 acc) {
+  float s = acc.x + acc.y;
+#pragma unroll
+  for (int j = 1; j < 4; ++j)
+    s = (__int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x111, 0xF, 0xF, false)) + acc.x) + acc.y;
+  return s;
+}
+
+template <int D, int METRIC>
+__device__ __forceinline__ float add_tail(const QueryRegs<D>& Q, const float* xt, float s) {
+  constexpr int TAIL = D & 15;
+  if constexpr (METRIC == 0) {
+#pragma unroll
+    for (int t = 0; t < TAIL; ++t) {
+      const float df = Q.qt[t] - xt[t];
+      s = __builtin_fmaf(df, df, s);
+    }
+    return s;
+  } else {
+    float tl = 0.f;
+#pragma unroll
+    for (int t = 0; t < TAIL; ++t) tl = __builtin_fmaf(Q.qt[t], xt[t], tl);
+    return 1.0f - (s + tl);
+  }
+}
+
+template <int METRIC>
+__device__ __forceinline__ f32x2 acc_step(f32x2 q, f32x2 x, f32x2 acc) {
+  if constexpr (METRIC == 0) {
+    const f32x2 df = q - x;
+    return __builtin_elementwise_fma(df, df, acc);
+  } else {
+    return __builtin_elementwise_fma(q, x, acc);
+  }
+}
+
+// out[p] = distance of the pass-p vector of this lane's group; valid in lanes c = 3.
+template <int D, int METRIC, typename E, int P>
+__device__ __forceinline__ void pass_dists(const QueryRegs<D>& Q, const NbrBuf<D, E, P>& B, float (&out)[P]) {
+  using L = Lay<D, E>;
+  f32x2 acc[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) acc[p] = f32x2{0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < L::NCH; ++u) {
+#pragma unroll
+    for (int p = 0; p < P; ++p) {  // P independent chains interleaved
+      f32x2 x0, x1;
+      if constexpr (std::is_same_v<E, float>) {
+        x0 = B.x[p][u].xy;
+        x1 = B.x[p][u].zw;
+      } else {
+        x0 = half2_to_f32x2(B.x[p][u].x);
+        x1 = half2_to_f32x2(B.x[p][u].y);
+      }
+      acc[p] = acc_step<METRIC>(Q.q2[2 * u], x0, acc[p]);
+      acc[p] = acc_step<METRIC>(Q.q2[2 * u + 1], x1, acc[p]);
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < P; ++p) out[p] = add_tail<D, METRIC>(Q, B.xt[p], fold8(acc[p]));
+}
+
+// sc_d[j] = dist(q, vec[sc_ids[j]]) for j < n.  All 64 lanes must call it.
+template <int D, int METRIC, typename E>
+__device__ __forceinline__ void dist_list(const E* __restrict__ vec, const QueryRegs<D>& Q, const u32* sc_ids,
+                                          float* sc_d, int n, int lane) {
+  constexpr int P = 2;
+  const int g4 = lane >> 2, c4 = lane & 3;
+  for (int p0 = 0; p0 < n; p0 += 16 * P) {
+    NbrBuf<D, E, P> B;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const int slot = p0 + 16 * p + g4;
+      issue_pass<D, E, P>(B, p, vec, slot < n ? sc_ids[slot] : INV, c4);
+    }
+    float out[P];
+    pass_dists<D, METRIC, E, P>(Q, B, out);
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const int slot = p0 + 16 * p + g4;
+      if (c4 == 3 && slot < n) sc_d[slot] = out[p];
+    }
+  }
+}
+
+// Exact visited set (hashset_t<RemotePtr>, types.hh:14-15) on dense node ids.
+//   VIS = 0: open-addressing table of u32 keys in LDS, linear probing, LDS compare-and-swap per lane.
+//   VIS = 1: per-slot bitmap in HBM (atomicOr test-and-set) + a log of set ids for clearing (large-LDS fallback).
+__device__ __forceinline__ u32 vhash(u32 key, u32 shift) { return (key * 0x9E3779B1u) >> shift; }
+
+// ------------------------------------------------------------------------------------------------------------
+// Read accounting (qstats words 8-11): the reads a search makes of records outside its GPU's own stripe, split
+// into those served by the local copies (cache hits) and those that cross xGMI — the analogue of the
+// reference's rdma_reads_in_bytes / cache_hits / cache_misses (rdma_reads.hh:12,46; statistics.hh:148-175).
+// Counted per wave step with ballots; a replica index (sharded = 0) skips it on a uniform branch.  With
+// A.access set (cache warmup), every record read is also counted per device id for the admission ranking.
+// ------------------------------------------------------------------------------------------------------------
+struct ReadCount {
+  u32 vec_remote = 0, list_remote = 0, vec_cached = 0, list_cached = 0;
+};
+
+__device__ __forceinline__ u32 read_class(const DevGraph& g, u32 x) {  // 0 own stripe, 1 cached copy, 2 xGMI
+  const u32 s = __umulhi(x, g.div_magic) >> g.div_shift;
+  const u32 r = x - s * g.stripe_ids;
+  return s == g.slot ? 0u : (r < g.cached_rows ? 1u : 2u);
+}
+
+// vector reads of the lanes with `active` set (each reads record x).  ACCT = false (replica, no warmup) compiles
+// the accounting out of the search loop.
+template <bool ACCT>
+__device__ __forceinline__ void count_vec_reads(const SearchArgs& A, ReadCount& rc, bool active, u32 x) {
+  if constexpr (!ACCT) return;
+  if (A.g.sharded) {
+    const u32 c = active ? read_class(A.g, x) : 0u;
+    rc.vec_remote += __popcll(__ballot(c == 2u));
+    rc.vec_cached += __popcll(__ballot(c == 1u));
+  }
+  if (A.access && active) atomicAdd(&A.access[x], 1u);
+}
+
+// one neighbour-list read of record x (x uniform over the wave)
+template <bool ACCT>
+__device__ __forceinline__ void count_list_read(const SearchArgs& A, ReadCount& rc, u32 x, int lane) {
+  if constexpr (!ACCT) return;
+  if (A.g.sharded) {
+    const u32 c = read_class(A.g, x);
+    rc.list_remote += c == 2u ? 1u : 0u;
+    rc.list_cached += c == 1u ? 1u : 0u;
+  }
+  if (A.access && lane == 0) atomicAdd(&A.access[x], 1u);
+}
+
+__device__ __forceinline__ void write_read_counts(u32* qs, const ReadCount& rc) {
+  qs[8] = rc.vec_remote;
+  qs[9] = rc.list_remote;
+  qs[10] = rc.vec_cached;
+  qs[11] = rc.list_cached;
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Wave-wide minimum on DPP: row_shr 1/2/4/8 inside each 16-lane row, then row_bcast15 / row_bcast31 — six VALU
+// steps instead of a ds_bpermute butterfly.  Lanes that hold nothing must pass +inf; NaN never wins.
+// ------------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_min(float v) {
+  int x = __float_as_int(v);
+#define SHINE_DPP_MIN(CTRL, RM)                                                                        \
+  x = __float_as_int(fminf(__int_as_float(x),                                                          \
+                           __int_as_float(__builtin_amdgcn_update_dpp(0x7F800000, x, CTRL, RM, 0xF, false))));
+  SHINE_DPP_MIN(0x111, 0xF)
+  SHINE_DPP_MIN(0x112, 0xF)
+  SHINE_DPP_MIN(0x114, 0xF)
+  SHINE_DPP_MIN(0x118, 0xF)
+  SHINE_DPP_MIN(0x142, 0xA)
+  SHINE_DPP_MIN(0x143, 0xC)
+#undef SHINE_DPP_MIN
+  return __int_as_float(__builtin_amdgcn_readlane(x, 63));
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Entry point + greedy descent, shared by both search kernels: HNSW::knn's EP read and distance
+// (hnsw.hh:256-272) and search_for_one over levels ep_level..1 (hnsw.hh:331-393).  Counters: distcomps,
+// visited_nodes (upper / L0 for the EP), visited_neighborlists (upper).  status = ST_FORMAT on a broken index.
+// ------------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ u32 sortable(float f) {  // order-preserving u32 image of a float (total order)
+  const u32 b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+template <int D, int METRIC, typename E, bool ACCT>
+__device__ __forceinline__ void entry_and_descent(const SearchArgs& A, const E* __restrict__ vec,
+                                                  const QueryRegs<D>& Q, u32* sc_ids, float* sc_d, int lane,
+                                                  u32& nn, float& closest, u32& st_dist, u32& st_vup, u32& st_vl0,
+                                                  u32& st_lup, u32& status, ReadCount& rc) {
+  const u32 ep = A.g.ep;
+  if (lane == 0) sc_ids[0] = ep;
+  count_vec_reads<ACCT>(A, rc, lane == 0, ep);
+  wave_sync();
+  dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, 1, lane);
+  wave_sync();
+  closest = sc_d[0];
+  ++st_dist;
+  if (A.g.ep_level > 0) ++st_vup; else ++st_vl0;
+  nn = ep;
+  const u32 MU = A.g.MU;
+  for (u32 level = A.g.ep_level; level > 0 && status == 0; --level) {
+    bool changed;
+    do {
+      changed = false;
+      const u32 ub = A.g.up_base[nn];
+      if (ub == INV) { status = ST_FORMAT; break; }
+      const u32* row = A.g.adjU + (static_cast<u64>(ub) + level - 1) * MU;
+      u32 e = INV;
+      if (static_cast<u32>(lane) < MU) e = row[lane];
+      const bool valid = e != INV;
+      const int cnt = __popcll(__ballot(valid));
+      ++st_lup;
+      st_vup += cnt;
+      st_dist += cnt;
+      if (valid) sc_ids[lane] = e;
+      count_vec_reads<ACCT>(A, rc, valid, e);  // upper-level lists are replicated: only the vectors can be remote
+      wave_sync();
+      dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, cnt, lane);
+      wave_sync();
+      // first neighbour (list order) attaining the minimum; adopted only if strictly closer (:378)
+      float bd = (lane < cnt) ? sc_d[lane] : __builtin_inff();
+      if (bd != bd) bd = __builtin_inff();  // NaN never compares less
+      const float mn = wave_min(bd);
+      if (mn < closest) {
+        const int bi = static_cast<int>(__builtin_ctzll(__ballot(bd == mn)));
+        closest = mn;
+        nn = sc_ids[bi];
+        changed = true;
+      }
+      wave_sync();
+    } while (changed);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// search kernel: one wavefront (= one workgroup) per persistent slot
+//   VIS   0: visited table in LDS, 1: visited bitmap in HBM
+// ------------------------------------------------------------------------------------------------------------
+// Phase stamps for the diagnostic (PROF) build: s_memtime with its lgkmcnt wait in one statement.
+__device__ __forceinline__ u64 stamp() {
+  u64 t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+template <bool PROF>
+struct PhaseClock {  // empty unless PROF
+  __device__ void start() {}
+  __device__ void mark(int) {}
+  __device__ void event(int) {}
+  __device__ void flush(unsigned long long*, int) {}
+};
+template <>
+struct PhaseClock<true> {  // lane i accumulates phase i: one compare and one 64-bit add per mark
+  u64 acc = 0;
+  u32 cnt = 0;
+  u64 t_last = 0;
+  int cur = 0;
+  __device__ void start() { t_last = stamp(); }
+  __device__ void mark(int i) {
+    __builtin_amdgcn_sched_barrier(0);
+    const u64 t = stamp();
+    __builtin_amdgcn_sched_barrier(0);
+    const int lane = static_cast<int>(threadIdx.x);
+    if (lane == cur) acc += t - t_last;
+    if (lane == i) ++cnt;
+    t_last = t;
+    cur = i;
+  }
+  __device__ void event(int i) {  // counts only (slots no phase uses)
+    if (static_cast<int>(threadIdx.x) == i) ++cnt;
+  }
+  __device__ void flush(unsigned long long* out, int lane) {
+    mark(0);
+    if (out && lane < 12) {
+      atomicAdd(&out[lane], static_cast<unsigned long long>(acc));
+      atomicAdd(&out[12 + lane], static_cast<unsigned long long>(cnt));
+    }
+  }
+};
+#define PHASE(i) clk.mark(i);
+#define EVENT(i) clk.event(i);
+
+//   VIS   0: visited table in LDS; 1: visited bitmap in HBM; 2: visited bitmap and both heaps in HBM (the last
+//         fallback pass: no capacity limit but the heap stride, ~µs per heap operation).  Heaps in HBM are
+//         written by some lanes and read by others: a workgroup-scope fence orders every heap operation.
+template <int D, int METRIC, typename E, int VIS, bool ACCT, bool PROF = false>
+__global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
+  PhaseClock<PROF> clk;
+  clk.start();
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int ef = static_cast<int>(A.ef), cap = static_cast<int>(A.cap);
+  const size_t top_b = align16(8ull * ef), next_b = align16(8ull * cap);
+  u64* const gheap = VIS == 2 ? reinterpret_cast<u64*>(A.heaps) + static_cast<u64>(blockIdx.x) * A.heap_stride
+                              : nullptr;
+  u64* top = VIS == 2 ? gheap : reinterpret_cast<u64*>(smem);                   // MaxHeap top_candidates
+  u64* nxt = VIS == 2 ? gheap + top_b / 8 : reinterpret_cast<u64*>(smem + top_b);  // MinHeap next_candidates
+  u32* vtab = reinterpret_cast<u32*>(VIS == 2 ? smem : smem + top_b + next_b);  // visited table (VIS = 0)
+  u32* sc_ids = vtab + (VIS == 0 ? A.vis_cap : 0u);            // fresh neighbours
+  float* sc_d = reinterpret_cast<float*>(sc_ids + 64);
+  auto hfence = []() {
+    if constexpr (VIS == 2) __threadfence_block();
+  };
+
+  const int lane = threadIdx.x;
+  const E* __restrict__ vec = static_cast<const E*>(A.g.vec);
+  const u32 M0 = A.g.M0;
+  const u32 vmask = A.vis_cap - 1, vshift = 32 - (31 - __clz(static_cast<int>(A.vis_cap > 1 ? A.vis_cap : 2)));
+  u32* __restrict__ vis = A.visited + (VIS >= 1 ? static_cast<u64>(blockIdx.x) * A.words_per_slot : 0ull);
+  u32* __restrict__ vlog = A.vlog + (VIS >= 1 ? static_cast<u64>(blockIdx.x) * A.log_cap : 0ull);
+  const u64 below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));  // lanes < this one
+
+  const u32 n_items = A.in_count ? *A.in_count : A.nq;
+  for (;;) {
+    u32 item = 0;
+    if (lane == 0) item = atomicAdd(A.counter, 1u);
+    item = bcast(item);
+    if (item >= n_items) break;
+    const u32 qi = A.in_list ? A.in_list[item] : item;
+
+    PHASE(0)
+    QueryRegs<D> Q;
+    load_query<D>(A.queries + static_cast<u64>(qi) * D, lane, Q);
+    if (VIS == 0) {  // visited_nodes.clear()  (:475) — done up front for this query
+      uint4* t4 = reinterpret_cast<uint4*>(vtab);
+      for (u32 i = lane; i < A.vis_cap / 4; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
+    }
+
+    u32 st_dist = 0, st_vup = 0, st_vl0 = 0, st_lup = 0, st_ll0 = 0, st_maxnext = 0, status = 0;
+    ReadCount rc;
+
+    // ---- entry point + greedy descent (hnsw.hh:256-287) ---------------------------------------------------
+    PHASE(1)
+    u32 nn;
+    float closest;
+    entry_and_descent<D, METRIC, E, ACCT>(A, vec, Q, sc_ids, sc_d, lane, nn, closest, st_dist, st_vup, st_vl0, st_lup, status,
+                                    rc);
+
+    // ---- top_candidates.push({nn, dist(q, nn)}) (hnsw.hh:285-286) ---------------------------------------
+    ++st_dist;
+    int ntop = 1, nnext = 1;
+    u32 logpos = 0, nvis = 1;
+    bool log_overflow = false;
+    if (status == 0) {
+      u64 troot = mk(closest, nn), nroot = troot;  // roots of top / next, kept in SGPRs
+      bool nan_keys = closest != closest;            // a NaN key in either heap: general pop from now on
+      if (lane == 0) {
+        top[0] = troot;
+        nxt[0] = troot;  // search_level :412-415
+        if (VIS == 0) {
+          vtab[vhash(nn, vshift)] = nn;  // table is empty: the first probe slot is free
+        } else {
+          atomicOr(&vis[nn >> 5], 1u << (nn & 31));
+          vlog[0] = nn;
+        }
+      }
+      logpos = 1;
+      st_maxnext = 1;
+      hfence();
+      wave_sync();
+
+      u32 pre_id = INV;  // candidate whose adjacency row is in flight in pre_e
+      u32 pre_e = INV;
+
+      // ---- search_level(q, ef, 0) (hnsw.hh:406-476) ---------------------------------------------------------
+      while (nnext > 0) {
+        PHASE(2)
+        const float ck = key(nroot), farthest0 = key(troot);  // next_candidates.top(); pop()  (:418-421)
+        const u32 cid = eid(nroot);
+        nroot = nan_keys ? heap_pop_any<false>(nxt, nnext, lane) : heap_pop<false>(nxt, nnext, lane);
+        hfence();
+        --nnext;
+        if (ck > farthest0) break;  // :421-426
+
+        // neighbour list of the candidate at level 0 (:436-438)
+        PHASE(3)
+        ++st_ll0;
+        count_list_read<ACCT>(A, rc, cid, lane);
+        u32 e = INV;
+        if (cid == pre_id) {
+          e = pre_e;
+        } else if (static_cast<u32>(lane) < M0) {
+          e = A.g.adj0[static_cast<u64>(cid) * M0 + lane];
+        }
+        bool cand = e != INV;
+        if (!A.g.lists_unique) {  // first occurrence in list order wins (visited.insert order, :443)
+          for (u32 j = 0; j < M0; ++j) {
+            const u32 ej = __shfl(e, static_cast<int>(j));
+            if (j < static_cast<u32>(lane) && ej == e) cand = false;
+          }
+        }
+        bool fresh = false;
+        if (cand) {  // visited.contains / insert (:441-443)
+          if (VIS == 0) {
+            u32 h = vhash(e, vshift);
+            for (;;) {
+              const u32 old = atomicCAS(&vtab[h], INV, e);
+              if (old == INV) { fresh = true; break; }
+              if (old == e) break;
+              h = (h + 1) & vmask;
+            }
+          } else {
+            const u32 bit = 1u << (e & 31);
+            fresh = (atomicOr(&vis[e >> 5], bit) & bit) == 0;
+          }
+        }
+        const u64 fm = __ballot(fresh);
+        const int nf = __popcll(fm);
+        count_vec_reads<ACCT>(A, rc, fresh, e);
+        if (fresh) {
+          const int r = __popcll(fm & below);
+          sc_ids[r] = e;
+          if (VIS >= 1) {
+            const u32 lp = logpos + r;
+            if (lp < A.log_cap) vlog[lp] = e;
+          }
+        }
+        logpos += nf;
+        nvis += nf;
+        if (VIS >= 1 && logpos > A.log_cap) log_overflow = true;
+        st_vl0 += nf;
+        st_dist += nf;
+        if (VIS == 0 && nvis > A.vis_limit) { status = ST_OVERFLOW; break; }
+        if (nf == 0) continue;
+        PHASE(4)
+        wave_sync();
+        dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, nf, lane);
+        wave_sync();
+        PHASE(5)
+        // lane j < nf holds fresh neighbour j (list order)
+        const float my_d = lane < nf ? sc_d[lane] : __builtin_inff();
+        const u32 my_id = lane < nf ? sc_ids[lane] : INV;
+        if (__ballot(my_d != my_d)) nan_keys = true;
+
+        // Speculative prefetch of the adjacency row of the candidate expected on top of next_candidates once
+        // this step's pushes are done: a min-heap root changes only for a strictly smaller key, so the root
+        // survives ties and, among the fresh keys, the first minimum in list order wins.
+        {
+          const float pd_l = (lane < nf && (my_d < farthest0 || ntop < ef) && my_d == my_d) ? my_d : __builtin_inff();
+          const float pd = wave_min(pd_l);
+          u32 pid = INV;
+          if (nnext > 0 && !(pd < key(nroot))) {
+            pid = eid(nroot);
+          } else if (pd < __builtin_inff()) {
+            const u64 hit = __ballot(pd_l == pd);
+            pid = __builtin_amdgcn_readlane(static_cast<int>(my_id), static_cast<int>(__builtin_ctzll(hit)));
+          }
+          pre_id = pid;
+          if (pid != INV && static_cast<u32>(lane) < M0) pre_e = A.g.adj0[static_cast<u64>(pid) * M0 + lane];
+        }
+
+        // accept / push / push_k in list order (:456-465)
+        PHASE(6)
+        for (int j = 0; j < nf; ++j) {
+          const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_d), j));
+          if (d < key(troot) || ntop < ef) {
+            if (nnext >= cap) { status = ST_OVERFLOW; break; }
+            const u32 id = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(my_id), j));
+            const u64 en = mk(d, id);
+            PHASE(8)
+            nroot = heap_push<false>(nxt, nnext, en, nroot, lane);
+            hfence();
+            if (ntop < ef) {  // heap.hh:34-41 push_k
+              PHASE(10)
+              troot = heap_push<true>(top, ntop, en, troot, lane);
+              hfence();
+              ++ntop;
+            } else {  // d < top().distance holds: it is the accept test with the top full
+              PHASE(9)
+              troot = nan_keys ? heap_pop_any<true>(top, ntop, lane) : heap_pop<true>(top, ntop, lane);
+              hfence();
+              PHASE(10)
+              troot = heap_push<true>(top, ntop - 1, en, troot, lane);
+              hfence();
+            }
+            PHASE(6)
+            ++nnext;
+            if (static_cast<u32>(nnext) > st_maxnext) st_maxnext = nnext;
+          }
+        }
+        if (status != 0) break;
+      }
+
+      // ---- trim to k and emit in heap-array order (:296-303) ------------------------------------------------
+      PHASE(7)
+      if (status == 0) {
+        PHASE(11)
+        while (ntop > static_cast<int>(A.k)) {
+          if (nan_keys) heap_pop_any<true>(top, ntop, lane);
+          else heap_pop<true>(top, ntop, lane);
+          hfence();
+          --ntop;
+        }
+      }
+    }
+
+    const u64 obase = static_cast<u64>(qi) * A.k;
+    for (u32 i = lane; i < A.k; i += 64) {
+      u32 id = INV;
+      float d = 0.f;
+      u32 slot = i;
+      if (status == 0 && static_cast<int>(i) < ntop) {
+        const u64 en = top[i];
+        id = A.g.uid[eid(en)];
+        d = key(en);
+        if (A.sort_out) {  // fast-mode fixup pass: ascending order (ties by heap position)
+          const u32 si = sortable(d);
+          slot = 0;
+          for (int j = 0; j < ntop; ++j) {
+            const u32 sj = sortable(key(top[j]));
+            slot += (sj < si || (sj == si && static_cast<u32>(j) < i)) ? 1u : 0u;
+          }
+        }
+      }
+      A.out_ids[obase + slot] = id;
+      if (A.out_dists) A.out_dists[obase + slot] = d;
+    }
+    if (status == ST_OVERFLOW && A.out_list && lane == 0) A.out_list[atomicAdd(A.out_count, 1u)] = qi;
+    if (A.qstats && lane == 0) {
+      u32* qs = A.qstats + static_cast<u64>(qi) * kQsWords;
+      qs[0] = st_dist;
+      qs[1] = st_vup;
+      qs[2] = st_vl0;
+      qs[3] = st_lup;
+      qs[4] = st_ll0;
+      qs[5] = A.sort_out ? 0u : st_maxnext;  // fast-mode fixup: exact, so no tie can have changed the set
+      qs[6] = status;
+      qs[7] = status == 0 ? static_cast<u32>(ntop < static_cast<int>(A.k) ? ntop : A.k) : 0u;
+      write_read_counts(qs, rc);
+    }
+
+    if (VIS >= 1) {  // visited_nodes.clear() (:475): clear exactly the words this query touched
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!log_overflow) {
+        for (u32 i = lane; i < logpos; i += 64) {
+          const u32 id = __hip_atomic_load(&vlog[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          vis[id >> 5] = 0u;
+        }
+      } else {
+        for (u64 w = lane; w < A.words_per_slot; w += 64) vis[w] = 0u;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  clk.flush(A.prof, lane);
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Fast search kernel (SHINE_MODE_FAST).  The same traversal with a different candidate structure: one sorted
+// list of the best ef candidates (key, id, expanded bit) held in VGPRs — position p in lane p % 64 of register
+// p / 64 — instead of the two std::vector heaps.
+//
+// Equivalence: every entry pushed onto next_candidates is also pushed onto top_candidates (hnsw.hh:461-465), and
+// with pairwise distinct distances an entry evicted from top has a key above every later farthest distance, so
+// it is never expanded.  next_candidates' minimum is therefore the smallest unexpanded top entry, and the loop
+// ends when none is left (the break at :424).  One expansion's accept / push / push_k sequence leaves top equal to
+// the ef smallest of (top ∪ fresh).  Hence, when no two keys compare equal where the reference's tie-breaking
+// could decide, this kernel expands the same nodes in the same order and returns the same ids, distances and
+// counters.  The events where heap layout decides are counted in qstats word 5 (0 = identical result):
+//   * a key inserted equal to an unexpanded one (which of the two next_candidates yields first),
+//   * an eviction whose farthest entry had an equal twin (which one push_k pops, heap.hh:34-41),
+//   * equal keys at positions k-1 and k at the end (which one the trim to k pops, hnsw.hh:296-299),
+//   * NaN keys.
+// A key equal to the farthest with the list full is rejected by both (:461 is strict).  Results are written
+// in ascending distance order.  Costs: an insertion is two ballots per register plus one DPP wave_shr per
+// register (no LDS), the next candidate is one ballot per register.
+// ------------------------------------------------------------------------------------------------------------
+constexpr u32 EXPANDED = 0x80000000u;  // id bit: this candidate has been expanded (ids < 2^31)
+
+// ------------------------------------------------------------------------------------------------------------
+// Pipelining.  The neighbour-vector loads of the NEXT expansion are issued before the current one's merge: once
+// the distances of expansion t are known, the next candidate is already determined — the smaller of the runner-up
+// unexpanded entry r (whose list was prefetched one expansion earlier) and the best accepted fresh key f* (merged
+// order puts fresh keys first among equals, later list positions first).  For r the vectors are requested at once;
+// for f* its list is loaded first.  Either way they land while the merge and the pick run.  A misprediction (only
+// possible through ties or NaN keys) re-issues the loads for the picked candidate.  The one neighbour buffer is
+// refilled as soon as the current distances have consumed it, and every list / vector load on the common path is
+// unconditional, so every wait is an exact vmcnt that never covers the younger prefetches.
+// ------------------------------------------------------------------------------------------------------------
+template <int D, typename E, int P>
+__device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restrict__ vec, u32 e, u32 pad, int g4,
+                                           int c4) {
+  u32 sid[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) sid[p] = static_cast<u32>(__shfl(static_cast<int>(e), 16 * p + g4));
+#pragma unroll
+  for (int p = 0; p < P; ++p) issue_pass_u<D, E, P>(B, p, vec, sid[p], pad, c4);
+}
+
+template <int D, int METRIC, typename E, int R, int P, bool ACCT, bool PROF = false>
+__global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
+  PhaseClock<PROF> clk;
+  clk.start();
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  u32* vtab = reinterpret_cast<u32*>(smem);  // visited table
+  u32* sc_ids = vtab + A.vis_cap;             // greedy-descent scratch
+  float* sc_d = reinterpret_cast<float*>(sc_ids + 64);
+  u64* mrg = reinterpret_cast<u64*>(sc_d + 64);  // merge scratch: (key, id) at merged positions 0 .. ef
+  const int lane = threadIdx.x, g4 = lane >> 2, c4 = lane & 3;
+  const E* __restrict__ vec = static_cast<const E*>(A.g.vec);
+  const u32* __restrict__ adj0 = A.g.adj0;
+  const u32 M0 = A.g.M0, pad = A.g.pad_node;
+  const int ef = static_cast<int>(A.ef);
+  const u32 vmask = A.vis_cap - 1, vshift = 32 - (31 - __clz(static_cast<int>(A.vis_cap)));
+  const float INF = __builtin_inff();
+  const bool in_row = static_cast<u32>(lane) < M0;
+  const u32 row_lane = in_row ? static_cast<u32>(lane) : 0u;
+  // Unconditional, and never masked right after the load (that would wait for it): lanes beyond M0 hold a copy of
+  // entry 0 and are excluded where the list is used (the visited test; slots >= M0 are never fresh).
+  auto load_row = [&](u32 node) -> u32 { return adj0[static_cast<u64>(node) * M0 + row_lane]; };
+
+  const u32 n_items = A.in_count ? *A.in_count : A.nq;
+  for (;;) {
+    u32 item = 0;
+    if (lane == 0) item = atomicAdd(A.counter, 1u);
+    item = bcast(item);
+    if (item >= n_items) break;
+    const u32 qi = A.in_list ? A.in_list[item] : item;
+
+    PHASE(0)
+    QueryRegs<D> Q;
+    load_query<D>(A.queries + static_cast<u64>(qi) * D, lane, Q);
+    {
+      uint4* t4 = reinterpret_cast<uint4*>(vtab);
+      for (u32 i = lane; i < A.vis_cap / 4; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
+    }
+    u32 st_dist = 0, st_vup = 0, st_vl0 = 0, st_lup = 0, st_ll0 = 0, ties = 0, status = 0;
+    ReadCount rc;
+    PHASE(1)
+    u32 nn;
+    float closest;
+    entry_and_descent<D, METRIC, E, ACCT>(A, vec, Q, sc_ids, sc_d, lane, nn, closest, st_dist, st_vup, st_vl0, st_lup, status,
+                                    rc);
+    ++st_dist;  // top_candidates.push({nn, dist(q, nn)}) (hnsw.hh:285-286)
+
+    float ck[R];  // candidate keys, ascending; +inf beyond the size
+    u32 ci[R];    // candidate ids | EXPANDED; INV beyond the size
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      ck[r] = INF;
+      ci[r] = INV;
+    }
+    int cs = 0;
+    float cmax = INF;  // key at position ef - 1 once the list is full
+    u32 nvis = 1;
+    if (status == 0) {
+      ck[0] = lane == 0 ? closest : INF;
+      ci[0] = lane == 0 ? (nn | EXPANDED) : INV;  // popped right away (:418)
+      cs = 1;
+      if (closest != closest) ++ties;
+      if (lane == 0) vtab[vhash(nn, vshift)] = nn;
+      wave_sync();
+    }
+
+    // pipeline state: the candidate's list `e` and its vectors in X (in flight); the runner-up r and its
+    // prefetched list.  X is refilled for the next candidate as soon as the current distances have consumed it.
+    NbrBuf<D, E, P> X;
+    u32 e = load_row(status == 0 ? nn : pad);
+    issue_list<D, E, P>(X, vec, e, pad, g4, c4);
+    u32 r_id = INV;
+    float r_key = INF;
+    u32 nid = nn;
+    u32 nrow = load_row(nn);
+    u32 cur = nn;  // the candidate whose list `e` is
+
+    while (status == 0) {
+      ++st_ll0;  // read_neighborlist (:436-438)
+      count_list_read<ACCT>(A, rc, cur, lane);
+      PHASE(8)
+      bool cand = in_row && e != INV;
+      if (!A.g.lists_unique) {  // first occurrence in list order wins (visited.insert order, :443)
+        for (u32 j = 0; j < M0; ++j) {
+          const u32 ej = __shfl(e, static_cast<int>(j));
+          if (j < static_cast<u32>(lane) && ej == e) cand = false;
+        }
+      }
+      bool fresh = false;
+      if (cand) {  // visited.contains / insert (:441-443)
+        u32 h = vhash(e, vshift);
+        for (;;) {
+          const u32 old = atomicCAS(&vtab[h], INV, e);
+          if (old == INV) { fresh = true; break; }
+          if (old == e) break;
+          h = (h + 1) & vmask;
+        }
+      }
+      const u64 fm = __ballot(fresh);
+      const int nf = __popcll(fm);
+      count_vec_reads<ACCT>(A, rc, fresh, e);
+      nvis += nf;
+      st_vl0 += nf;
+      st_dist += nf;
+      if (nvis > A.vis_limit) {
+        status = ST_OVERFLOW;
+        break;
+      }
+
+      PHASE(5)
+      float my_d = INF;  // lane j: distance of list slot j
+      u64 acc = 0;
+      if (nf > 0) {
+        float out[P];
+        pass_dists<D, METRIC, E, P>(Q, X, out);
+        const int src = ((lane & 15) << 2) + 3;
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+          const float v = __shfl(out[p], src);
+          if ((lane >> 4) == p) my_d = v;
+        }
+        if (!fresh) my_d = INF;
+        if (fresh && my_d != my_d) {  // NaN: the reference's comparisons are all false; no ordered slot exists here
+          my_d = INF;
+          ++ties;
+        }
+        acc = __ballot(fresh && (cs < ef || my_d < cmax));  // fresh keys that can enter (:461)
+      }
+
+      // ---- the next candidate, known before the merge ----------------------------------------------------------
+      // the smaller of f* (best accepted fresh key; among equals the last list position, as merged) and the
+      // runner-up r; its vectors are requested here, one issue point for every path, into the buffer the
+      // distances above have just consumed
+      PHASE(4)
+      u32 pid = r_id;
+      if (acc) {
+        const float fstar = wave_min(((acc >> lane) & 1ull) ? my_d : INF);
+        const u64 hit = acc & __ballot(my_d == fstar);
+        if (r_id == INV || fstar <= r_key)
+          pid = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(e), 63 - static_cast<int>(__clzll(hit))));
+      }
+      if (pid == r_id) EVENT(9) else EVENT(10)
+      const u32 prow = pid == r_id ? nrow : load_row(pid != INV ? pid : pad);  // a fresh f*: its list now
+      // an entry already at its home slot of the visited table is not fresh: its row is not requested (one
+      // read-only LDS probe; the visit proper still runs at the top of the next expansion)
+      const bool seen = in_row && prow != INV && vtab[vhash(prow, vshift)] == prow;
+      issue_list<D, E, P>(X, vec, seen ? INV : prow, pad, g4, c4);
+
+      // ---- merge (:456-465 over the whole list at once) ----------------------------------------------------------
+      PHASE(6)
+      if (acc) {
+        int shift[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) shift[r] = 0;
+        int frank = 0;  // fresh lane: accepted keys ordered before it
+        int fbase = 0;  // fresh lane: list entries below it
+        u64 todo = acc;
+        while (todo) {
+          const int i = static_cast<int>(__builtin_ctzll(todo));
+          todo &= todo - 1;
+          const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_d), i));
+          int below = 0;
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            shift[r] += d <= ck[r] ? 1 : 0;
+            below += __popcll(__ballot(ck[r] < d));
+          }
+          frank += (d < my_d || (d == my_d && i > lane)) ? 1 : 0;
+          fbase = lane == i ? below : fbase;
+        }
+        const int total = cs + __popcll(acc);
+        const int hi = total < ef + 1 ? total : ef + 1;  // merged positions written: 0 .. hi-1
+        const int sink = ef + 1;  // entries that fall past the cut are written to a scratch slot (no branches)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int p = 64 * r + lane;
+          const int np = p + shift[r];
+          mrg[(p < cs && np <= ef) ? np : sink] = (static_cast<u64>(ci[r]) << 32) | __float_as_uint(ck[r]);
+        }
+        {
+          const int np = fbase + frank;
+          mrg[(((acc >> lane) & 1ull) && np <= ef) ? np : sink] = (static_cast<u64>(e) << 32) | __float_as_uint(my_d);
+        }
+        wave_sync();
+        cs = total < ef ? total : ef;
+        bool tie = false;
+        const u64 none = (static_cast<u64>(INV) << 32) | __float_as_uint(INF);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int p = 64 * r + lane;
+          const int pc = p < ef ? p : ef;  // positions p, p + 1 in one ds_read2 (p + 1 <= sink)
+          const u64 m0r = mrg[pc], m1r = mrg[pc + 1];
+          tie |= p + 1 < hi && key(m0r) == key(m1r) &&
+                 ((eid(m0r) & EXPANDED) == 0 || (eid(m1r) & EXPANDED) == 0 || p + 1 == ef);
+          const u64 m0 = p < cs ? m0r : none;
+          ck[r] = key(m0);
+          ci[r] = eid(m0);
+        }
+        if (__ballot(tie)) ++ties;
+        wave_sync();
+        if (cs == ef) {
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            if (((ef - 1) >> 6) == r) cmax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ck[r]), (ef - 1) & 63));
+        }
+      }
+
+      // ---- next_candidates.top(); pop() (:418-426) and the new runner-up -----------------------------------
+      PHASE(2)
+      u64 um[R];  // unexpanded entries (INV carries the EXPANDED bit)
+#pragma unroll
+      for (int r = 0; r < R; ++r) um[r] = __ballot(static_cast<int>(ci[r]) >= 0);
+      int p1 = -1;
+#pragma unroll
+      for (int r = R - 1; r >= 0; --r) p1 = um[r] ? 64 * r + static_cast<int>(__builtin_ctzll(um[r])) : p1;
+      if (p1 < 0) break;  // every candidate within the radius expanded: the break at :424
+      const int r1 = p1 >> 6, l1 = p1 & 63;
+      u32 c = 0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const u32 cr = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(ci[r]), l1));
+        c = r == r1 ? cr : c;
+        ci[r] = (r == r1 && lane == l1) ? (ci[r] | EXPANDED) : ci[r];
+        um[r] = r == r1 ? (um[r] & (um[r] - 1)) : um[r];
+      }
+      int p2 = -1;
+#pragma unroll
+      for (int r = R - 1; r >= 0; --r) p2 = um[r] ? 64 * r + static_cast<int>(__builtin_ctzll(um[r])) : p2;
+      u32 c2 = INV;
+      float k2 = INF;
+      {
+        const int r2 = p2 >> 6, l2 = p2 & 63;  // p2 = -1: r2 = -1 matches no register
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const u32 cr = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(ci[r]), l2 & 63));
+          const float kr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ck[r]), l2 & 63));
+          c2 = r == r2 ? cr : c2;
+          k2 = r == r2 ? kr : k2;
+        }
+      }
+      u32 erow = prow;
+      if (c != pid) {  // mispredicted (ties / NaN keys): fetch the picked candidate's list and vectors
+        EVENT(11)
+        erow = c == nid ? nrow : load_row(c);
+        issue_list<D, E, P>(X, vec, erow, pad, g4, c4);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this rare path leaves nothing in flight behind the prefetch
+      }
+      nid = c2 != INV ? c2 : c;
+      nrow = load_row(nid);  // unconditional: always the youngest load
+      e = erow;
+      cur = c;
+      r_id = c2;
+      r_key = k2;
+    }
+
+    PHASE(7)
+    // top-k in ascending order; an equal pair straddling position k is decided by heap layout in the reference
+    if (status == 0 && cs > static_cast<int>(A.k)) {
+      const int k = static_cast<int>(A.k);
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (((k - 1) >> 6) == r) a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ck[r]), (k - 1) & 63));
+        if ((k >> 6) == r) b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ck[r]), k & 63));
+      }
+      if (a == b) ++ties;
+    }
+    const u64 obase = static_cast<u64>(qi) * A.k;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const u32 i = static_cast<u32>(64 * r + lane);
+      if (i < A.k) {
+        const bool ok = status == 0 && static_cast<int>(i) < cs;
+        A.out_ids[obase + i] = ok ? A.g.uid[ci[r] & ~EXPANDED] : INV;
+        if (A.out_dists) A.out_dists[obase + i] = ok ? ck[r] : 0.f;
+      }
+    }
+    if (status == ST_OVERFLOW && A.out_list && lane == 0) A.out_list[atomicAdd(A.out_count, 1u)] = qi;
+    if (A.qstats && lane == 0) {
+      u32* qs = A.qstats + static_cast<u64>(qi) * kQsWords;
+      qs[0] = st_dist;
+      qs[1] = st_vup;
+      qs[2] = st_vl0;
+      qs[3] = st_lup;
+      qs[4] = st_ll0;
+      qs[5] = ties;
+      qs[6] = status;
+      qs[7] = status == 0 ? static_cast<u32>(cs < static_cast<int>(A.k) ? cs : A.k) : 0u;
+      write_read_counts(qs, rc);
+    }
+  }
+  clk.flush(A.prof, lane);
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// batched distance kernel: one wavefront per (query, 64-node chunk)
+// ------------------------------------------------------------------------------------------------------------
+template <int D, int METRIC, typename E>
+__global__ __launch_bounds__(64) void distance_kernel(DistArgs A) {
+  __shared__ u32 sc_ids[64];
+  __shared__ float sc_d[64];
+  const int lane = threadIdx.x;
+  const u32 chunks = (A.n_per + 63) / 64;
+  const u64 w = blockIdx.x;
+  const u32 qi = static_cast<u32>(w / chunks), ch = static_cast<u32>(w % chunks);
+  if (qi >= A.nq) return;
+  QueryRegs<D> Q;
+  load_query<D>(A.queries + static_cast<u64>(qi) * D, lane, Q);
+  const u32 j = ch * 64 + lane;
+  u32 dense = INV;
+  if (j < A.n_per) {
+    const u32 u = A.node_uids[static_cast<u64>(qi) * A.n_per + j];
+    if (u < A.g.inv_size) dense = A.g.inv_uid[u];
+  }
+  const bool ok = dense != INV;
+  const u64 om = __ballot(ok);
+  const int n = __popcll(om);
+  const u64 below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const int r = __popcll(om & below);
+  if (ok) sc_ids[r] = dense;
+  wave_sync();
+  dist_list<D, METRIC, E>(static_cast<const E*>(A.g.vec), Q, sc_ids, sc_d, n, lane);
+  wave_sync();
+  if (j < A.n_per) A.out[static_cast<u64>(qi) * A.n_per + j] = ok ? sc_d[r] : __builtin_nanf("");
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// heap replay (diagnostics): op 0 = push, 1 = pop, 2 = push_k(k)
+// ------------------------------------------------------------------------------------------------------------
+template <bool MAXH>
+__global__ __launch_bounds__(64) void heap_replay_kernel(const int32_t* ops, const float* vals, const uint32_t* ids,
+                                                         uint32_t n_ops, uint32_t k, float* out_d, uint32_t* out_ids,
+                                                         uint32_t* out_n) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  u64* h = reinterpret_cast<u64*>(smem);
+  const int lane = threadIdx.x;
+  const bool any = (k & 0x80000000u) != 0;  // exercise the general pop instead of the fast one
+  k &= 0x7FFFFFFFu;
+  int n = 0;
+  u64 root = 0;  // tracked exactly as the search kernel tracks it; checked against h[0] after every op
+  bool root_ok = true;
+  for (u32 i = 0; i < n_ops; ++i) {
+    const u64 e = mk(vals[i], ids[i]);
+    const int op = ops[i];
+    if (op == 0) {
+      root = heap_push<MAXH>(h, n, e, root, lane);
+      ++n;
+    } else if (op == 1) {
+      if (n > 0) {
+        root = any ? heap_pop_any<MAXH>(h, n, lane) : heap_pop<MAXH>(h, n, lane);
+        --n;
+      }
+    } else {
+      if (n < static_cast<int>(k)) {
+        root = heap_push<MAXH>(h, n, e, root, lane);
+        ++n;
+      } else if (hcmp<MAXH>(vals[i], key(root))) {
+        root = any ? heap_pop_any<MAXH>(h, n, lane) : heap_pop<MAXH>(h, n, lane);
+        root = heap_push<MAXH>(h, n - 1, e, root, lane);
+      }
+    }
+    if (n > 0 && bcast64(h[0]) != root) root_ok = false;
+  }
+  for (int i = lane; i < n; i += 64) {
+    out_d[i] = key(h[i]);
+    out_ids[i] = eid(h[i]);
+  }
+  if (lane == 0) *out_n = root_ok ? static_cast<u32>(n) : 0xFFFFFFFFu;
+}
+
+template <int D, int METRIC, typename E, bool AC>
+hipError_t launch_search_acct(uint32_t grid, const SearchArgs& a, hipStream_t s) {
+  const size_t lds = search_lds_bytes(a.ef, a.cap, a.vis_cap);
+  auto run = [&](auto kern) -> hipError_t {
+    if (lds > 65536) {  // beyond the default dynamic-LDS limit: opt in (per device, so every launch)
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, s, a);
+    return hipGetLastError();
+  };
+  if (a.fast) {  // sorted-list kernel; the launcher's caller guarantees ef <= kFastMaxEf and a visited table in LDS
+    const size_t lds_f = search_fast_lds_bytes(a.vis_cap, a.ef);
+    auto runf = [&](auto kern) -> hipError_t {
+      if (lds_f > 65536) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_f));
+        if (e != hipSuccess) return e;
+      }
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds_f, s, a);
+      return hipGetLastError();
+    };
+    if (a.vis_cap == 0 || a.ef == 0 || a.ef > kFastMaxEf) return hipErrorInvalidValue;
+    // P = passes of 16 list slots: 2 covers M0 <= 32 (M <= 16), 4 covers M0 <= 64
+    if (a.g.M0 > 64) return hipErrorInvalidValue;
+    const bool wide = a.g.M0 > 32;
+    if constexpr (!AC && D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
+      if (a.prof && !wide && a.ef > 64 && a.ef <= 128) return runf(search_fast_kernel<D, METRIC, E, 2, 2, AC, true>);
+    }
+    if (a.ef <= 64)
+      return wide ? runf(search_fast_kernel<D, METRIC, E, 1, 4, AC>) : runf(search_fast_kernel<D, METRIC, E, 1, 2, AC>);
+    if (a.ef <= 128)
+      return wide ? runf(search_fast_kernel<D, METRIC, E, 2, 4, AC>) : runf(search_fast_kernel<D, METRIC, E, 2, 2, AC>);
+    if (a.ef <= 256)
+      return wide ? runf(search_fast_kernel<D, METRIC, E, 4, 4, AC>) : runf(search_fast_kernel<D, METRIC, E, 4, 2, AC>);
+    return wide ? runf(search_fast_kernel<D, METRIC, E, 8, 4, AC>) : runf(search_fast_kernel<D, METRIC, E, 8, 2, AC>);
+  }
+  if constexpr (!AC && D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
+    if (a.prof && a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0, AC, true>);
+  }
+  if (a.global_heaps) {  // both heaps in HBM: only the scratch ids / distances stay in LDS
+    if (a.vis_cap != 0 || !a.heaps || a.heap_stride < align16(8ull * a.ef) / 8 + a.cap) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((search_kernel<D, METRIC, E, 2, AC>), dim3(grid), dim3(64), 64 * 4 * 2, s, a);
+    return hipGetLastError();
+  }
+  if (a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0, AC>);
+  return run(search_kernel<D, METRIC, E, 1, AC>);
+}
+
+// Read accounting (qstats words 8-11, cache-warmup counters) is compiled in only where it can count something.
+template <int D, int METRIC, typename E>
+hipError_t launch_search_t(uint32_t grid, const SearchArgs& a, hipStream_t s) {
+  if (a.g.sharded || a.access) return launch_search_acct<D, METRIC, E, true>(grid, a, s);
+  return launch_search_acct<D, METRIC, E, false>(grid, a, s);
+}
+
+template <int D, int METRIC, typename E>
+hipError_t launch_distance_t(const DistArgs& a, hipStream_t s) {
+  const u64 chunks = (a.n_per + 63) / 64;
+  const u64 grid = static_cast<u64>(a.nq) * chunks;
+  if (grid == 0) return hipSuccess;
+  if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((distance_kernel<D, METRIC, E>), dim3(static_cast<u32>(grid)), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+}  // namespace shine

@@ -69,6 +69,8 @@ class IndexInfo(C.Structure):
         ("reserved0", C.c_uint32),
         ("id_space", C.c_uint64),
         ("cache_fraction", C.c_double),
+        ("cus", C.c_uint32),
+        ("lds_per_cu", C.c_uint32),
     ]
 
     def as_dict(self) -> dict:
@@ -106,6 +108,7 @@ PROTOTYPES = {
                                     C.c_double, C.POINTER(P)]),
     "shine_knn_batch": (I32, [P, P, P, U32, U32, U32, P, P, P, C.POINTER(Stats)]),
     "shine_release_stream": (I32, [P, P]),
+    "shine_cache_warmup": (I32, [P, P, P, U32, U32, U32]),
     "shine_knn_batch_device": (I32, [P, U32, P, U32, U32, U32, P, P, P, P]),
     "shine_distance_batch_device": (I32, [P, U32, P, U32, P, U32, P, P]),
     "shine_route": (I32, [P, P, U32, P]),

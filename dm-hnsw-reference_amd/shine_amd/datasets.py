@@ -109,21 +109,33 @@ def harmonic_number(n: int, alpha: float) -> float:  # skew.py:14-19
     return float(np.sum(1.0 / np.arange(1, n + 1, dtype=np.float64) ** alpha))
 
 
-def zipf_query_mix(pool: np.ndarray, num_queries: int, alpha: float, split: int = 0, seed: int = 0):
-    """skew.py:114-164: query i of the pool is repeated ceil(num_queries * pmf(i+1)) times (until num_queries
-    are drawn), the multiset is shuffled, and the last `split` become the warm-up set.  Returns
-    (queries, warmup, pool_index_of_each_query)."""
-    n = pool.shape[0]
+def zipf_counts(n: int, num_queries: int, alpha: float) -> tuple[list[int], int]:
+    """skew.py:114-132: occurrences of pool query i (0-based) = ceil(num_queries * pmf(i+1)), drawn until the total
+    reaches num_queries.  Returns (counts, drawn); drawn can exceed num_queries (the ceilings)."""
     h = harmonic_number(n, alpha)
     counts = []
     drawn = 0
     for idx in range(n):
         if drawn >= num_queries:
             break
-        occ = math.ceil(num_queries * ((1.0 / (idx + 1) ** alpha) / h))
+        occ = math.ceil(num_queries * ((1.0 / (idx + 1) ** alpha) / h))  # pmf(k) = (1 / k^alpha) / H (skew.py:22-23)
         counts.append(occ)
         drawn += occ
-    if drawn > num_queries:  # skew.py:141 TODO: trim the last count instead of asserting
+    return counts, drawn
+
+
+def zipf_query_mix(pool: np.ndarray, num_queries: int, alpha: float, split: int = 0, seed: int = 0,
+                   strict: bool = False):
+    """skew.py:114-164: query i of the pool is repeated ceil(num_queries * pmf(i+1)) times (until num_queries
+    are drawn), the multiset is shuffled, and the last `split` become the warm-up set.  Returns
+    (queries, warmup, pool_index_of_each_query).  The reference asserts drawn == num_queries (skew.py:135); with
+    strict=True so does this (ValueError), otherwise the overshoot is trimmed from the last count, the fix the
+    reference's TODO names (skew.py:136)."""
+    n = pool.shape[0]
+    counts, drawn = zipf_counts(n, num_queries, alpha)
+    if drawn != num_queries:
+        if strict:
+            raise ValueError(f"drawn {drawn} != num_queries {num_queries} (skew.py:135)")
         counts[-1] -= drawn - num_queries
     src = np.repeat(np.arange(len(counts)), counts)
     perm = np.random.default_rng(seed).permutation(num_queries)

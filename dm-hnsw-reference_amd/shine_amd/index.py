@@ -131,6 +131,12 @@ class Index:
                                         C.byref(st)))
         return KnnResult(ids, dists, qs, st.as_dict())
 
+    def cache_warmup(self, queries: np.ndarray, k: int, ef: int, query_ids: np.ndarray | None = None) -> None:
+        """shine_cache_warmup: run the warmup split and re-rank every stripe's cached prefix by its reads."""
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        qid = None if query_ids is None else np.ascontiguousarray(query_ids, dtype=np.uint32)
+        L.check(L.lib().shine_cache_warmup(self._h, _ptr(q), _ptr(qid), q.shape[0], k, ef))
+
     def release_stream(self, stream: int) -> None:
         """shine_release_stream: wait for `stream` and drop the handle's scratch for it."""
         L.check(L.lib().shine_release_stream(self._h, C.c_void_p(stream)))

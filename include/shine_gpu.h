@@ -86,6 +86,8 @@ typedef struct shine_index_info {
   uint32_t reserved0;
   uint64_t id_space;       /* device node-id range: num_nodes (replica) or n_gpus x ids_per_gpu (sharded) */
   double cache_fraction;   /* sharded: share of every other GPU's records held in local HBM copies */
+  uint32_t cus;            /* compute units of GPU slot 0 (hipDeviceProp_t), used to size the launches */
+  uint32_t lds_per_cu;     /* LDS bytes per CU of GPU slot 0 */
 } shine_index_info;
 
 /* Placement of the records over the GPUs of a handle.
@@ -156,6 +158,15 @@ int shine_knn_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_qu
 
 /* Wait for the work enqueued on `stream` and free the handle's scratch for it (every GPU slot). */
 int shine_release_stream(shine_index_t h, void* stream);
+
+/* Cache warmup (the reference's warmup split, compute_node.cc:116-131, feeding cache::Cache admission,
+ * hnsw.hh:447-448): answers the warmup queries like shine_knn_batch while counting every record read, then re-ranks
+ * each stripe — upper-level records first (always admitted, cache.hh:368), then level-0 records by warmup reads,
+ * most first — and re-lays out the sharded arrays so the cached prefix every GPU copies holds the hottest records.
+ * Results of later searches do not change; their cache_hits / cache_misses do.  No-op for a replica, one slot, or a
+ * zero cache fraction.  On failure the handle keeps its previous layout but can no longer be re-ranked. */
+int shine_cache_warmup(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
+                       uint32_t ef);
 
 /* The GPU slot each query of a batch is answered on: id % n_gpus, or for SHINE_PLACE_SHARDED_REGIONS the slot of
  * the query's nearest region that still has room in this batch (QueryRouter::run_routing, query_router.hh:280-387).

@@ -250,3 +250,49 @@ def test_release_stream_then_reuse(four_shards, gpu_available):
             idx.release_stream(s.cuda_stream)  # waits for the stream, then drops its scratch
             np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32), ref_ids)
             del s
+
+
+@pytest.fixture(scope="module")
+def skew_index():
+    """200K DEEP-shaped records in 8 memory-node dumps: two slots of ~100K records, so a 0.15 cache (rounded up to
+    whole 2 MiB page steps of 16,384 rows) holds under a third of each stripe."""
+    base = D.deep_like(200_000, seed=111, d=96)
+    dumps, _ = shine_amd.build(base, 16, 100, 0, 8, seed=7, threads=16)
+    pool = D.deep_like(3000, seed=112, d=96)
+    return dumps, pool
+
+
+def test_cache_warmup_hit_rate_rises_with_skew_and_results_do_not_change(skew_index, gpu_available):
+    """The skew grid of exp_cache_size_and_skew.py on the sharded layout: the warmup split (skew.py's last `split`
+    queries) ranks every stripe's cached prefix by its reads (shine_cache_warmup, the admission of hnsw.hh:447-448);
+    the measured queries then hit the cache more as the Zipf alpha grows, more than with the static ranking, and
+    return exactly what the oracle returns."""
+    dumps, pool = skew_index
+    hit = {}
+    for alpha in (0.0, 1.0, 1.5):
+        q, warm, _ = D.zipf_query_mix(pool, 3000, alpha, split=1000, seed=9)
+        with shine_amd.Index.from_buffers(dumps, 96, 16, 0, gpus=[0, 0], placement="sharded", cache=0.15) as idx:
+            assert 0.2 < idx.info()["cache_fraction"] < 0.5
+            static = idx.knn(q, 10, 128)
+            idx.cache_warmup(warm, 10, 128)
+            warmed = idx.knn(q, 10, 128)
+        np.testing.assert_array_equal(warmed.ids, static.ids)
+        np.testing.assert_array_equal(warmed.qstats[:, :8], static.qstats[:, :8])
+        rate = lambda r: r.stats["cache_hits"] / (r.stats["cache_hits"] + r.stats["cache_misses"])
+        hit[alpha] = (rate(static), rate(warmed))
+        if alpha == 1.0:
+            ref_ids, ref_d, ref_qs = O.OracleIndex(dumps, 96, 16, 0).knn(q, 10, 128, threads=8)
+            np.testing.assert_array_equal(warmed.ids, ref_ids)
+            np.testing.assert_array_equal(warmed.dists.view(np.uint32), ref_d.view(np.uint32))
+    print("cache hit rate (static, warmed) by alpha:", hit)
+    assert hit[0.0][1] < hit[1.0][1] < hit[1.5][1], hit
+    assert hit[1.5][1] > hit[1.5][0] + 0.05, hit  # the warmup ranking beats the static one on a skewed mix
+
+
+def test_cache_warmup_is_a_noop_for_a_replica(four_shards, gpu_available):
+    _, q, dumps = four_shards
+    with shine_amd.Index.from_buffers(dumps, 128, 8, 0, gpus=[0], placement="replica") as idx:
+        before = idx.knn(q, 10, 48)
+        idx.cache_warmup(q[:50], 10, 48)
+        after = idx.knn(q, 10, 48)
+    np.testing.assert_array_equal(before.ids, after.ids)

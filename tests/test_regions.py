@@ -46,3 +46,50 @@ def test_unknown_k_is_rejected(clustered):
     _, dumps = clustered
     with pytest.raises(shine_amd.ShineError):
         shine_amd.plan_regions(dumps, 128, 8, 0, 0)
+
+
+# ---- Zipf query mix (f4: scripts/data/skew.py:80-172) -----------------------------------------------------------
+def _skew_py_counts(n, num_queries, alpha):
+    """skew.py:110-132 line by line: probabilities over the whole pool, then ceil-draws until num_queries."""
+    import math
+    h = sum(1.0 / (k ** alpha) for k in range(1, n + 1))
+    probs = [(1.0 / (k ** alpha)) / h for k in range(1, n + 1)]
+    dist, drawn = [], 0
+    for idx in range(n):
+        if drawn >= num_queries:
+            break
+        occ = math.ceil(num_queries * probs[idx])
+        dist.append(occ)
+        drawn += occ
+    return dist, drawn
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("n,nq,alpha", [(1000, 1000, 0.0), (500, 2000, 0.5), (2000, 3000, 1.0), (300, 5000, 1.5)])
+def test_zipf_counts_follow_skew_py(n, nq, alpha):
+    from shine_amd import datasets as D
+    counts, drawn = D.zipf_counts(n, nq, alpha)
+    ref, ref_drawn = _skew_py_counts(n, nq, alpha)
+    assert counts == ref and drawn == ref_drawn
+
+
+def test_zipf_mix_overshoot_trims_or_raises():
+    import numpy as np
+    from shine_amd import datasets as D
+    pool = np.arange(2000, dtype=np.float32).reshape(2000, 1)
+    counts, drawn = D.zipf_counts(1000, 2500, 0.5)
+    assert drawn > 2500  # the ceilings overshoot: the reference's assert (skew.py:135) would fire here
+    with pytest.raises(ValueError):
+        D.zipf_query_mix(pool[:1000], 2500, 0.5, strict=True)
+    q, warm, src = D.zipf_query_mix(pool[:1000], 2500, 0.5, split=500, seed=4)
+    assert q.shape[0] == 2000 and warm.shape[0] == 500
+    bc = np.bincount(src, minlength=len(counts))
+    want = np.array(counts)
+    want[-1] -= drawn - 2500  # trimmed from the last count
+    np.testing.assert_array_equal(bc[:len(counts)], want)
+    np.testing.assert_array_equal(np.concatenate([q, warm])[:, 0], pool[src, 0])
+    # alpha 0 with num_queries == pool size: every pool query exactly once, no overshoot (strict passes)
+    q0, _, src0 = D.zipf_query_mix(pool, 2000, 0.0, strict=True, seed=1)
+    assert sorted(src0.tolist()) == list(range(2000))
