@@ -609,6 +609,7 @@ enum PassKind { PASS_LDS = 0, PASS_WHOLE_CU = 1, PASS_LIGHT = 2, PASS_GLOBAL = 3
 
 struct LaunchShape {
   uint32_t cap, grid, vis_cap, vis_limit;
+  uint32_t vis16, vis_bits;  // fast kernel: u16 quotient visited entries over a vis_bits-bit id space
 };
 
 uint32_t pow2_at_least(uint32_t x) {
@@ -622,23 +623,41 @@ int64_t env_int(const char* name, int64_t dflt) {
   return e ? std::atoll(e) : dflt;
 }
 
-// Fast mode: the sorted list lives in VGPRs, LDS holds only the visited table.  The table is sized for concurrency
-// first: as large as the LDS share of the wavefronts that hold the whole batch (up to 16 per CU), never below
-// pow2(24·ef) (a query visits ~5-20·ef nodes; one that fills 7/8 of the table goes to the light pass) and never
-// above pow2(48·ef).
-LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds_per_cu) {
+// Fast mode: the sorted list lives in VGPRs, LDS holds only the visited table.  The table holds between pow2(24·ef)
+// and pow2(48·ef) entries (a query visits ~5-20·ef nodes; one that fills 7/8 of it goes to the light pass).  The
+// shape aims at the wavefronts of two batches being resident together (the next batch in flight runs beside this
+// one instead of waiting for LDS): for each entry width — u32 keys, or u16 quotient entries (VisitedLds<1>) when
+// the id space fits them — the largest table that allows that many wavefronts per CU is taken, and the width with
+// more resident wavefronts, then the larger table, wins; u32 on a tie (its inserts take fewer LDS round trips:
+// measured 8.7 M vs 6.0 M QPS at ef = 32, where both fit; 4.26 M vs 3.89 M at ef = 128, where only u16 does).
+LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds_per_cu, uint64_t id_space) {
   LaunchShape sh{};
-  {
-    const uint32_t want = std::max<uint32_t>(1, std::min<uint32_t>(16, (nq + cus - 1) / cus));
-    const int64_t budget = static_cast<int64_t>(lds_per_cu / want) - static_cast<int64_t>(search_fast_lds_bytes(0, ef));
+  const uint32_t want = std::max<uint32_t>(1, std::min<uint32_t>(16, (nq + cus - 1) / cus));
+  const uint32_t target = std::min<uint32_t>(16, 2 * want);
+  const uint32_t lo = std::min<uint32_t>(8192, std::max<uint32_t>(2048, pow2_at_least(24 * ef)));
+  const uint32_t hi = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(48 * ef)));
+  uint32_t bits = 14;
+  while (bits < 32 && (1ull << bits) < id_space) ++bits;
+  auto log2u = [](uint32_t x) { uint32_t l = 0; while ((1u << l) < x) ++l; return l; };
+  auto table_for = [&](uint32_t entry_bytes) {
+    const int64_t budget = static_cast<int64_t>(lds_per_cu / target) - static_cast<int64_t>(search_fast_lds_bytes(0, ef));
     uint32_t fit = 1024;
-    while (static_cast<int64_t>(fit) * 2 * 4 <= budget) fit *= 2;
-    const uint32_t lo = std::min<uint32_t>(8192, std::max<uint32_t>(2048, pow2_at_least(24 * ef)));
-    const uint32_t hi = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(48 * ef)));
-    sh.vis_cap = std::max(lo, std::min(hi, fit));
-  }
+    while (static_cast<int64_t>(fit) * 2 * entry_bytes <= budget) fit *= 2;
+    return std::max(lo, std::min(hi, fit));
+  };
+  auto resident = [&](uint32_t t, uint32_t entry_bytes) {
+    return std::min<uint64_t>(target, lds_per_cu / search_fast_lds_bytes(t, ef, entry_bytes));
+  };
+  const uint32_t t32 = table_for(4), t16 = table_for(2);
+  const bool can16 = env_int("SHINE_DEBUG_VIS16", 1) != 0 && bits <= log2u(t16) + 11;
+  const uint64_t w32 = resident(t32, 4), w16 = can16 ? resident(t16, 2) : 0;
+  sh.vis16 = can16 && (w16 > w32 || (w16 == w32 && t16 > t32)) ? 1 : 0;
+  if (env_int("SHINE_DEBUG_VIS16", -1) == 1 && can16) sh.vis16 = 1;  // test hook: force the u16 entries
+  sh.vis_cap = sh.vis16 ? t16 : t32;
   sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
-  const uint64_t need = search_fast_lds_bytes(sh.vis_cap, ef);
+  if (sh.vis16 && bits > log2u(sh.vis_cap) + 11) sh.vis16 = 0;  // a forced small table: back to u32 entries
+  sh.vis_bits = std::max(bits, log2u(sh.vis_cap) + 1);
+  const uint64_t need = search_fast_lds_bytes(sh.vis_cap, ef, sh.vis16 ? 2 : 4);
   const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(lds_per_cu / need));
   const uint32_t wpc = std::max<uint32_t>(1, std::min<uint32_t>({(nq + cus - 1) / cus, 16u, fit}));
   sh.cap = 0;
@@ -747,7 +766,8 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   for (int i = 0; i < n_pass; ++i) {
     const int pass = chain[i];
     const LaunchShape sh =
-        pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu) : pick_shape(h, R, nq, ef, pass, handed);
+        pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu, h->id_space)
+                          : pick_shape(h, R, nq, ef, pass, handed);
     SearchArgs a{};
     a.g = dev_graph(h, R);
     if (!a.g.vec || !a.g.adj0 || !a.g.uid || !a.g.up_base)
@@ -780,6 +800,9 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     a.log_cap = kLogCap;
     a.counter = S.counter.p + i;
     a.fast = pass == PASS_FAST ? 1u : 0u;
+    a.vis16 = sh.vis16;
+    a.vis_bits = sh.vis_bits;
+    a.vis_mul = 0x9E3779B1u;  // odd: x -> x * mul mod 2^vis_bits permutes the id space
     a.sort_out = fast_mode ? 1u : 0u;
     a.access = d_access;
     if (i > 0) {

@@ -53,6 +53,9 @@ struct SearchArgs {
   uint32_t fast;            // 1: sorted-list kernel (SHINE_MODE_FAST; ef <= kFastMaxEf, vis_cap > 0)
   uint32_t sort_out;        // heap kernel writes ascending order (fast-mode fixup passes)
   uint32_t global_heaps;    // 1: heap kernel with both heaps in HBM (last fallback pass; vis_cap must be 0)
+  uint32_t vis16;           // fast kernel: u16 quotient visited entries (kernels_impl.h VisitedLds<1>)
+  uint32_t vis_bits;        // ... bits of the id space the multiply permutes (vis_bits - log2(vis_cap) <= 11)
+  uint32_t vis_mul;         // ... odd multiplier
 };
 
 struct DistArgs {
@@ -70,13 +73,13 @@ inline size_t search_lds_bytes(uint32_t ef, uint32_t cap, uint32_t vis_cap) {
   return align16(8ull * ef) + align16(8ull * cap) + 4ull * vis_cap + 64 * 4 * 2;
 }
 
-// LDS of the fast kernel: visited table[vis_cap] | scratch ids[64], dists[64] | merge scratch[kFastMaxEf + 1] u64
+// LDS of the fast kernel: visited table[vis_cap] (entry_bytes each) | scratch ids[64], dists[64] | merge scratch
 constexpr uint32_t kFastMaxEf = 512;
 // list registers per lane of the fast kernel for this ef (1, 2, 4 or 8)
 inline uint32_t fast_list_regs(uint32_t ef) { return ef <= 64 ? 1 : ef <= 128 ? 2 : ef <= 256 ? 4 : 8; }
 // the merge scratch holds the 64 R list positions plus the cut and sink slots
-inline size_t search_fast_lds_bytes(uint32_t vis_cap, uint32_t ef) {
-  return 4ull * vis_cap + 64 * 4 * 2 + 8ull * (64 * fast_list_regs(ef) + 2);
+inline size_t search_fast_lds_bytes(uint32_t vis_cap, uint32_t ef, uint32_t entry_bytes = 4) {
+  return align16(static_cast<size_t>(entry_bytes) * vis_cap) + 64 * 4 * 2 + 8ull * (64 * fast_list_regs(ef) + 2);
 }
 
 // Device row layout of the vectors.  The reference's AVX2 kernels keep 8 accumulators: accumulator a sums the

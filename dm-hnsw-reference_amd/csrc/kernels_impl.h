@@ -875,23 +875,104 @@ constexpr u32 EXPANDED = 0x80000000u;  // id bit: this candidate has been expand
 // refilled as soon as the current distances have consumed it, and every list / vector load on the common path is
 // unconditional, so every wait is an exact vmcnt that never covers the younger prefetches.
 // ------------------------------------------------------------------------------------------------------------
-template <int D, typename E, int P>
-__device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restrict__ vec, u32 e, u32 pad, int g4,
-                                           int c4) {
-  u32 sid[P];
-#pragma unroll
-  for (int p = 0; p < P; ++p) sid[p] = static_cast<u32>(__shfl(static_cast<int>(e), 16 * p + g4));
-#pragma unroll
-  for (int p = 0; p < P; ++p) issue_pass_u<D, E, P>(B, p, vec, sid[p], pad, c4);
-}
+// ------------------------------------------------------------------------------------------------------------
+// Exact visited set of the fast kernel (hashset_t<RemotePtr>, types.hh:14-15) in the wave's LDS share.
+//   VT = 0: u32 keys, linear probing from a multiplicative hash (4 B per entry).
+//   VT = 1: u16 quotient entries (2 B per entry): an odd multiply permutes the b-bit id space, the top t bits of
+//           the image pick the home slot, and the entry keeps the other b - t bits plus the slot's distance from
+//           home, so (slot, entry) names the id exactly.  Two entries share a 32-bit word; inserts are word-wide
+//           compare-and-swaps whose first attempt assumes an empty word (one LDS round trip when it is).  Half the
+//           LDS per wave lets two batches of 1,024 queries hold all their wavefronts on the CUs at once.  An id
+//           that would land farther than 2^(16-(b-t)) - 2 slots from home stops the query (light pass re-runs it).
+// ------------------------------------------------------------------------------------------------------------
+template <int VT>
+struct VisitedLds;
 
-template <int D, int METRIC, typename E, int R, int P, bool ACCT, bool PROF = false>
+template <>
+struct VisitedLds<0> {
+  u32* t;
+  u32 mask, shift;
+  __device__ __forceinline__ VisitedLds(void* base, const SearchArgs& A)
+      : t(static_cast<u32*>(base)), mask(A.vis_cap - 1), shift(32 - (31 - __clz(static_cast<int>(A.vis_cap)))) {}
+  static constexpr u32 kBytes = 4;
+  __device__ __forceinline__ void clear(const SearchArgs& A, int lane) {
+    uint4* t4 = reinterpret_cast<uint4*>(t);
+    for (u32 i = lane; i < A.vis_cap / 4; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
+  }
+  __device__ __forceinline__ void insert_first(u32 x) { t[vhash(x, shift)] = x; }  // the table is empty
+  __device__ __forceinline__ bool at_home(u32 x) const { return t[vhash(x, shift)] == x; }
+  __device__ __forceinline__ bool test_and_set(u32 x, bool& /*ovf*/) {
+    u32 h = vhash(x, shift);
+    for (;;) {
+      const u32 old = atomicCAS(&t[h], INV, x);
+      if (old == INV) return true;
+      if (old == x) return false;
+      h = (h + 1) & mask;
+    }
+  }
+};
+
+template <>
+struct VisitedLds<1> {
+  u32* t;
+  unsigned short* t16;
+  u32 mask, mul, bmask, rbits, rmask, dbits, dmax;
+  __device__ __forceinline__ VisitedLds(void* base, const SearchArgs& A)
+      : t(static_cast<u32*>(base)), t16(static_cast<unsigned short*>(base)), mask(A.vis_cap - 1), mul(A.vis_mul) {
+    const u32 tb = 31 - __clz(static_cast<int>(A.vis_cap));
+    bmask = A.vis_bits >= 32 ? ~0u : (1u << A.vis_bits) - 1;
+    rbits = A.vis_bits - tb;
+    rmask = (1u << rbits) - 1;
+    dbits = 16 - rbits;
+    dmax = (1u << dbits) - 2;  // an all-ones entry is the empty marker
+  }
+  static constexpr u32 kBytes = 2;
+  __device__ __forceinline__ void clear(const SearchArgs& A, int lane) {
+    uint4* t4 = reinterpret_cast<uint4*>(t);
+    for (u32 i = lane; i < A.vis_cap / 8; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
+  }
+  __device__ __forceinline__ u32 image(u32 x) const { return (x * mul) & bmask; }
+  __device__ __forceinline__ void insert_first(u32 x) {
+    const u32 h = image(x);
+    t16[h >> rbits] = static_cast<unsigned short>((h & rmask) << dbits);
+  }
+  __device__ __forceinline__ bool at_home(u32 x) const {
+    const u32 h = image(x);
+    return t16[h >> rbits] == static_cast<unsigned short>((h & rmask) << dbits);
+  }
+  __device__ __forceinline__ bool test_and_set(u32 x, bool& ovf) {
+    const u32 h = image(x);
+    u32 s = h >> rbits, disp = 0, cur = INV;  // first attempt: the word is assumed empty
+    const u32 rem = (h & rmask) << dbits;
+    for (;;) {
+      const u32 sh = (s & 1u) << 4;
+      const u32 half = (cur >> sh) & 0xFFFFu;
+      const u32 entry = rem | disp;
+      if (half == 0xFFFFu) {
+        const u32 want = (cur & ~(0xFFFFu << sh)) | (entry << sh);
+        const u32 old = atomicCAS(&t[s >> 1], cur, want);
+        if (old == cur) return true;
+        cur = old;  // the word was not as assumed: look at this slot again
+        continue;
+      }
+      if (half == entry) return false;  // same home, same remainder: this id
+      s = (s + 1) & mask;
+      if (++disp > dmax) {
+        ovf = true;
+        return false;
+      }
+      if ((s & 1u) == 0) cur = INV;  // a new word: assume it empty again
+    }
+  }
+};
+
+template <int D, int METRIC, typename E, int R, int P, bool ACCT, int VT, bool PROF = false>
 __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
   PhaseClock<PROF> clk;
   clk.start();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  u32* vtab = reinterpret_cast<u32*>(smem);  // visited table
-  u32* sc_ids = vtab + A.vis_cap;             // greedy-descent scratch
+  VisitedLds<VT> vis(smem, A);                // visited table
+  u32* sc_ids = reinterpret_cast<u32*>(smem + A.vis_cap * VisitedLds<VT>::kBytes);  // greedy-descent scratch
   float* sc_d = reinterpret_cast<float*>(sc_ids + 64);
   u64* mrg = reinterpret_cast<u64*>(sc_d + 64);  // merge scratch: (key, id) at merged positions 0 .. ef
   const int lane = threadIdx.x, g4 = lane >> 2, c4 = lane & 3;
@@ -899,13 +980,27 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
   const u32* __restrict__ adj0 = A.g.adj0;
   const u32 M0 = A.g.M0, pad = A.g.pad_node;
   const int ef = static_cast<int>(A.ef);
-  const u32 vmask = A.vis_cap - 1, vshift = 32 - (31 - __clz(static_cast<int>(A.vis_cap)));
   const float INF = __builtin_inff();
   const bool in_row = static_cast<u32>(lane) < M0;
   const u32 row_lane = in_row ? static_cast<u32>(lane) : 0u;
   // Unconditional, and never masked right after the load (that would wait for it): lanes beyond M0 hold a copy of
   // entry 0 and are excluded where the list is used (the visited test; slots >= M0 are never fresh).
   auto load_row = [&](u32 node) -> u32 { return adj0[static_cast<u64>(node) * M0 + row_lane]; };
+  // The same row in the layout of the vector loads: lane l holds entry 16p + (l >> 2) for pass p (the four lanes
+  // of a group read one word, a broadcast inside the row's cache line), so the slot ids reach the address
+  // computation without a cross-lane shuffle (two LDS round trips fewer between the pick and the vector loads).
+  // Slots past M0 read entry M0 - 1 and are masked where the row is used.
+  u32 gcol[P];
+  bool gvalid[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    gvalid[p] = static_cast<u32>(16 * p + g4) < M0;
+    gcol[p] = gvalid[p] ? static_cast<u32>(16 * p + g4) : M0 - 1;
+  }
+  auto load_row_g = [&](u32 node, u32 (&g)[P]) {
+#pragma unroll
+    for (int p = 0; p < P; ++p) g[p] = adj0[static_cast<u64>(node) * M0 + gcol[p]];
+  };
 
   const u32 n_items = A.in_count ? *A.in_count : A.nq;
   for (;;) {
@@ -918,10 +1013,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
     PHASE(0)
     QueryRegs<D> Q;
     load_query<D>(A.queries + static_cast<u64>(qi) * D, lane, Q);
-    {
-      uint4* t4 = reinterpret_cast<uint4*>(vtab);
-      for (u32 i = lane; i < A.vis_cap / 4; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
-    }
+    vis.clear(A, lane);
     u32 st_dist = 0, st_vup = 0, st_vl0 = 0, st_lup = 0, st_ll0 = 0, ties = 0, status = 0;
     ReadCount rc;
     PHASE(1)
@@ -946,19 +1038,35 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       ci[0] = lane == 0 ? (nn | EXPANDED) : INV;  // popped right away (:418)
       cs = 1;
       if (closest != closest) ++ties;
-      if (lane == 0) vtab[vhash(nn, vshift)] = nn;
+      if (lane == 0) vis.insert_first(nn);
       wave_sync();
     }
 
     // pipeline state: the candidate's list `e` and its vectors in X (in flight); the runner-up r and its
     // prefetched list.  X is refilled for the next candidate as soon as the current distances have consumed it.
     NbrBuf<D, E, P> X;
+    // issue the vector loads of a row held in group layout; with `filter`, entries already at their home slot of
+    // the visited table read the pad node instead (they cannot be fresh)
+    auto issue_group = [&](const u32 (&g)[P], bool filter) {
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        u32 v = gvalid[p] ? g[p] : INV;
+        if (filter && v != INV && vis.at_home(v)) v = INV;
+        issue_pass_u<D, E, P>(X, p, vec, v, pad, c4);
+      }
+    };
     u32 e = load_row(status == 0 ? nn : pad);
-    issue_list<D, E, P>(X, vec, e, pad, g4, c4);
+    {
+      u32 eg[P];
+      load_row_g(status == 0 ? nn : pad, eg);
+      issue_group(eg, false);
+    }
     u32 r_id = INV;
     float r_key = INF;
     u32 nid = nn;
     u32 nrow = load_row(nn);
+    u32 nrow_g[P];
+    load_row_g(nn, nrow_g);
     u32 cur = nn;  // the candidate whose list `e` is
 
     while (status == 0) {
@@ -972,15 +1080,11 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
           if (j < static_cast<u32>(lane) && ej == e) cand = false;
         }
       }
-      bool fresh = false;
-      if (cand) {  // visited.contains / insert (:441-443)
-        u32 h = vhash(e, vshift);
-        for (;;) {
-          const u32 old = atomicCAS(&vtab[h], INV, e);
-          if (old == INV) { fresh = true; break; }
-          if (old == e) break;
-          h = (h + 1) & vmask;
-        }
+      bool fresh = false, vovf = false;
+      if (cand) fresh = vis.test_and_set(e, vovf);  // visited.contains / insert (:441-443)
+      if (VT == 1 && __ballot(vovf)) {  // an id too far from its home slot: the light pass re-runs the query
+        status = ST_OVERFLOW;
+        break;
       }
       const u64 fm = __ballot(fresh);
       const int nf = __popcll(fm);
@@ -1026,11 +1130,18 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
           pid = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(e), 63 - static_cast<int>(__clzll(hit))));
       }
       if (pid == r_id) EVENT(9) else EVENT(10)
-      const u32 prow = pid == r_id ? nrow : load_row(pid != INV ? pid : pad);  // a fresh f*: its list now
+      u32 prow, prow_g[P];
+      if (pid == r_id) {
+        prow = nrow;
+#pragma unroll
+        for (int p = 0; p < P; ++p) prow_g[p] = nrow_g[p];
+      } else {  // a fresh f*: its list now
+        prow = load_row(pid != INV ? pid : pad);
+        load_row_g(pid != INV ? pid : pad, prow_g);
+      }
       // an entry already at its home slot of the visited table is not fresh: its row is not requested (one
-      // read-only LDS probe; the visit proper still runs at the top of the next expansion)
-      const bool seen = in_row && prow != INV && vtab[vhash(prow, vshift)] == prow;
-      issue_list<D, E, P>(X, vec, seen ? INV : prow, pad, g4, c4);
+      // read-only LDS probe per lane group; the visit proper still runs at the top of the next expansion)
+      issue_group(prow_g, true);
 
       // ---- merge (:456-465 over the whole list at once) ----------------------------------------------------------
       PHASE(6)
@@ -1127,12 +1238,21 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       u32 erow = prow;
       if (c != pid) {  // mispredicted (ties / NaN keys): fetch the picked candidate's list and vectors
         EVENT(11)
-        erow = c == nid ? nrow : load_row(c);
-        issue_list<D, E, P>(X, vec, erow, pad, g4, c4);
+        u32 eg[P];
+        if (c == nid) {
+          erow = nrow;
+#pragma unroll
+          for (int p = 0; p < P; ++p) eg[p] = nrow_g[p];
+        } else {
+          erow = load_row(c);
+          load_row_g(c, eg);
+        }
+        issue_group(eg, false);
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this rare path leaves nothing in flight behind the prefetch
       }
       nid = c2 != INV ? c2 : c;
-      nrow = load_row(nid);  // unconditional: always the youngest load
+      nrow = load_row(nid);  // unconditional: always the youngest loads
+      load_row_g(nid, nrow_g);
       e = erow;
       cur = c;
       r_id = c2;
@@ -1267,7 +1387,7 @@ hipError_t launch_search_acct(uint32_t grid, const SearchArgs& a, hipStream_t s)
     return hipGetLastError();
   };
   if (a.fast) {  // sorted-list kernel; the launcher's caller guarantees ef <= kFastMaxEf and a visited table in LDS
-    const size_t lds_f = search_fast_lds_bytes(a.vis_cap, a.ef);
+    const size_t lds_f = search_fast_lds_bytes(a.vis_cap, a.ef, a.vis16 ? 2 : 4);
     auto runf = [&](auto kern) -> hipError_t {
       if (lds_f > 65536) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -1281,16 +1401,20 @@ hipError_t launch_search_acct(uint32_t grid, const SearchArgs& a, hipStream_t s)
     // P = passes of 16 list slots: 2 covers M0 <= 32 (M <= 16), 4 covers M0 <= 64
     if (a.g.M0 > 64) return hipErrorInvalidValue;
     const bool wide = a.g.M0 > 32;
-    if constexpr (!AC && D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
-      if (a.prof && !wide && a.ef > 64 && a.ef <= 128) return runf(search_fast_kernel<D, METRIC, E, 2, 2, AC, true>);
-    }
-    if (a.ef <= 64)
-      return wide ? runf(search_fast_kernel<D, METRIC, E, 1, 4, AC>) : runf(search_fast_kernel<D, METRIC, E, 1, 2, AC>);
-    if (a.ef <= 128)
-      return wide ? runf(search_fast_kernel<D, METRIC, E, 2, 4, AC>) : runf(search_fast_kernel<D, METRIC, E, 2, 2, AC>);
-    if (a.ef <= 256)
-      return wide ? runf(search_fast_kernel<D, METRIC, E, 4, 4, AC>) : runf(search_fast_kernel<D, METRIC, E, 4, 2, AC>);
-    return wide ? runf(search_fast_kernel<D, METRIC, E, 8, 4, AC>) : runf(search_fast_kernel<D, METRIC, E, 8, 2, AC>);
+    auto pick = [&](auto vt) -> hipError_t {
+      constexpr int VT = decltype(vt)::value;
+      if constexpr (!AC && D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
+        if (a.prof && !wide && a.ef > 64 && a.ef <= 128) return runf(search_fast_kernel<D, METRIC, E, 2, 2, AC, VT, true>);
+      }
+      if (a.ef <= 64)
+        return wide ? runf(search_fast_kernel<D, METRIC, E, 1, 4, AC, VT>) : runf(search_fast_kernel<D, METRIC, E, 1, 2, AC, VT>);
+      if (a.ef <= 128)
+        return wide ? runf(search_fast_kernel<D, METRIC, E, 2, 4, AC, VT>) : runf(search_fast_kernel<D, METRIC, E, 2, 2, AC, VT>);
+      if (a.ef <= 256)
+        return wide ? runf(search_fast_kernel<D, METRIC, E, 4, 4, AC, VT>) : runf(search_fast_kernel<D, METRIC, E, 4, 2, AC, VT>);
+      return wide ? runf(search_fast_kernel<D, METRIC, E, 8, 4, AC, VT>) : runf(search_fast_kernel<D, METRIC, E, 8, 2, AC, VT>);
+    };
+    return a.vis16 ? pick(std::integral_constant<int, 1>{}) : pick(std::integral_constant<int, 0>{});
   }
   if constexpr (!AC && D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
     if (a.prof && a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0, AC, true>);

@@ -194,3 +194,17 @@ def test_concurrent_batches_on_streams_share_one_handle(mode, gpu_available, mon
             np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32).reshape(-1, 10), want.ids)
             np.testing.assert_array_equal(qs.cpu().numpy().view(np.uint32).reshape(-1, L.QS_WORDS)[:, :5],
                                           want.qstats[:, :5])
+
+
+@pytest.mark.parametrize("vis16", ["0", "1"])
+def test_fast_mode_visited_entry_widths_agree(vis16, gpu_available, monkeypatch):
+    """The u16 quotient visited table (VisitedLds<1>) and the u32 table (forced with SHINE_DEBUG_VIS16=0) are the
+    same exact set: identical results, counters and tie counts, here with a small table so probe chains are long."""
+    base = D.deep_like(6000, seed=97, d=96)
+    q = D.deep_like(200, seed=98, d=96)
+    dumps, _, _ = O.build(base, 16, 100, 0, 1, seed=4)
+    ref = O.OracleIndex(dumps, 96, 16, 0).knn(q, 10, 128)
+    monkeypatch.setenv("SHINE_DEBUG_VIS16", vis16)
+    monkeypatch.setenv("SHINE_DEBUG_VISCAP", "4096")
+    r = _fast_knn(dumps, 96, 16, 0, q, 10, 128)
+    _check_tie_free_exact(r, ref, 0.95)
