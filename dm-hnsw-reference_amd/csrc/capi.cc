@@ -623,7 +623,7 @@ int64_t env_int(const char* name, int64_t dflt) {
   return e ? std::atoll(e) : dflt;
 }
 
-// Fast mode: the sorted list lives in VGPRs, LDS holds only the visited table.  The table holds between pow2(24·ef)
+// Fast mode: the sorted list lives in VGPRs, LDS holds only the visited table.  The table holds between pow2(40·ef)
 // and pow2(48·ef) entries (a query visits ~5-20·ef nodes; one that fills 7/8 of it goes to the light pass).  The
 // shape aims at the wavefronts of two batches being resident together (the next batch in flight runs beside this
 // one instead of waiting for LDS): for each entry width — u32 keys, or u16 quotient entries (VisitedLds<1>) when
@@ -634,8 +634,10 @@ LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds
   LaunchShape sh{};
   const uint32_t want = std::max<uint32_t>(1, std::min<uint32_t>(16, (nq + cus - 1) / cus));
   const uint32_t target = std::min<uint32_t>(16, 2 * want);
-  const uint32_t lo = std::min<uint32_t>(8192, std::max<uint32_t>(2048, pow2_at_least(24 * ef)));
-  const uint32_t hi = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(48 * ef)));
+  // a table below pow2(40·ef) entries sends a measurable share of queries to the light pass (ef = 128 on the bench's
+  // index: 4,096 entries gave 1.1 M QPS against 4.2 M for 8,192), whatever residency it buys
+  const uint32_t lo = std::min<uint32_t>(16384, std::max<uint32_t>(2048, pow2_at_least(40 * ef)));
+  const uint32_t hi = std::min<uint32_t>(16384, std::max<uint32_t>(lo, pow2_at_least(48 * ef)));
   uint32_t bits = 14;
   while (bits < 32 && (1ull << bits) < id_space) ++bits;
   auto log2u = [](uint32_t x) { uint32_t l = 0; while ((1u << l) < x) ++l; return l; };
@@ -822,8 +824,10 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("search launch: ") + hipGetErrorString(e));
   }
   if (timed) HIP_TRY(hipEventRecord(R.ev1, s));
-  HIP_TRY(hipMemcpyAsync(S.seen.p, S.counter.p + 4, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  S.seen.p[3] = 1;
+  if (!env_int("SHINE_DEBUG_NO_SEEN", 0)) {  // measurement hook: the light pass sized without the last counts
+    HIP_TRY(hipMemcpyAsync(S.seen.p, S.counter.p + 4, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    S.seen.p[3] = 1;
+  }
   return 0;
 }
 

@@ -17,7 +17,7 @@ if not path.exists():
     dumps[0].tofile(path)
     if os.environ.get("BUILD_ONLY"):
         sys.exit(0)
-q = D.sift_like(1024, seed=2)
+q = D.sift_like(int(os.environ.get("NQ", "1024")), seed=2)
 idx = shine_amd.Index.open([path], 128, 16, 0, gpus=[0])
 idx.set_search_mode(shine_amd.MODE_FAST)
 for _ in range(int(os.environ.get("REPS", "2"))):
