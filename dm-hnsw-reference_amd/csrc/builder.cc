@@ -24,13 +24,10 @@
 #include <thread>
 #include <vector>
 
-#if defined(__AVX2__) && defined(__FMA__)
-#include <immintrin.h>
-#define SHINE_HOST_AVX2 1
-#endif
 
 #include "../../include/shine_gpu.h"
 #include "graph.h"
+#include "hostdist.h"
 
 namespace shine {
 namespace {
@@ -38,53 +35,6 @@ namespace {
 constexpr u64 kLock = 0b01;                    // node.hh:28
 constexpr u64 kNewLevelLock = 0b100000000;     // node.hh:29
 constexpr u64 kEntryNode = 0b10000000000000000;// node.hh:30
-
-// Same FP order as the GPU kernels and the oracle (DESIGN.md "Distance FP order").
-f32 host_l2(const f32* a, const f32* b, u32 dim) {
-  const u32 q16 = dim >> 4 << 4;
-  alignas(32) f32 acc[8];
-#ifdef SHINE_HOST_AVX2
-  __m256 s = _mm256_setzero_ps();
-  for (u32 i = 0; i < q16; i += 8) {
-    const __m256 d = _mm256_sub_ps(_mm256_loadu_ps(a + i), _mm256_loadu_ps(b + i));
-    s = _mm256_fmadd_ps(d, d, s);
-  }
-  _mm256_store_ps(acc, s);
-#else
-  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-  for (u32 i = 0; i < q16; i += 8)
-    for (int j = 0; j < 8; ++j) {
-      const f32 d = a[i + j] - b[i + j];
-      acc[j] = std::fmaf(d, d, acc[j]);
-    }
-#endif
-  f32 r = acc[0];
-  for (int j = 1; j < 8; ++j) r = r + acc[j];
-  for (u32 i = q16; i < dim; ++i) {
-    const f32 d = a[i] - b[i];
-    r = std::fmaf(d, d, r);
-  }
-  return r;
-}
-
-f32 host_ip(const f32* a, const f32* b, u32 dim) {
-  const u32 q16 = dim >> 4 << 4;
-  alignas(32) f32 acc[8];
-#ifdef SHINE_HOST_AVX2
-  __m256 s = _mm256_setzero_ps();
-  for (u32 i = 0; i < q16; i += 8) s = _mm256_fmadd_ps(_mm256_loadu_ps(a + i), _mm256_loadu_ps(b + i), s);
-  _mm256_store_ps(acc, s);
-#else
-  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-  for (u32 i = 0; i < q16; i += 8)
-    for (int j = 0; j < 8; ++j) acc[j] = std::fmaf(a[i + j], b[i + j], acc[j]);
-#endif
-  f32 r = acc[0];
-  for (int j = 1; j < 8; ++j) r = r + acc[j];
-  f32 t = 0.f;
-  for (u32 i = q16; i < dim; ++i) t = std::fmaf(a[i], b[i], t);
-  return 1.0f - (r + t);
-}
 
 struct Entry {
   u64 node;

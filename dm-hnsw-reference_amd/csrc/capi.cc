@@ -180,6 +180,8 @@ struct IndexState {
   ShardedArray svec, sadj0;    // sharded: level-0 vectors and lists
   double cache_fraction = 0;
   Regions regions;             // SHINE_PLACE_SHARDED_REGIONS: slot o owns (and is routed) region o
+  Router router;               // ... the query router's limits and histogram, kept across calls
+  std::vector<double> slot_rate;  // ... queries per ms each slot answered in its last call (0 = not measured)
   std::vector<Replica> reps;
   // sharded placements: the host graph and its device ids, kept to re-rank the stripes after a cache warmup
   HostGraph host;
@@ -426,8 +428,11 @@ int make_index(HostGraph G, int elem, const int* gpu_ids, uint32_t n_gpus, int p
   uint64_t U = G.N;
   size_t gran = 0;
   if (sharded) {
-    if (placement == SHINE_PLACE_SHARDED_REGIONS) {  // k-means regions of the top levels (placement.hh:22-61)
-      h->regions = kmeans_regions(G, top_level_sample(G, std::max<uint32_t>(500, 64 * slots)), slots, 0);
+    if (placement == SHINE_PLACE_SHARDED_REGIONS) {  // balanced k-means regions of the top levels (placement.hh:22-61)
+      if (plan_regions(G, slots, true, h->regions))
+        return set_error(SHINE_ERR_ARG, "region placement: fewer top-level nodes than k-means clusters");
+      h->router.init(slots);
+      h->slot_rate.assign(slots, 0.0);
       const std::vector<uint32_t> region = assign_regions(G, h->regions, 0.05, 1);
       for (uint64_t g = 0; g < G.N; ++g) order[region[g]].push_back(static_cast<uint32_t>(g));
     } else {
@@ -863,10 +868,29 @@ int validate_views(shine_index* h) {
   return 0;
 }
 
-void route_batch(const shine_index* h, const float* q, const uint32_t* ids, uint32_t nq, uint32_t* out) {
+// The queue sizes the compute nodes' acks would carry at a batch boundary (query_router.hh:233-255, 304-311).  The
+// host routes a whole call before any slot starts, so a slot's queue is modelled: the queries routed to it so far
+// minus what it answers while the node as a whole answers all of them, at the per-slot rates of the last call.
+void modelled_queues(const std::vector<double>& rate, const std::vector<uint64_t>& routed, std::vector<uint32_t>& q) {
+  double total = 0, rsum = 0;
+  for (size_t i = 0; i < routed.size(); ++i) {
+    total += static_cast<double>(routed[i]);
+    rsum += rate[i] > 0 ? rate[i] : 1.0;
+  }
+  const double t = total / rsum;
+  for (size_t i = 0; i < routed.size(); ++i) {
+    const double r = rate[i] > 0 ? rate[i] : 1.0;
+    q[i] = static_cast<uint32_t>(std::llround(std::max(0.0, static_cast<double>(routed[i]) - r * t)));
+  }
+}
+
+void route_batch(shine_index* h, const float* q, const uint32_t* ids, uint32_t nq, uint32_t* out) {
   const uint32_t G = static_cast<uint32_t>(h->reps.size());
-  if (h->placement == SHINE_PLACE_SHARDED_REGIONS && G > 1) {
-    route_queries(h->regions, q, nq, 0.25, out);  // per-batch limits, query_router.hh:359-372
+  if (h->placement == SHINE_PLACE_SHARDED_REGIONS && G > 1) {  // QueryRouter::run_routing (query_router.hh:280-387)
+    const std::vector<double>& rate = h->slot_rate;
+    h->router.route(h->regions, q, nq, h->dim,
+                    [&](const std::vector<uint64_t>& routed, std::vector<uint32_t>& p) { modelled_queues(rate, routed, p); },
+                    out);
     return;
   }
   for (uint32_t i = 0; i < nq; ++i) out[i] = (ids ? ids[i] : i) % G;
@@ -1061,6 +1085,7 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, R.ev0, R.ev1));
     kernel_ms = std::max(kernel_ms, static_cast<double>(ms));
+    if (r < h->slot_rate.size() && ms > 0) h->slot_rate[r] = n / static_cast<double>(ms);
     const uint32_t* cnt = R.hqs.p + static_cast<size_t>(n) * kQsWords;
     retries += cnt[4] + cnt[5] + cnt[6];  // queries handed on by each pass
     if (env_int("SHINE_PHASE_PROFILE", 0) && R.prof.p) print_phase_profile(h, R);
@@ -1186,14 +1211,18 @@ int shine_route(shine_index_t h, const float* queries, uint32_t nq, uint32_t* ou
 }
 
 int shine_plan_regions(const uint8_t* const* dumps, const uint64_t* sizes, uint32_t n_dumps, uint32_t dim, uint32_t M,
-                       int metric, uint32_t k, uint32_t* region_of_uid, uint64_t uid_capacity, float* centroids) {
+                       int metric, uint32_t k, uint32_t* region_of_uid, uint64_t uid_capacity, float* centroids,
+                       uint32_t* mapping, uint32_t* n_centroids) {
   if (!dumps || !sizes) return set_error(SHINE_ERR_ARG, "dumps / sizes is NULL");
   if (k == 0) return set_error(SHINE_ERR_ARG, "k must be > 0");
   if (metric != SHINE_METRIC_L2 && metric != SHINE_METRIC_IP) return set_error(SHINE_ERR_ARG, "metric must be 0 or 1");
   HostGraph G;
   if (int rc = parse_dumps(dumps, sizes, n_dumps, dim, M, metric, 0, G)) return rc;
-  const Regions R = kmeans_regions(G, top_level_sample(G, std::max<uint32_t>(500, 64 * k)), k, 0);
+  Regions R;
+  if (plan_regions(G, k, true, R)) return set_error(SHINE_ERR_ARG, "fewer top-level nodes than k-means clusters");
   if (centroids) std::memcpy(centroids, R.centroids.data(), R.centroids.size() * sizeof(float));
+  if (mapping) std::memcpy(mapping, R.mapping.data(), R.mapping.size() * sizeof(uint32_t));
+  if (n_centroids) *n_centroids = R.n_centroids();
   if (region_of_uid) {
     const std::vector<uint32_t> region = assign_regions(G, R, 0.05, 1);
     for (uint64_t g = 0; g < G.N; ++g) {
@@ -1201,6 +1230,60 @@ int shine_plan_regions(const uint8_t* const* dumps, const uint64_t* sizes, uint3
       region_of_uid[G.uid[g]] = region[g];
     }
   }
+  return SHINE_OK;
+}
+
+int shine_kmeans(const float* rows, uint64_t n, uint32_t dim, int metric, uint32_t k, int balanced, float* centroids,
+                 uint32_t* mapping, uint32_t* n_centroids, uint64_t* region_sizes, uint32_t* iterations) {
+  if (!rows || !centroids || !mapping) return set_error(SHINE_ERR_ARG, "NULL argument");
+  if (k == 0 || dim == 0) return set_error(SHINE_ERR_ARG, "k and dim must be > 0");
+  if (metric != SHINE_METRIC_L2 && metric != SHINE_METRIC_IP) return set_error(SHINE_ERR_ARG, "metric must be 0 or 1");
+  KmeansInput in;
+  in.metric = metric;
+  in.dim = dim;
+  in.rows.resize(n);
+  for (uint64_t i = 0; i < n; ++i) in.rows[i] = rows + i * dim;
+  Regions R;
+  if (run_and_optimize(in, k, balanced != 0, R)) return set_error(SHINE_ERR_ARG, "fewer rows than k-means clusters");
+  std::memcpy(centroids, R.centroids.data(), R.centroids.size() * sizeof(float));
+  std::memcpy(mapping, R.mapping.data(), R.mapping.size() * sizeof(uint32_t));
+  if (n_centroids) *n_centroids = R.n_centroids();
+  if (region_sizes) std::memcpy(region_sizes, R.sizes.data(), R.sizes.size() * sizeof(uint64_t));
+  if (iterations) {
+    iterations[0] = R.iterations;
+    iterations[1] = R.balance_iterations;
+  }
+  return SHINE_OK;
+}
+
+int shine_router_run(const float* centroids, const uint32_t* mapping, uint32_t n_centroids, uint32_t k, uint32_t dim,
+                     int metric, const float* queries, uint32_t nq, const uint32_t* queue_sizes, uint32_t n_rows,
+                     int adaptive, uint32_t* out_region, uint64_t* out_limits) {
+  if (!centroids || !mapping || (!queries && nq) || (!out_region && nq)) return set_error(SHINE_ERR_ARG, "NULL argument");
+  if (k == 0 || n_centroids == 0 || dim == 0) return set_error(SHINE_ERR_ARG, "k, n_centroids and dim must be > 0");
+  for (uint32_t i = 0; i < n_centroids; ++i)
+    if (mapping[i] >= k) return set_error(SHINE_ERR_ARG, "mapping names a region >= k");
+  Regions R;
+  R.k = k;
+  R.dim = dim;
+  R.metric = metric;
+  R.centroids.assign(centroids, centroids + static_cast<size_t>(n_centroids) * dim);
+  R.mapping.assign(mapping, mapping + n_centroids);
+  Router router;
+  router.init(k);
+  router.adaptive = adaptive != 0;
+  uint32_t boundary = 0;
+  router.route(R, queries, nq, dim,
+               [&](const std::vector<uint64_t>&, std::vector<uint32_t>& p) {
+                 if (queue_sizes && n_rows) {
+                   const uint32_t row = std::min(boundary, n_rows - 1);
+                   std::copy(queue_sizes + static_cast<size_t>(row) * k, queue_sizes + static_cast<size_t>(row + 1) * k,
+                             p.begin());
+                 }
+                 ++boundary;
+               },
+               out_region);
+  if (out_limits) std::copy(router.limits.begin(), router.limits.end(), out_limits);
   return SHINE_OK;
 }
 

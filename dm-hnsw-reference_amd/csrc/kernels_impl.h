@@ -875,6 +875,16 @@ constexpr u32 EXPANDED = 0x80000000u;  // id bit: this candidate has been expand
 // refilled as soon as the current distances have consumed it, and every list / vector load on the common path is
 // unconditional, so every wait is an exact vmcnt that never covers the younger prefetches.
 // ------------------------------------------------------------------------------------------------------------
+template <int D, typename E, int P>
+__device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restrict__ vec, u32 e, u32 pad, int g4,
+                                           int c4) {
+  u32 sid[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) sid[p] = static_cast<u32>(__shfl(static_cast<int>(e), 16 * p + g4));
+#pragma unroll
+  for (int p = 0; p < P; ++p) issue_pass_u<D, E, P>(B, p, vec, sid[p], pad, c4);
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // Exact visited set of the fast kernel (hashset_t<RemotePtr>, types.hh:14-15) in the wave's LDS share.
 //   VT = 0: u32 keys, linear probing from a multiplicative hash (4 B per entry).
@@ -986,21 +996,6 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
   // Unconditional, and never masked right after the load (that would wait for it): lanes beyond M0 hold a copy of
   // entry 0 and are excluded where the list is used (the visited test; slots >= M0 are never fresh).
   auto load_row = [&](u32 node) -> u32 { return adj0[static_cast<u64>(node) * M0 + row_lane]; };
-  // The same row in the layout of the vector loads: lane l holds entry 16p + (l >> 2) for pass p (the four lanes
-  // of a group read one word, a broadcast inside the row's cache line), so the slot ids reach the address
-  // computation without a cross-lane shuffle (two LDS round trips fewer between the pick and the vector loads).
-  // Slots past M0 read entry M0 - 1 and are masked where the row is used.
-  u32 gcol[P];
-  bool gvalid[P];
-#pragma unroll
-  for (int p = 0; p < P; ++p) {
-    gvalid[p] = static_cast<u32>(16 * p + g4) < M0;
-    gcol[p] = gvalid[p] ? static_cast<u32>(16 * p + g4) : M0 - 1;
-  }
-  auto load_row_g = [&](u32 node, u32 (&g)[P]) {
-#pragma unroll
-    for (int p = 0; p < P; ++p) g[p] = adj0[static_cast<u64>(node) * M0 + gcol[p]];
-  };
 
   const u32 n_items = A.in_count ? *A.in_count : A.nq;
   for (;;) {
@@ -1045,28 +1040,12 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
     // pipeline state: the candidate's list `e` and its vectors in X (in flight); the runner-up r and its
     // prefetched list.  X is refilled for the next candidate as soon as the current distances have consumed it.
     NbrBuf<D, E, P> X;
-    // issue the vector loads of a row held in group layout; with `filter`, entries already at their home slot of
-    // the visited table read the pad node instead (they cannot be fresh)
-    auto issue_group = [&](const u32 (&g)[P], bool filter) {
-#pragma unroll
-      for (int p = 0; p < P; ++p) {
-        u32 v = gvalid[p] ? g[p] : INV;
-        if (filter && v != INV && vis.at_home(v)) v = INV;
-        issue_pass_u<D, E, P>(X, p, vec, v, pad, c4);
-      }
-    };
     u32 e = load_row(status == 0 ? nn : pad);
-    {
-      u32 eg[P];
-      load_row_g(status == 0 ? nn : pad, eg);
-      issue_group(eg, false);
-    }
+    issue_list<D, E, P>(X, vec, e, pad, g4, c4);
     u32 r_id = INV;
     float r_key = INF;
     u32 nid = nn;
     u32 nrow = load_row(nn);
-    u32 nrow_g[P];
-    load_row_g(nn, nrow_g);
     u32 cur = nn;  // the candidate whose list `e` is
 
     while (status == 0) {
@@ -1130,18 +1109,11 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
           pid = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(e), 63 - static_cast<int>(__clzll(hit))));
       }
       if (pid == r_id) EVENT(9) else EVENT(10)
-      u32 prow, prow_g[P];
-      if (pid == r_id) {
-        prow = nrow;
-#pragma unroll
-        for (int p = 0; p < P; ++p) prow_g[p] = nrow_g[p];
-      } else {  // a fresh f*: its list now
-        prow = load_row(pid != INV ? pid : pad);
-        load_row_g(pid != INV ? pid : pad, prow_g);
-      }
+      const u32 prow = pid == r_id ? nrow : load_row(pid != INV ? pid : pad);  // a fresh f*: its list now
       // an entry already at its home slot of the visited table is not fresh: its row is not requested (one
-      // read-only LDS probe per lane group; the visit proper still runs at the top of the next expansion)
-      issue_group(prow_g, true);
+      // read-only LDS probe; the visit proper still runs at the top of the next expansion)
+      const bool seen = in_row && prow != INV && vis.at_home(prow);
+      issue_list<D, E, P>(X, vec, seen ? INV : prow, pad, g4, c4);
 
       // ---- merge (:456-465 over the whole list at once) ----------------------------------------------------------
       PHASE(6)
@@ -1238,21 +1210,12 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       u32 erow = prow;
       if (c != pid) {  // mispredicted (ties / NaN keys): fetch the picked candidate's list and vectors
         EVENT(11)
-        u32 eg[P];
-        if (c == nid) {
-          erow = nrow;
-#pragma unroll
-          for (int p = 0; p < P; ++p) eg[p] = nrow_g[p];
-        } else {
-          erow = load_row(c);
-          load_row_g(c, eg);
-        }
-        issue_group(eg, false);
+        erow = c == nid ? nrow : load_row(c);
+        issue_list<D, E, P>(X, vec, erow, pad, g4, c4);
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this rare path leaves nothing in flight behind the prefetch
       }
       nid = c2 != INV ? c2 : c;
-      nrow = load_row(nid);  // unconditional: always the youngest loads
-      load_row_g(nid, nrow_g);
+      nrow = load_row(nid);  // unconditional: always the youngest load
       e = erow;
       cur = c;
       r_id = c2;

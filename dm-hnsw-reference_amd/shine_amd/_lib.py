@@ -112,7 +112,9 @@ PROTOTYPES = {
     "shine_knn_batch_device": (I32, [P, U32, P, U32, U32, U32, P, P, P, P]),
     "shine_distance_batch_device": (I32, [P, U32, P, U32, P, U32, P, P]),
     "shine_route": (I32, [P, P, U32, P]),
-    "shine_plan_regions": (I32, [C.POINTER(PU8), C.POINTER(U64), U32, U32, U32, I32, U32, P, U64, P]),
+    "shine_plan_regions": (I32, [C.POINTER(PU8), C.POINTER(U64), U32, U32, U32, I32, U32, P, U64, P, P, P]),
+    "shine_kmeans": (I32, [P, U64, U32, I32, U32, I32, P, P, P, P, P]),
+    "shine_router_run": (I32, [P, P, U32, U32, U32, I32, P, U32, P, U32, I32, P, P]),
     "shine_set_search_mode": (I32, [P, I32]),
     "shine_index_get_info": (I32, [P, C.POINTER(IndexInfo)]),
     "shine_algorithmic_bytes": (U64, [P, P, U32]),

@@ -185,14 +185,50 @@ def build(base: np.ndarray, M: int, ef_construction: int, metric: int = L.METRIC
     return dumps, dc
 
 
-def plan_regions(dumps, dim: int, M: int, metric: int, k: int) -> tuple[np.ndarray, np.ndarray]:
-    """Host-only region planner of SHINE_PLACE_SHARDED_REGIONS: (centroids [k, dim], region of every uid)."""
+def plan_regions(dumps, dim: int, M: int, metric: int, k: int) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Host-only region planner of SHINE_PLACE_SHARDED_REGIONS: fetch_level(500) + balanced k-means.
+    Returns (centroids [k or 2k, dim], region of every uid, region of every centroid)."""
     dumps, ptrs, sizes = _dump_arrays(dumps)
-    cent = np.empty((k, dim), dtype=np.float32)
+    cent = np.empty((2 * k, dim), dtype=np.float32)
+    mapping = np.empty(2 * k, dtype=np.uint32)
+    nc = C.c_uint32(0)
     n_uid = _max_uid(dumps, dim, M) + 1
     region = np.full(n_uid, 0xFFFFFFFF, dtype=np.uint32)
-    L.check(L.lib().shine_plan_regions(ptrs, sizes, len(dumps), dim, M, metric, k, _ptr(region), n_uid, _ptr(cent)))
-    return cent, region
+    L.check(L.lib().shine_plan_regions(ptrs, sizes, len(dumps), dim, M, metric, k, _ptr(region), n_uid, _ptr(cent),
+                                       _ptr(mapping), C.byref(nc)))
+    return cent[:nc.value].copy(), region, mapping[:nc.value].copy()
+
+
+def kmeans(rows: np.ndarray, k: int, metric: int = L.METRIC_L2, balanced: bool = True) -> dict:
+    """Kmeans<Distance> over rows (shine_kmeans): run_and_optimize (balanced) or run_kmeans.  Returns centroids
+    [k or 2k, dim], mapping (centroid -> region), region sizes and the Lloyd / balancing iteration counts."""
+    x = np.ascontiguousarray(rows, dtype=np.float32)
+    n, dim = x.shape
+    cent = np.empty((2 * k, dim), dtype=np.float32)
+    mapping = np.empty(2 * k, dtype=np.uint32)
+    sizes = np.zeros(k, dtype=np.uint64)
+    nc = C.c_uint32(0)
+    it = np.zeros(2, dtype=np.uint32)
+    L.check(L.lib().shine_kmeans(_ptr(x), n, dim, metric, k, int(balanced), _ptr(cent), _ptr(mapping), C.byref(nc),
+                                 _ptr(sizes), _ptr(it)))
+    return {"centroids": cent[:nc.value].copy(), "mapping": mapping[:nc.value].copy(), "sizes": sizes,
+            "iterations": int(it[0]), "balance_iterations": int(it[1])}
+
+
+def router_run(centroids: np.ndarray, mapping: np.ndarray, k: int, queries: np.ndarray, metric: int = L.METRIC_L2,
+               queue_sizes: np.ndarray | None = None, adaptive: bool = True) -> tuple[np.ndarray, np.ndarray]:
+    """QueryRouter::run_routing's region per query (shine_router_run); queue_sizes[b] are the queue sizes at batch
+    boundary b (the last row repeats).  Returns (region per query, limits after the last boundary)."""
+    c = np.ascontiguousarray(centroids, dtype=np.float32)
+    m = np.ascontiguousarray(mapping, dtype=np.uint32)
+    q = np.ascontiguousarray(queries, dtype=np.float32)
+    qs = None if queue_sizes is None else np.ascontiguousarray(queue_sizes, dtype=np.uint32).reshape(-1, k)
+    out = np.empty(q.shape[0], dtype=np.uint32)
+    lim = np.zeros(k, dtype=np.uint64)
+    L.check(L.lib().shine_router_run(_ptr(c), _ptr(m), c.shape[0], k, c.shape[1], metric, _ptr(q), q.shape[0],
+                                     None if qs is None else _ptr(qs), 0 if qs is None else qs.shape[0], int(adaptive),
+                                     _ptr(out), _ptr(lim)))
+    return out, lim
 
 
 def graph_stats(dumps, dim: int, M: int) -> dict:

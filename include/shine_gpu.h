@@ -101,10 +101,11 @@ typedef struct shine_index_info {
  *   the slots like over compute nodes (id % G, read_data.hh:57-58); no collective is on the query path. */
 #define SHINE_PLACE_REPLICA 0
 #define SHINE_PLACE_SHARDED 1
-/* SHARDED_REGIONS: as SHARDED, but GPU slot o owns region o of the space rather than memory nodes: k-means (k = n_gpus)
- *   over the top-level nodes (placement.hh:22-61, kmeans.hh:93-137), every record in its nearest region with at
- *   most 5 % imbalance, and shine_knn_batch routes each query to its nearest region within per-batch limits
- *   (query_router.hh:359-372), so that a search reads mostly its own GPU's HBM. */
+/* SHARDED_REGIONS: as SHARDED, but GPU slot o owns region o of the space rather than memory nodes: balanced k-means
+ *   (k = n_gpus; Kmeans::run_and_optimize, kmeans.hh:24-91) over the top-level nodes (Placement::fetch_level,
+ *   placement.hh:78-106), every record in its closest region with at most 5 % imbalance, and shine_knn_batch routes
+ *   each query to its closest region within per-batch limits that adapt to the slots' queues (QueryRouter,
+ *   query_router.hh:106-151, 280-387), so that a search reads mostly its own GPU's HBM. */
 #define SHINE_PLACE_SHARDED_REGIONS 2
 
 /* Open the index from the memory nodes' dumps `index_m{M}_efc{efC}_node{i}_of{N}.dat`, i = 1..N, in that
@@ -168,15 +169,37 @@ int shine_release_stream(shine_index_t h, void* stream);
 int shine_cache_warmup(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
                        uint32_t ef);
 
-/* The GPU slot each query of a batch is answered on: id % n_gpus, or for SHINE_PLACE_SHARDED_REGIONS the slot of
- * the query's nearest region that still has room in this batch (QueryRouter::run_routing, query_router.hh:280-387).
- * Host-only. */
+/* The GPU slot each query of a batch is answered on: id % n_gpus, or for SHINE_PLACE_SHARDED_REGIONS the slot the
+ * handle's query router picks (QueryRouter::run_routing, query_router.hh:280-387): the closest region whose count in
+ * the current batch of 200 * n_gpus queries (LIMIT_PER_CN, constants.hh:25) is below its limit.  At every batch
+ * boundary the limits are re-derived from the slots' queue sizes (update_limits, query_router.hh:106-151), modelled
+ * from each slot's rate in its last call.  The router's state lives in the handle across calls, as the reference's
+ * router lives for the whole query phase, so this call advances it like a shine_knn_batch would.  Host-only. */
 int shine_route(shine_index_t h, const float* queries, uint32_t nq, uint32_t* out_slot);
 
-/* Host-only planner behind SHINE_PLACE_SHARDED_REGIONS (no device needed): the k region centroids (k x dim, nullable)
- * and the region of every record by uid (region_of_uid[uid], capacity uid_capacity, nullable). */
+/* Host-only planner behind SHINE_PLACE_SHARDED_REGIONS (no device needed): fetch_level(500) + balanced k-means.
+ * centroids (nullable): capacity 2k x dim (k odd: 2k centroids merged in pairs); mapping (nullable, capacity 2k):
+ * region of every centroid; n_centroids (nullable): k or 2k; region_of_uid (nullable): region of every record by
+ * uid, capacity uid_capacity. */
 int shine_plan_regions(const uint8_t* const* dumps, const uint64_t* sizes, uint32_t n_dumps, uint32_t dim, uint32_t M,
-                       int metric, uint32_t k, uint32_t* region_of_uid, uint64_t uid_capacity, float* centroids);
+                       int metric, uint32_t k, uint32_t* region_of_uid, uint64_t uid_capacity, float* centroids,
+                       uint32_t* mapping, uint32_t* n_centroids);
+
+/* Kmeans<Distance> over n rows (kmeans.hh:10-378), host-only: balanced != 0 is run_and_optimize (balanced k-means,
+ * c = 0.15, penalty factor 1.01, max size difference 1; odd k runs 2k clusters and merges the closest pairs),
+ * balanced == 0 is run_kmeans with k clusters.  centroids: capacity 2k x dim; mapping: capacity 2k (centroid ->
+ * region); n_centroids, region_sizes (k; rows per region after balancing) and iterations ([0] Lloyd, [1] balancing)
+ * are nullable.  SHINE_ERR_ARG when n < the number of clusters (the reference asserts). */
+int shine_kmeans(const float* rows, uint64_t n, uint32_t dim, int metric, uint32_t k, int balanced, float* centroids,
+                 uint32_t* mapping, uint32_t* n_centroids, uint64_t* region_sizes, uint32_t* iterations);
+
+/* QueryRouter::run_routing's decisions for a stream of nq queries over the given centroids (host-only): the region
+ * of every query, with BALANCED_ROUTING limits and, when adaptive != 0, update_limits at every boundary of
+ * 200 * k queries from the queue sizes the acks carry: row b of queue_sizes (n_rows x k; the last row repeats;
+ * NULL = all zero, no update) at boundary b.  out_limits (nullable, k): the limits after the last boundary. */
+int shine_router_run(const float* centroids, const uint32_t* mapping, uint32_t n_centroids, uint32_t k, uint32_t dim,
+                     int metric, const float* queries, uint32_t nq, const uint32_t* queue_sizes, uint32_t n_rows,
+                     int adaptive, uint32_t* out_region, uint64_t* out_limits);
 
 /* Batched distance kernel: for query i and its n_per_query node uids node_uids[i*n_per_query + j], write
  * out[i*n_per_query + j] = Distance::dist(q_i, x_uid) (distance.hh:153-161).  Device pointers, async. */

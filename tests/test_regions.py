@@ -1,5 +1,6 @@
 """Region planner of SHINE_PLACE_SHARDED_REGIONS (csrc/placement.cc), host-only: the GPU-node form of the
-reference's Placement / Kmeans (cache/placement.hh:22-72, cache/kmeans.hh:93-137).  Runs without a GPU."""
+reference's Placement / Kmeans (cache/placement.hh:22-106, cache/kmeans.hh:24-377) over real dumps.  The k-means
+itself is checked bitwise against its restatement in test_placement.py.  Runs without a GPU."""
 import numpy as np
 import pytest
 
@@ -18,8 +19,9 @@ def clustered():
 @pytest.mark.parametrize("k", [2, 3, 8])
 def test_regions_are_balanced_and_cover_every_record(clustered, k):
     base, dumps = clustered
-    cent, region = shine_amd.plan_regions(dumps, 128, 8, 0, k)
-    assert cent.shape == (k, 128) and np.isfinite(cent).all()
+    cent, region, mapping = shine_amd.plan_regions(dumps, 128, 8, 0, k)
+    assert cent.shape == (k if k % 2 == 0 else 2 * k, 128) and np.isfinite(cent).all()
+    assert sorted(set(mapping.tolist())) == list(range(k))
     assert region.shape[0] == base.shape[0] and (region < k).all()
     sizes = np.bincount(region, minlength=k)
     assert sizes.max() <= int(np.ceil(base.shape[0] / k * 1.05))  # at most 5 % above an even split
@@ -27,9 +29,9 @@ def test_regions_are_balanced_and_cover_every_record(clustered, k):
 
 def test_regions_follow_the_nearest_centroid(clustered):
     base, dumps = clustered
-    cent, region = shine_amd.plan_regions(dumps, 128, 8, 0, 4)
+    cent, region, mapping = shine_amd.plan_regions(dumps, 128, 8, 0, 4)
     d = ((base[:, None, :] - cent[None, :, :]) ** 2).sum(-1)
-    nearest = d.argmin(1)
+    nearest = mapping[d.argmin(1)]
     # the balance cap moves only a few records away from their nearest region
     assert (nearest == region).mean() > 0.9
 
@@ -40,6 +42,15 @@ def test_planner_is_deterministic(clustered):
     b = shine_amd.plan_regions(dumps, 128, 8, 0, 4)
     np.testing.assert_array_equal(a[0], b[0])
     np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(a[2], b[2])
+
+
+def test_planner_samples_the_top_levels(clustered):
+    """fetch_level(500) (placement.hh:78-106) then balanced k-means: the planner's centroids are shine_kmeans over
+    the same sample, which is the entry point's breadth-first closure from the top level down until >= 500 nodes."""
+    base, dumps = clustered
+    cent, _, mapping = shine_amd.plan_regions(dumps, 128, 8, 0, 3)
+    assert cent.shape[0] == 6 and sorted(set(mapping.tolist())) == [0, 1, 2]
 
 
 def test_unknown_k_is_rejected(clustered):
