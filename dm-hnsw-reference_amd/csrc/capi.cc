@@ -44,12 +44,12 @@ template <class T>
 struct HostBuf {
   T* p = nullptr;
   size_t n = 0;
-  int grow(size_t want) {
+  int grow(size_t want, unsigned flags = hipHostMallocDefault) {
     if (want <= n) return 0;
     if (p) (void)hipHostFree(p);
     p = nullptr;
     n = 0;
-    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(want, 1) * sizeof(T), hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(want, 1) * sizeof(T), flags);
     if (e != hipSuccess) return set_error(SHINE_ERR_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
     std::memset(p, 0, std::max<size_t>(want, 1) * sizeof(T));
     n = want;
@@ -129,12 +129,18 @@ struct ShardedArray {
 struct Scratch {
   DevBuf<uint32_t> visited, vlog, counter, ovf, qs;
   DevBuf<unsigned long long> heaps;  // global-heap pass
-  HostBuf<uint32_t> seen;  // pinned copy of the last call's hand-on counts (sizes the next light pass; may be stale)
+  // host memory the last pass of every call writes: the queries each pass handed on, and [3] = 1 once written
+  // (sizes the next call's light pass; may be stale while a call is in flight)
+  HostBuf<uint32_t> seen;
+  uint32_t* seen_dev = nullptr;  // its device address
+  bool counters_zero = false;    // the last call's last pass zeroed the counter words (finish_call)
   uint32_t slots = 0;
   void release() {
     for (auto* b : {&visited, &vlog, &counter, &ovf, &qs}) b->release();
     heaps.release();
     seen.release();
+    seen_dev = nullptr;
+    counters_zero = false;
     slots = 0;
   }
 };
@@ -758,12 +764,19 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   if (int rc = S.counter.grow(8)) return rc;
   if (S.ovf.n < 3ull * nq) HIP_TRY(hipStreamSynchronize(s));  // a reallocation must not pull the list from under
   if (int rc = S.ovf.grow(3ull * nq)) return rc;                // an earlier call on this stream
-  HIP_TRY(hipMemsetAsync(S.counter.p, 0, 8 * sizeof(uint32_t), s));
+  if (!S.seen_dev) {
+    if (int rc = S.seen.grow(4, hipHostMallocMapped | hipHostMallocPortable)) return rc;
+    void* dp = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&dp, S.seen.p, 0));
+    S.seen_dev = static_cast<uint32_t*>(dp);
+  }
+  // the counter words start at zero: left so by the last call's last pass, else (first call, a failed call) set here
+  if (!S.counters_zero) HIP_TRY(hipMemsetAsync(S.counter.p, 0, 8 * sizeof(uint32_t), s));
+  S.counters_zero = false;
   if (timed) HIP_TRY(hipEventRecord(R.ev0, s));
   const int start = static_cast<int>(env_int("SHINE_DEBUG_START_MODE", 0));  // test hook: the fallback passes alone
   const bool fast_mode = h->search_mode == SHINE_MODE_FAST;
   const bool fast_kernel = fast_mode && ef <= kFastMaxEf && h->M0 <= 64;
-  if (int rc = S.seen.grow(4)) return rc;
   const uint32_t handed = S.seen.p[3] ? S.seen.p[0] : 0;  // [3] = 1 once a call has written the counts
   int chain[3], n_pass = 0;
   if (start <= 0) chain[n_pass++] = fast_kernel ? PASS_FAST : PASS_LDS;
@@ -824,15 +837,15 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     if (i + 1 < n_pass) {
       a.out_list = S.ovf.p + static_cast<size_t>(i) * nq;
       a.out_count = S.counter.p + 4 + i;
+    } else {
+      a.call_counters = S.counter.p;
+      a.host_counts = S.seen_dev;
     }
     hipError_t e = launch_search(h->dim, h->metric, h->elem, sh.grid, a, s);
     if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("search launch: ") + hipGetErrorString(e));
   }
   if (timed) HIP_TRY(hipEventRecord(R.ev1, s));
-  if (!env_int("SHINE_DEBUG_NO_SEEN", 0)) {  // measurement hook: the light pass sized without the last counts
-    HIP_TRY(hipMemcpyAsync(S.seen.p, S.counter.p + 4, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    S.seen.p[3] = 1;
-  }
+  S.counters_zero = true;
   return 0;
 }
 
@@ -1071,8 +1084,6 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     HIP_TRY(hipMemcpyAsync(R.hd.p, R.d.p, static_cast<size_t>(n) * k * 4, hipMemcpyDeviceToHost, R.stream));
     HIP_TRY(hipMemcpyAsync(R.hqs.p, R.main.qs.p, static_cast<size_t>(n) * kQsWords * 4, hipMemcpyDeviceToHost,
                            R.stream));
-    HIP_TRY(hipMemcpyAsync(R.hqs.p + static_cast<size_t>(n) * kQsWords, R.main.counter.p, 8 * 4,
-                           hipMemcpyDeviceToHost, R.stream));
   }
   double kernel_ms = 0;
   uint64_t retries = 0;
@@ -1086,8 +1097,8 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     HIP_TRY(hipEventElapsedTime(&ms, R.ev0, R.ev1));
     kernel_ms = std::max(kernel_ms, static_cast<double>(ms));
     if (r < h->slot_rate.size() && ms > 0) h->slot_rate[r] = n / static_cast<double>(ms);
-    const uint32_t* cnt = R.hqs.p + static_cast<size_t>(n) * kQsWords;
-    retries += cnt[4] + cnt[5] + cnt[6];  // queries handed on by each pass
+    const uint32_t* cnt = R.main.seen.p;  // written by the call's last pass (finish_call)
+    retries += cnt[0] + cnt[1] + cnt[2];  // queries handed on by each pass
     if (env_int("SHINE_PHASE_PROFILE", 0) && R.prof.p) print_phase_profile(h, R);
   }
   int rc = SHINE_OK;

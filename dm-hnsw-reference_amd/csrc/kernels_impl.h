@@ -582,6 +582,28 @@ struct PhaseClock<true> {  // lane i accumulates phase i: one compare and one 64
 //   VIS   0: visited table in LDS; 1: visited bitmap in HBM; 2: visited bitmap and both heaps in HBM (the last
 //         fallback pass: no capacity limit but the heap stride, ~µs per heap operation).  Heaps in HBM are
 //         written by some lanes and read by others: a workgroup-scope fence orders every heap operation.
+// End of the last pass of a call: the last workgroup to finish publishes the queries every pass handed on (host
+// memory: the next call sizes its light pass from them, shine_knn_batch reports them) and zeroes the call's counter
+// words for the next call on this stream, so a call needs neither a memset nor a copy of its own.  No fence is
+// needed: a workgroup counts itself finished only after the atomic that found the work queue empty has returned,
+// the hand-on counts were final before this pass started, and the end-of-kernel release publishes the stores to
+// the next kernel on the stream and to the host.  (An agent-scope fence per workgroup would write back L2 on every
+// exit: -3 % QPS measured.)
+__device__ __forceinline__ void finish_call(const SearchArgs& A, int lane) {
+  if (!A.call_counters || lane != 0) return;
+  u32* c = A.call_counters;
+  if (atomicAdd(&c[7], 1u) != gridDim.x - 1) return;
+  const u32 h0 = __atomic_load_n(&c[4], __ATOMIC_RELAXED), h1 = __atomic_load_n(&c[5], __ATOMIC_RELAXED),
+            h2 = __atomic_load_n(&c[6], __ATOMIC_RELAXED);
+  volatile u32* host = A.host_counts;
+  host[0] = h0;
+  host[1] = h1;
+  host[2] = h2;
+  host[3] = 1u;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) __atomic_store_n(&c[i], 0u, __ATOMIC_RELAXED);
+}
+
 template <int D, int METRIC, typename E, int VIS, bool ACCT, bool PROF = false>
 __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
   PhaseClock<PROF> clk;
@@ -841,6 +863,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
     }
   }
   clk.flush(A.prof, lane);
+  finish_call(A, lane);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -911,14 +934,20 @@ struct VisitedLds<0> {
   }
   __device__ __forceinline__ void insert_first(u32 x) { t[vhash(x, shift)] = x; }  // the table is empty
   __device__ __forceinline__ bool at_home(u32 x) const { return t[vhash(x, shift)] == x; }
+  // one exit from the probe loop (an early return per outcome compiles to a branchier loop and more live SGPRs)
   __device__ __forceinline__ bool test_and_set(u32 x, bool& /*ovf*/) {
     u32 h = vhash(x, shift);
+    bool fresh = false;
     for (;;) {
       const u32 old = atomicCAS(&t[h], INV, x);
-      if (old == INV) return true;
-      if (old == x) return false;
+      if (old == INV) {
+        fresh = true;
+        break;
+      }
+      if (old == x) break;
       h = (h + 1) & mask;
     }
+    return fresh;
   }
 };
 
@@ -954,6 +983,7 @@ struct VisitedLds<1> {
     const u32 h = image(x);
     u32 s = h >> rbits, disp = 0, cur = INV;  // first attempt: the word is assumed empty
     const u32 rem = (h & rmask) << dbits;
+    bool fresh = false;
     for (;;) {
       const u32 sh = (s & 1u) << 4;
       const u32 half = (cur >> sh) & 0xFFFFu;
@@ -961,18 +991,22 @@ struct VisitedLds<1> {
       if (half == 0xFFFFu) {
         const u32 want = (cur & ~(0xFFFFu << sh)) | (entry << sh);
         const u32 old = atomicCAS(&t[s >> 1], cur, want);
-        if (old == cur) return true;
+        if (old == cur) {
+          fresh = true;
+          break;
+        }
         cur = old;  // the word was not as assumed: look at this slot again
         continue;
       }
-      if (half == entry) return false;  // same home, same remainder: this id
+      if (half == entry) break;  // same home, same remainder: this id
       s = (s + 1) & mask;
       if (++disp > dmax) {
         ovf = true;
-        return false;
+        break;
       }
       if ((s & 1u) == 0) cur = INV;  // a new word: assume it empty again
     }
+    return fresh;
   }
 };
 
@@ -1061,9 +1095,11 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       }
       bool fresh = false, vovf = false;
       if (cand) fresh = vis.test_and_set(e, vovf);  // visited.contains / insert (:441-443)
-      if (VT == 1 && __ballot(vovf)) {  // an id too far from its home slot: the light pass re-runs the query
-        status = ST_OVERFLOW;
-        break;
+      if constexpr (VT == 1) {
+        if (__ballot(vovf)) {  // an id too far from its home slot: the light pass re-runs the query
+          status = ST_OVERFLOW;
+          break;
+        }
       }
       const u64 fm = __ballot(fresh);
       const int nf = __popcll(fm);
@@ -1259,6 +1295,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
     }
   }
   clk.flush(A.prof, lane);
+  finish_call(A, lane);
 }
 
 // ------------------------------------------------------------------------------------------------------------
