@@ -629,6 +629,12 @@ uint32_t pow2_at_least(uint32_t x) {
   return p;
 }
 
+uint32_t log2_ceil(uint32_t x) {
+  uint32_t l = 0;
+  while ((1u << l) < x) ++l;
+  return l;
+}
+
 int64_t env_int(const char* name, int64_t dflt) {
   const char* e = std::getenv(name);
   return e ? std::atoll(e) : dflt;
@@ -706,11 +712,23 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
   uint32_t wpc = 1;
   uint64_t budget = lds;
   if (pass == PASS_LDS) {
+    // u16 quotient entries (VisitedLds<1>) when the id space fits them and they let more wavefronts share a CU with
+    // next_candidates still >= 5·ef entries (u32: 4·ef)
     sh.vis_cap = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(48 * ef)));
-    const uint64_t need = search_lds_bytes(ef, 4 * ef, sh.vis_cap);
-    const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(lds / need));
-    wpc = std::max<uint32_t>(1, std::min<uint32_t>({(nq + cus - 1) / cus, 16u, fit}));
     sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
+    // aim at the wavefronts of two batches in flight being resident together, as pick_fast_shape does
+    const uint32_t want = std::min<uint32_t>(2 * ((nq + cus - 1) / cus), 16u);
+    auto waves = [&](uint64_t need) {
+      return std::max<uint32_t>(1, std::min<uint32_t>(want, static_cast<uint32_t>(lds / need)));
+    };
+    const uint32_t w32 = waves(search_lds_bytes(ef, 4 * ef, sh.vis_cap, 4));
+    const uint32_t w16 = waves(search_lds_bytes(ef, 5 * ef, sh.vis_cap, 2));
+    uint32_t bits = 14;
+    while (bits < 32 && (1ull << bits) < h->id_space) ++bits;
+    const bool can16 = env_int("SHINE_DEBUG_VIS16", 1) != 0 && bits <= log2_ceil(sh.vis_cap) + 11;
+    sh.vis16 = can16 && (w16 > w32 || env_int("SHINE_DEBUG_VIS16", -1) == 1) ? 1 : 0;
+    sh.vis_bits = std::max(bits, log2_ceil(sh.vis_cap) + 1);
+    wpc = sh.vis16 ? w16 : w32;
     budget = (lds / wpc) & ~15u;
   } else if (pass == PASS_WHOLE_CU) {
     sh.vis_cap = 16384;
@@ -719,7 +737,8 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
     budget = kLightFixupLds;
     wpc = static_cast<uint32_t>(env_int("SHINE_DEBUG_LIGHT_WPC", std::max<uint32_t>(1, static_cast<uint32_t>(lds / kLightFixupLds))));
   }
-  const int64_t cap = (static_cast<int64_t>(budget) - static_cast<int64_t>(top_bytes) - 4ll * sh.vis_cap - 512) / 8;
+  const int64_t vis_bytes = static_cast<int64_t>(align16((sh.vis16 ? 2ull : 4ull) * sh.vis_cap));
+  const int64_t cap = (static_cast<int64_t>(budget) - static_cast<int64_t>(top_bytes) - vis_bytes - 512) / 8;
   sh.cap = static_cast<uint32_t>(std::max<int64_t>(cap & ~1ll, 2));
   if (pass == PASS_LDS) sh.cap = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_DEBUG_CAP", sh.cap)));
   if (pass == PASS_LIGHT) sh.cap = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_DEBUG_LIGHT_CAP", sh.cap)));

@@ -56,7 +56,7 @@ struct SearchArgs {
   uint32_t fast;            // 1: sorted-list kernel (SHINE_MODE_FAST; ef <= kFastMaxEf, vis_cap > 0)
   uint32_t sort_out;        // heap kernel writes ascending order (fast-mode fixup passes)
   uint32_t global_heaps;    // 1: heap kernel with both heaps in HBM (last fallback pass; vis_cap must be 0)
-  uint32_t vis16;           // fast kernel: u16 quotient visited entries (kernels_impl.h VisitedLds<1>)
+  uint32_t vis16;           // LDS visited table of u16 quotient entries (kernels_impl.h VisitedLds<1>)
   uint32_t vis_bits;        // ... bits of the id space the multiply permutes (vis_bits - log2(vis_cap) <= 11)
   uint32_t vis_mul;         // ... odd multiplier
 };
@@ -70,10 +70,11 @@ struct DistArgs {
   float* out;                 // [nq][n_per]
 };
 
-// LDS layout of a search workgroup: top[ef] | next[cap] | visited table[vis_cap] | scratch ids[64], dists[64]
+// LDS layout of a search workgroup: top[ef] | next[cap] | visited table[vis_cap] (entry_bytes each) | scratch
+// ids[64], dists[64]
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
-inline size_t search_lds_bytes(uint32_t ef, uint32_t cap, uint32_t vis_cap) {
-  return align16(8ull * ef) + align16(8ull * cap) + 4ull * vis_cap + 64 * 4 * 2;
+inline size_t search_lds_bytes(uint32_t ef, uint32_t cap, uint32_t vis_cap, uint32_t entry_bytes = 4) {
+  return align16(8ull * ef) + align16(8ull * cap) + align16(static_cast<size_t>(entry_bytes) * vis_cap) + 64 * 4 * 2;
 }
 
 // LDS of the fast kernel: visited table[vis_cap] (entry_bytes each) | scratch ids[64], dists[64] | merge scratch

@@ -582,6 +582,108 @@ struct PhaseClock<true> {  // lane i accumulates phase i: one compare and one 64
 //   VIS   0: visited table in LDS; 1: visited bitmap in HBM; 2: visited bitmap and both heaps in HBM (the last
 //         fallback pass: no capacity limit but the heap stride, ~µs per heap operation).  Heaps in HBM are
 //         written by some lanes and read by others: a workgroup-scope fence orders every heap operation.
+// ------------------------------------------------------------------------------------------------------------
+// Exact visited set (hashset_t<RemotePtr>, types.hh:14-15) in the wave's LDS share (fast kernel; exact kernel VIS 0).
+//   VT = 0: u32 keys, linear probing from a multiplicative hash (4 B per entry).
+//   VT = 1: u16 quotient entries (2 B per entry): an odd multiply permutes the b-bit id space, the top t bits of
+//           the image pick the home slot, and the entry keeps the other b - t bits plus the slot's distance from
+//           home, so (slot, entry) names the id exactly.  Two entries share a 32-bit word; inserts are word-wide
+//           compare-and-swaps whose first attempt assumes an empty word (one LDS round trip when it is).  Half the
+//           LDS per wave lets two batches of 1,024 queries hold all their wavefronts on the CUs at once.  An id
+//           that would land farther than 2^(16-(b-t)) - 2 slots from home stops the query (light pass re-runs it).
+// ------------------------------------------------------------------------------------------------------------
+template <int VT>
+struct VisitedLds;
+
+template <>
+struct VisitedLds<0> {
+  u32* t;
+  u32 mask, shift;
+  __device__ __forceinline__ VisitedLds(void* base, const SearchArgs& A)
+      : t(static_cast<u32*>(base)), mask(A.vis_cap - 1), shift(32 - (31 - __clz(static_cast<int>(A.vis_cap)))) {}
+  static constexpr u32 kBytes = 4;
+  __device__ __forceinline__ void clear(const SearchArgs& A, int lane) {
+    uint4* t4 = reinterpret_cast<uint4*>(t);
+    for (u32 i = lane; i < A.vis_cap / 4; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
+  }
+  __device__ __forceinline__ void insert_first(u32 x) { t[vhash(x, shift)] = x; }  // the table is empty
+  __device__ __forceinline__ bool at_home(u32 x) const { return t[vhash(x, shift)] == x; }
+  // one exit from the probe loop (an early return per outcome compiles to a branchier loop and more live SGPRs)
+  __device__ __forceinline__ bool test_and_set(u32 x, bool& /*ovf*/) {
+    u32 h = vhash(x, shift);
+    bool fresh = false;
+    for (;;) {
+      const u32 old = atomicCAS(&t[h], INV, x);
+      if (old == INV) {
+        fresh = true;
+        break;
+      }
+      if (old == x) break;
+      h = (h + 1) & mask;
+    }
+    return fresh;
+  }
+};
+
+template <>
+struct VisitedLds<1> {
+  u32* t;
+  unsigned short* t16;
+  u32 mask, mul, bmask, rbits, rmask, dbits, dmax;
+  __device__ __forceinline__ VisitedLds(void* base, const SearchArgs& A)
+      : t(static_cast<u32*>(base)), t16(static_cast<unsigned short*>(base)), mask(A.vis_cap - 1), mul(A.vis_mul) {
+    const u32 tb = 31 - __clz(static_cast<int>(A.vis_cap));
+    bmask = A.vis_bits >= 32 ? ~0u : (1u << A.vis_bits) - 1;
+    rbits = A.vis_bits - tb;
+    rmask = (1u << rbits) - 1;
+    dbits = 16 - rbits;
+    dmax = (1u << dbits) - 2;  // an all-ones entry is the empty marker
+  }
+  static constexpr u32 kBytes = 2;
+  __device__ __forceinline__ void clear(const SearchArgs& A, int lane) {
+    uint4* t4 = reinterpret_cast<uint4*>(t);
+    for (u32 i = lane; i < A.vis_cap / 8; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
+  }
+  __device__ __forceinline__ u32 image(u32 x) const { return (x * mul) & bmask; }
+  __device__ __forceinline__ void insert_first(u32 x) {
+    const u32 h = image(x);
+    t16[h >> rbits] = static_cast<unsigned short>((h & rmask) << dbits);
+  }
+  __device__ __forceinline__ bool at_home(u32 x) const {
+    const u32 h = image(x);
+    return t16[h >> rbits] == static_cast<unsigned short>((h & rmask) << dbits);
+  }
+  __device__ __forceinline__ bool test_and_set(u32 x, bool& ovf) {
+    const u32 h = image(x);
+    u32 s = h >> rbits, disp = 0, cur = INV;  // first attempt: the word is assumed empty
+    const u32 rem = (h & rmask) << dbits;
+    bool fresh = false;
+    for (;;) {
+      const u32 sh = (s & 1u) << 4;
+      const u32 half = (cur >> sh) & 0xFFFFu;
+      const u32 entry = rem | disp;
+      if (half == 0xFFFFu) {
+        const u32 want = (cur & ~(0xFFFFu << sh)) | (entry << sh);
+        const u32 old = atomicCAS(&t[s >> 1], cur, want);
+        if (old == cur) {
+          fresh = true;
+          break;
+        }
+        cur = old;  // the word was not as assumed: look at this slot again
+        continue;
+      }
+      if (half == entry) break;  // same home, same remainder: this id
+      s = (s + 1) & mask;
+      if (++disp > dmax) {
+        ovf = true;
+        break;
+      }
+      if ((s & 1u) == 0) cur = INV;  // a new word: assume it empty again
+    }
+    return fresh;
+  }
+};
+
 // End of the last pass of a call: the last workgroup to finish publishes the queries every pass handed on (host
 // memory: the next call sizes its light pass from them, shine_knn_batch reports them) and zeroes the call's counter
 // words for the next call on this stream, so a call needs neither a memset nor a copy of its own.  No fence is
@@ -604,7 +706,7 @@ __device__ __forceinline__ void finish_call(const SearchArgs& A, int lane) {
   for (int i = 0; i < 8; ++i) __atomic_store_n(&c[i], 0u, __ATOMIC_RELAXED);
 }
 
-template <int D, int METRIC, typename E, int VIS, bool ACCT, bool PROF = false>
+template <int D, int METRIC, typename E, int VIS, bool ACCT, int VT = 0, bool PROF = false>
 __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
   PhaseClock<PROF> clk;
   clk.start();
@@ -615,8 +717,9 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
                               : nullptr;
   u64* top = VIS == 2 ? gheap : reinterpret_cast<u64*>(smem);                   // MaxHeap top_candidates
   u64* nxt = VIS == 2 ? gheap + top_b / 8 : reinterpret_cast<u64*>(smem + top_b);  // MinHeap next_candidates
-  u32* vtab = reinterpret_cast<u32*>(VIS == 2 ? smem : smem + top_b + next_b);  // visited table (VIS = 0)
-  u32* sc_ids = vtab + (VIS == 0 ? A.vis_cap : 0u);            // fresh neighbours
+  unsigned char* vbase = VIS == 2 ? smem : smem + top_b + next_b;  // visited table (VIS = 0)
+  VisitedLds<VT> vt(vbase, A);
+  u32* sc_ids = reinterpret_cast<u32*>(vbase + (VIS == 0 ? A.vis_cap * VisitedLds<VT>::kBytes : 0u));  // fresh ids
   float* sc_d = reinterpret_cast<float*>(sc_ids + 64);
   auto hfence = []() {
     if constexpr (VIS == 2) __threadfence_block();
@@ -625,7 +728,6 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
   const int lane = threadIdx.x;
   const E* __restrict__ vec = static_cast<const E*>(A.g.vec);
   const u32 M0 = A.g.M0;
-  const u32 vmask = A.vis_cap - 1, vshift = 32 - (31 - __clz(static_cast<int>(A.vis_cap > 1 ? A.vis_cap : 2)));
   u32* __restrict__ vis = A.visited + (VIS >= 1 ? static_cast<u64>(blockIdx.x) * A.words_per_slot : 0ull);
   u32* __restrict__ vlog = A.vlog + (VIS >= 1 ? static_cast<u64>(blockIdx.x) * A.log_cap : 0ull);
   const u64 below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));  // lanes < this one
@@ -641,10 +743,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
     PHASE(0)
     QueryRegs<D> Q;
     load_query<D>(A.queries + static_cast<u64>(qi) * D, lane, Q);
-    if (VIS == 0) {  // visited_nodes.clear()  (:475) — done up front for this query
-      uint4* t4 = reinterpret_cast<uint4*>(vtab);
-      for (u32 i = lane; i < A.vis_cap / 4; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
-    }
+    if (VIS == 0) vt.clear(A, lane);  // visited_nodes.clear()  (:475) — done up front for this query
 
     u32 st_dist = 0, st_vup = 0, st_vl0 = 0, st_lup = 0, st_ll0 = 0, st_maxnext = 0, status = 0;
     ReadCount rc;
@@ -668,7 +767,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         top[0] = troot;
         nxt[0] = troot;  // search_level :412-415
         if (VIS == 0) {
-          vtab[vhash(nn, vshift)] = nn;  // table is empty: the first probe slot is free
+          vt.insert_first(nn);  // table is empty: the first probe slot is free
         } else {
           atomicOr(&vis[nn >> 5], 1u << (nn & 31));
           vlog[0] = nn;
@@ -709,16 +808,10 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
             if (j < static_cast<u32>(lane) && ej == e) cand = false;
           }
         }
-        bool fresh = false;
+        bool fresh = false, vovf = false;
         if (cand) {  // visited.contains / insert (:441-443)
           if (VIS == 0) {
-            u32 h = vhash(e, vshift);
-            for (;;) {
-              const u32 old = atomicCAS(&vtab[h], INV, e);
-              if (old == INV) { fresh = true; break; }
-              if (old == e) break;
-              h = (h + 1) & vmask;
-            }
+            fresh = vt.test_and_set(e, vovf);
           } else {
             const u32 bit = 1u << (e & 31);
             fresh = (atomicOr(&vis[e >> 5], bit) & bit) == 0;
@@ -741,6 +834,9 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         st_vl0 += nf;
         st_dist += nf;
         if (VIS == 0 && nvis > A.vis_limit) { status = ST_OVERFLOW; break; }
+        if constexpr (VIS == 0 && VT == 1) {
+          if (__ballot(vovf)) { status = ST_OVERFLOW; break; }  // an id too far from its home slot
+        }
         if (nf == 0) continue;
         PHASE(4)
         wave_sync();
@@ -907,108 +1003,6 @@ __device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restri
 #pragma unroll
   for (int p = 0; p < P; ++p) issue_pass_u<D, E, P>(B, p, vec, sid[p], pad, c4);
 }
-
-// ------------------------------------------------------------------------------------------------------------
-// Exact visited set of the fast kernel (hashset_t<RemotePtr>, types.hh:14-15) in the wave's LDS share.
-//   VT = 0: u32 keys, linear probing from a multiplicative hash (4 B per entry).
-//   VT = 1: u16 quotient entries (2 B per entry): an odd multiply permutes the b-bit id space, the top t bits of
-//           the image pick the home slot, and the entry keeps the other b - t bits plus the slot's distance from
-//           home, so (slot, entry) names the id exactly.  Two entries share a 32-bit word; inserts are word-wide
-//           compare-and-swaps whose first attempt assumes an empty word (one LDS round trip when it is).  Half the
-//           LDS per wave lets two batches of 1,024 queries hold all their wavefronts on the CUs at once.  An id
-//           that would land farther than 2^(16-(b-t)) - 2 slots from home stops the query (light pass re-runs it).
-// ------------------------------------------------------------------------------------------------------------
-template <int VT>
-struct VisitedLds;
-
-template <>
-struct VisitedLds<0> {
-  u32* t;
-  u32 mask, shift;
-  __device__ __forceinline__ VisitedLds(void* base, const SearchArgs& A)
-      : t(static_cast<u32*>(base)), mask(A.vis_cap - 1), shift(32 - (31 - __clz(static_cast<int>(A.vis_cap)))) {}
-  static constexpr u32 kBytes = 4;
-  __device__ __forceinline__ void clear(const SearchArgs& A, int lane) {
-    uint4* t4 = reinterpret_cast<uint4*>(t);
-    for (u32 i = lane; i < A.vis_cap / 4; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
-  }
-  __device__ __forceinline__ void insert_first(u32 x) { t[vhash(x, shift)] = x; }  // the table is empty
-  __device__ __forceinline__ bool at_home(u32 x) const { return t[vhash(x, shift)] == x; }
-  // one exit from the probe loop (an early return per outcome compiles to a branchier loop and more live SGPRs)
-  __device__ __forceinline__ bool test_and_set(u32 x, bool& /*ovf*/) {
-    u32 h = vhash(x, shift);
-    bool fresh = false;
-    for (;;) {
-      const u32 old = atomicCAS(&t[h], INV, x);
-      if (old == INV) {
-        fresh = true;
-        break;
-      }
-      if (old == x) break;
-      h = (h + 1) & mask;
-    }
-    return fresh;
-  }
-};
-
-template <>
-struct VisitedLds<1> {
-  u32* t;
-  unsigned short* t16;
-  u32 mask, mul, bmask, rbits, rmask, dbits, dmax;
-  __device__ __forceinline__ VisitedLds(void* base, const SearchArgs& A)
-      : t(static_cast<u32*>(base)), t16(static_cast<unsigned short*>(base)), mask(A.vis_cap - 1), mul(A.vis_mul) {
-    const u32 tb = 31 - __clz(static_cast<int>(A.vis_cap));
-    bmask = A.vis_bits >= 32 ? ~0u : (1u << A.vis_bits) - 1;
-    rbits = A.vis_bits - tb;
-    rmask = (1u << rbits) - 1;
-    dbits = 16 - rbits;
-    dmax = (1u << dbits) - 2;  // an all-ones entry is the empty marker
-  }
-  static constexpr u32 kBytes = 2;
-  __device__ __forceinline__ void clear(const SearchArgs& A, int lane) {
-    uint4* t4 = reinterpret_cast<uint4*>(t);
-    for (u32 i = lane; i < A.vis_cap / 8; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
-  }
-  __device__ __forceinline__ u32 image(u32 x) const { return (x * mul) & bmask; }
-  __device__ __forceinline__ void insert_first(u32 x) {
-    const u32 h = image(x);
-    t16[h >> rbits] = static_cast<unsigned short>((h & rmask) << dbits);
-  }
-  __device__ __forceinline__ bool at_home(u32 x) const {
-    const u32 h = image(x);
-    return t16[h >> rbits] == static_cast<unsigned short>((h & rmask) << dbits);
-  }
-  __device__ __forceinline__ bool test_and_set(u32 x, bool& ovf) {
-    const u32 h = image(x);
-    u32 s = h >> rbits, disp = 0, cur = INV;  // first attempt: the word is assumed empty
-    const u32 rem = (h & rmask) << dbits;
-    bool fresh = false;
-    for (;;) {
-      const u32 sh = (s & 1u) << 4;
-      const u32 half = (cur >> sh) & 0xFFFFu;
-      const u32 entry = rem | disp;
-      if (half == 0xFFFFu) {
-        const u32 want = (cur & ~(0xFFFFu << sh)) | (entry << sh);
-        const u32 old = atomicCAS(&t[s >> 1], cur, want);
-        if (old == cur) {
-          fresh = true;
-          break;
-        }
-        cur = old;  // the word was not as assumed: look at this slot again
-        continue;
-      }
-      if (half == entry) break;  // same home, same remainder: this id
-      s = (s + 1) & mask;
-      if (++disp > dmax) {
-        ovf = true;
-        break;
-      }
-      if ((s & 1u) == 0) cur = INV;  // a new word: assume it empty again
-    }
-    return fresh;
-  }
-};
 
 template <int D, int METRIC, typename E, int R, int P, bool ACCT, int VT, bool PROF = false>
 __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
@@ -1376,7 +1370,7 @@ __global__ __launch_bounds__(64) void heap_replay_kernel(const int32_t* ops, con
 
 template <int D, int METRIC, typename E, bool AC>
 hipError_t launch_search_acct(uint32_t grid, const SearchArgs& a, hipStream_t s) {
-  const size_t lds = search_lds_bytes(a.ef, a.cap, a.vis_cap);
+  const size_t lds = search_lds_bytes(a.ef, a.cap, a.vis_cap, a.vis16 && a.vis_cap > 0 ? 2 : 4);
   auto run = [&](auto kern) -> hipError_t {
     if (lds > 65536) {  // beyond the default dynamic-LDS limit: opt in (per device, so every launch)
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -1417,14 +1411,14 @@ hipError_t launch_search_acct(uint32_t grid, const SearchArgs& a, hipStream_t s)
     return a.vis16 ? pick(std::integral_constant<int, 1>{}) : pick(std::integral_constant<int, 0>{});
   }
   if constexpr (!AC && D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
-    if (a.prof && a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0, AC, true>);
+    if (a.prof && a.vis_cap > 0 && !a.vis16) return run(search_kernel<D, METRIC, E, 0, AC, 0, true>);
   }
   if (a.global_heaps) {  // both heaps in HBM: only the scratch ids / distances stay in LDS
     if (a.vis_cap != 0 || !a.heaps || a.heap_stride < align16(8ull * a.ef) / 8 + a.cap) return hipErrorInvalidValue;
     hipLaunchKernelGGL((search_kernel<D, METRIC, E, 2, AC>), dim3(grid), dim3(64), 64 * 4 * 2, s, a);
     return hipGetLastError();
   }
-  if (a.vis_cap > 0) return run(search_kernel<D, METRIC, E, 0, AC>);
+  if (a.vis_cap > 0) return a.vis16 ? run(search_kernel<D, METRIC, E, 0, AC, 1>) : run(search_kernel<D, METRIC, E, 0, AC, 0>);
   return run(search_kernel<D, METRIC, E, 1, AC>);
 }
 

@@ -53,6 +53,27 @@ def test_knn_parity(case, gpu_available):
     _check_same(r, *case["ref"])
 
 
+def test_knn_parity_u16_visited(case, gpu_available, monkeypatch):
+    """The exact kernel with the u16 quotient visited table (VisitedLds<1>; chosen on large batches, where it lets
+    more wavefronts share a CU), forced here on every case: same bar."""
+    monkeypatch.setenv("SHINE_DEBUG_VIS16", "1")
+    with shine_amd.Index.from_buffers(case["dumps"], case["dim"], case["M"], case["metric"], gpus=[0]) as idx:
+        r = idx.knn(case["q"], case["k"], case["ef"])
+    _check_same(r, *case["ref"])
+
+
+def test_exact_large_batch_picks_u16_and_matches(gpu_available):
+    """2,048 queries want 8 wavefronts per CU: the u16 table (7 fit) beats the u32 one (4 fit), so the exact pass
+    runs VisitedLds<1> without any hook.  Every query must still match the oracle bitwise."""
+    base = D.sift_like(20000, seed=41)
+    q = D.sift_like(2048, seed=42)
+    dumps, _ = shine_amd.build(base, 16, 100, 0, 1, seed=6, threads=8)
+    ref = O.OracleIndex(dumps, 128, 16, 0).knn(q, 10, 128)
+    with shine_amd.Index.from_buffers(dumps, 128, 16, 0, gpus=[0]) as idx:
+        r = idx.knn(q, 10, 128)
+    _check_same(r, *ref)
+
+
 def test_knn_device_entry(case, gpu_available):
     import torch
     q = torch.from_numpy(case["q"]).cuda()

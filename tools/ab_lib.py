@@ -37,6 +37,7 @@ def main():
     p.add_argument("--reps", type=int, default=5)
     p.add_argument("--inflight", type=int, default=2)
     p.add_argument("--n", type=int, default=1_000_000)
+    p.add_argument("--mode", default="fast", choices=["fast", "exact"])
     p.add_argument("--cache", default=os.environ.get("SHINE_BENCH_CACHE", "/tmp/shine_bench"))
     a = p.parse_args()
     import torch
@@ -64,7 +65,7 @@ def main():
         gpu = (C.c_int * 1)(0)
         if lib.shine_open(cp, 1, 128, 16, shine_amd.METRIC_L2, 0, gpu, 1, C.byref(h)) != 0:
             raise SystemExit(f"{path}: {lib.shine_last_error()}")
-        if lib.shine_set_search_mode(h, shine_amd.MODE_FAST) != 0:
+        if lib.shine_set_search_mode(h, shine_amd.MODE_FAST if a.mode == "fast" else shine_amd.MODE_EXACT) != 0:
             raise SystemExit(f"{path}: {lib.shine_last_error()}")
         envd = dict(kv.split("=", 1) for kv in env.split(";") if kv)
         ids = torch.empty((a.nbatches, a.batch, 10), dtype=torch.int32, device="cuda")

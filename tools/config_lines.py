@@ -10,6 +10,7 @@ events.  One JSON line per workload and search mode is printed and appended to -
            ef=250 (scripts/datasets.py: TTI reaches ~95 % at 250) (configs[4]; N reduced from 50M, one GPU)
   sharded  the bench's SIFT-shaped L2 index as 4 memory-node dumps under SHINE_PLACE_SHARDED over GPU slots [0, 0]
            (one physical GPU: both stripes are local, so this checks the layout's cost, not xGMI)
+  cfg5skew cfg5's cache-size-and-skew grid on the sharded layout: hit rate before / after a cache warmup per alpha
 
 Usage: python tools/config_lines.py [--which cfg3,cfg5,sharded] [--n 1000000] [--steps 10]
 """
@@ -184,6 +185,66 @@ def run(name, a):
     return lines
 
 
+def run_skew(a):
+    """cfg5's skew experiment (scripts/exp_cache_size_and_skew.py: Zipf alpha 0-1.5, cache 5 % of the index) on the
+    sharded layout: the TTI-shaped fp16 index as 8 memory-node dumps over 8 GPU slots (repeated device ids on a
+    one-GPU box: every stripe is a separate allocation, so the read classes are exact, but all reads are local HBM),
+    a 5 % cache fraction, and per alpha: a fresh open, the static (in-degree) ranking's hit rate, a cache warmup
+    on the warmup split (shine_cache_warmup), then the measured split's hit rate and remote-read share.  Results
+    must not change with the layout: recall is reported for both."""
+    import torch
+    import shine_amd
+    from shine_amd import datasets as D
+    gen, dim, metric, elem, M, efc, ef, shards = "tti_like", 200, 1, 1, 16, 200, 250, 8
+    n = a.n
+    key = hashlib.sha1(f"{n}-{dim}-{M}-{efc}-{shards}-{gen}-v1".encode()).hexdigest()[:12]
+    cache = Path(a.cache) / key
+    base = getattr(D, gen)(n, seed=1, d=dim)
+    paths = [cache / shine_amd.dump_name(M, efc, i, shards) for i in range(shards)]
+    if not all(p.exists() for p in paths):
+        with Heartbeat(f"skew: building {n} x {dim}"):
+            dumps, _ = shine_amd.build(base, M, efc, metric, shards, seed=1234, threads=host_threads())
+        cache.mkdir(parents=True, exist_ok=True)
+        for p, d in zip(paths, dumps):
+            d.tofile(p)
+        del dumps
+    pool = getattr(D, gen)(20_000, seed=2, d=dim)
+    base_t = torch.from_numpy(base).cuda()
+    lines = []
+    for alpha in [float(x) for x in a.alphas.split(",")]:
+        q, warm, _ = D.zipf_query_mix(pool, 3 * 1024, alpha, split=1024, seed=9)
+        q, warm = np.ascontiguousarray(q), np.ascontiguousarray(warm)
+        with Heartbeat("skew: ground truth"):
+            gt = ground_truth(torch, base_t, torch.from_numpy(q).cuda(), a.k, metric)
+        qid = np.arange(q.shape[0], dtype=np.uint32)
+        with Heartbeat("skew: opening"):
+            idx = shine_amd.Index.open(paths, dim, M, metric, elem=elem, gpus=[0] * shards, placement="sharded",
+                                       cache=0.05)
+        idx.set_search_mode(shine_amd.MODE_FAST)
+        r0 = idx.knn(q, a.k, ef, query_ids=qid)
+        with Heartbeat("skew: warmup"):
+            idx.cache_warmup(warm, a.k, ef, query_ids=np.arange(warm.shape[0], dtype=np.uint32))
+        r1 = idx.knn(q, a.k, ef, query_ids=qid)
+        idx.close()
+
+        def rate(r):
+            h, m = r.stats["cache_hits"], r.stats["cache_misses"]
+            return h / max(1, h + m)
+
+        line = {"workload": "cfg5-skew", "alpha": alpha, "cache_fraction": 0.05, "gpu_slots": shards,
+                "hit_rate_static": rate(r0), "hit_rate_warmed": rate(r1),
+                "remote_share_static": r0.stats["remote_reads_in_bytes"] / max(1, r0.stats["algorithmic_bytes"]),
+                "remote_share_warmed": r1.stats["remote_reads_in_bytes"] / max(1, r1.stats["algorithmic_bytes"]),
+                "recall_at_10": D.recall_at_k(r1.ids, gt, a.k), "same_ids": bool((r0.ids == r1.ids).all()),
+                "config": {"generator": gen, "n": n, "dim": dim, "metric": "IP", "elem": "f16", "M": M, "efc": efc,
+                           "ef": ef, "queries": int(q.shape[0]), "warmup_queries": int(warm.shape[0])},
+                "note": "one physical GPU: the read classes (local / cached / remote) are exact, the xGMI rate is not "
+                        "measured"}
+        log(json.dumps(line))
+        lines.append(line)
+    return lines
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--which", default="cfg3,cfg5,sharded")
@@ -197,12 +258,13 @@ def main():
     p.add_argument("--inflight", type=int, default=2, help="batches in flight per GPU slot (HIP streams)")
     p.add_argument("--cache", default=os.environ.get("SHINE_CFG_CACHE", "/tmp/shine_cfg"))
     p.add_argument("--out", default=str(ROOT / "gpurun_out" / "config_lines.jsonl"))
+    p.add_argument("--alphas", default="0,0.5,1.0,1.5", help="cfg5skew: Zipf exponents")
     a = p.parse_args()
     import torch
     torch.cuda.set_device(0)
     Path(a.out).parent.mkdir(parents=True, exist_ok=True)
     for name in a.which.split(","):
-        for line in run(name, a):
+        for line in (run_skew(a) if name == "cfg5skew" else run(name, a)):
             print(json.dumps(line), flush=True)
             with open(a.out, "a") as f:
                 f.write(json.dumps(line) + "\n")
