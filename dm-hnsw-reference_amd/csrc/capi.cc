@@ -181,10 +181,12 @@ struct IndexState {
   int placement = SHINE_PLACE_REPLICA;
   uint64_t id_space = 0;       // device ids are < id_space (sharded: slot o owns [o * ids_per_slot, ...))
   uint64_t ids_per_slot = 0;
-  uint64_t cached_rows = 0;    // sharded: rows of every stripe other slots keep local copies of
+  uint64_t cached_rows = 0;    // sharded: vectors of every stripe other slots keep local copies of
+  uint64_t cached_list_rows = 0;  // ... and neighbour lists (each array's copy is whole VM pages of that array)
   uint32_t div_magic = 0, div_shift = 0;  // id / ids_per_slot = umulhi(id, div_magic) >> div_shift
   ShardedArray svec, sadj0;    // sharded: level-0 vectors and lists
-  double cache_fraction = 0;
+  double cache_fraction = 0;   // the cached share of every stripe's vectors, after rounding to whole pages
+  double cache_requested = 0;  // the caller's cache_fraction (a re-layout after a warmup rounds it again)
   Regions regions;             // SHINE_PLACE_SHARDED_REGIONS: slot o owns (and is routed) region o
   Router router;               // ... the query router's limits and histogram, kept across calls
   std::vector<double> slot_rate;  // ... queries per ms each slot answered in its last call (0 = not measured)
@@ -222,6 +224,7 @@ DevGraph dev_graph(const shine_index* h, const Replica& r) {
   g.slot = r.slot;
   g.stripe_ids = static_cast<uint32_t>(h->ids_per_slot);
   g.cached_rows = static_cast<uint32_t>(h->cached_rows);
+  g.cached_list_rows = static_cast<uint32_t>(h->cached_list_rows);
   g.div_magic = h->div_magic;
   g.div_shift = h->div_shift;
   return g;
@@ -568,15 +571,21 @@ int make_index(HostGraph G, int elem, const int* gpu_ids, uint32_t n_gpus, int p
   }
   const uint64_t replicated = 4 * (uid_d->size() + upb_d->size() + adjU_d->size() + inv.size());
   if (sharded) {
-    // the cached prefix of every stripe, in whole VM pages of both arrays (rows of the two arrays stay aligned)
-    uint64_t crows = static_cast<uint64_t>(cache_fraction * static_cast<double>(U) + 0.5);
-    uint64_t step = 1;
-    while ((step * vrow) % gran != 0 || (step * arow) % gran != 0) step <<= 1;
-    crows = std::min<uint64_t>(U, (crows + step - 1) / step * step);
-    h->cache_fraction = static_cast<double>(crows) / static_cast<double>(U);
-    h->cached_rows = slots > 1 ? crows : 0;
-    if (int rc = map_sharded(h->svec, U * vrow, crows * vrow, devs, gran)) return rc;
-    if (int rc = map_sharded(h->sadj0, U * arow, crows * arow, devs, gran)) return rc;
+    // the cached prefix of every stripe: the leading cache_fraction of each array's bytes, rounded up to whole VM
+    // pages of that array.  A record counts as cached when its row lies wholly inside (a row straddling the edge
+    // reads partly over xGMI and counts as remote).  Rounding the two arrays to a common row count instead would
+    // cost whole stripes: 400-byte fp16 rows (cfg 5) meet a 2 MiB page only every 131,072 rows.
+    auto hot_bytes = [&](uint64_t stride) {
+      const uint64_t b = static_cast<uint64_t>(cache_fraction * static_cast<double>(stride) + 0.5);
+      return std::min<uint64_t>(stride, (b + gran - 1) / gran * gran);
+    };
+    const uint64_t hot_v = slots > 1 ? hot_bytes(U * vrow) : 0, hot_a = slots > 1 ? hot_bytes(U * arow) : 0;
+    h->cached_rows = hot_v / vrow;
+    h->cached_list_rows = hot_a / arow;
+    h->cache_fraction = static_cast<double>(hot_v) / static_cast<double>(U * vrow);
+    h->cache_requested = cache_fraction;
+    if (int rc = map_sharded(h->svec, U * vrow, hot_v, devs, gran)) return rc;
+    if (int rc = map_sharded(h->sadj0, U * arow, hot_a, devs, gran)) return rc;
     std::vector<uint8_t> vb;
     std::vector<uint32_t> rows;
     for (uint32_t o = 0; o < slots; ++o) {
@@ -594,7 +603,7 @@ int make_index(HostGraph G, int elem, const int* gpu_ids, uint32_t n_gpus, int p
     }
     if (int rc = fill_copies(h->svec, devs)) return rc;
     if (int rc = fill_copies(h->sadj0, devs)) return rc;
-    h->device_bytes = U * (vrow + arow) + (slots - 1) * crows * (vrow + arow) + replicated;
+    h->device_bytes = U * (vrow + arow) + (slots - 1) * (hot_v + hot_a) + replicated;
   } else {
     h->device_bytes = vlen + 4 * G.adj0.size() + replicated;
   }
@@ -1174,7 +1183,8 @@ int shine_cache_warmup(shine_index_t h, const float* queries, const uint32_t* qu
   if (!queries) return set_error(SHINE_ERR_ARG, "NULL host pointer");
   std::lock_guard<std::mutex> lk(h->mu);
   const uint32_t G = static_cast<uint32_t>(h->reps.size());
-  if (h->placement == SHINE_PLACE_REPLICA || G < 2 || h->cached_rows == 0) return SHINE_OK;  // nothing is cached
+  if (h->placement == SHINE_PLACE_REPLICA || G < 2 || (h->cached_rows == 0 && h->cached_list_rows == 0))
+    return SHINE_OK;  // nothing is cached
   if (h->host.N == 0 || h->dev_of.size() != h->host.N)
     return set_error(SHINE_ERR_ARG, "the index's host graph is gone (an earlier warmup failed): reopen it");
   // 1. the warmup split, with every record read counted per slot (the reference's warmup run, compute_node.cc:116-131)
@@ -1205,7 +1215,7 @@ int shine_cache_warmup(shine_index_t h, const float* queries, const uint32_t* qu
   shine_index_t nh = nullptr;
   const std::vector<int> devs = h->devs;
   if (int rc = make_index(std::move(h->host), h->elem, devs.data(), static_cast<uint32_t>(devs.size()), h->placement,
-                          h->cache_fraction, &nh, &heat))
+                          h->cache_requested, &nh, &heat))
     return rc;
   nh->search_mode = h->search_mode;
   release_state(h);

@@ -22,6 +22,8 @@ struct DevGraph {
   // umulhi(x, div_magic) >> div_shift, exact for x < 2^31); it is local when the stripe is `slot`, a cached copy
   // when x % stripe_ids < cached_rows, otherwise an xGMI read.  sharded = 0: every read is local (replica).
   uint32_t sharded, slot, stripe_ids, cached_rows, div_magic, div_shift;
+  uint32_t cached_list_rows;  // lists of rows x % stripe_ids < cached_list_rows are cached (the arrays' cached
+                              // prefixes are whole VM pages of each array, so the two row counts differ)
 };
 
 // Per-query counter words (u32) written by the search kernels; include/shine_gpu.h SHINE_QS_*.

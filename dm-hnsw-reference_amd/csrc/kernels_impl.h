@@ -414,10 +414,11 @@ struct ReadCount {
   u32 vec_remote = 0, list_remote = 0, vec_cached = 0, list_cached = 0;
 };
 
-__device__ __forceinline__ u32 read_class(const DevGraph& g, u32 x) {  // 0 own stripe, 1 cached copy, 2 xGMI
+// 0 own stripe, 1 cached copy, 2 xGMI; `cached` = the array's cached rows per stripe (vectors or lists)
+__device__ __forceinline__ u32 read_class(const DevGraph& g, u32 x, u32 cached) {
   const u32 s = __umulhi(x, g.div_magic) >> g.div_shift;
   const u32 r = x - s * g.stripe_ids;
-  return s == g.slot ? 0u : (r < g.cached_rows ? 1u : 2u);
+  return s == g.slot ? 0u : (r < cached ? 1u : 2u);
 }
 
 // vector reads of the lanes with `active` set (each reads record x).  ACCT = false (replica, no warmup) compiles
@@ -426,7 +427,7 @@ template <bool ACCT>
 __device__ __forceinline__ void count_vec_reads(const SearchArgs& A, ReadCount& rc, bool active, u32 x) {
   if constexpr (!ACCT) return;
   if (A.g.sharded) {
-    const u32 c = active ? read_class(A.g, x) : 0u;
+    const u32 c = active ? read_class(A.g, x, A.g.cached_rows) : 0u;
     rc.vec_remote += __popcll(__ballot(c == 2u));
     rc.vec_cached += __popcll(__ballot(c == 1u));
   }
@@ -438,7 +439,7 @@ template <bool ACCT>
 __device__ __forceinline__ void count_list_read(const SearchArgs& A, ReadCount& rc, u32 x, int lane) {
   if constexpr (!ACCT) return;
   if (A.g.sharded) {
-    const u32 c = read_class(A.g, x);
+    const u32 c = read_class(A.g, x, A.g.cached_list_rows);
     rc.list_remote += c == 2u ? 1u : 0u;
     rc.list_cached += c == 1u ? 1u : 0u;
   }
@@ -994,12 +995,24 @@ constexpr u32 EXPANDED = 0x80000000u;  // id bit: this candidate has been expand
 // refilled as soon as the current distances have consumed it, and every list / vector load on the common path is
 // unconditional, so every wait is an exact vmcnt that never covers the younger prefetches.
 // ------------------------------------------------------------------------------------------------------------
+// Slot layout of a neighbour list in the fast kernel: list slot 16p + g lives in lane 4g + p (p < P), so the lane
+// group g that evaluates slot 16p + g in pass p finds the slot's id in its own lane p (a DPP quad broadcast) and the
+// group's distance reaches the slot's lane the same way: no ds_bpermute between the pick, the vector loads and the
+// merge.  List order is slot order, not lane order, wherever the reference's list order decides.
+__device__ __forceinline__ u32 quad_bcast(u32 x, int p) {  // lane 4g + p's value to all of group g
+  switch (p) {
+    case 0: return static_cast<u32>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x00, 0xF, 0xF, false));
+    case 1: return static_cast<u32>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x55, 0xF, 0xF, false));
+    case 2: return static_cast<u32>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0xAA, 0xF, 0xF, false));
+    default: return static_cast<u32>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0xFF, 0xF, 0xF, false));
+  }
+}
+
 template <int D, typename E, int P>
-__device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restrict__ vec, u32 e, u32 pad, int g4,
-                                           int c4) {
+__device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restrict__ vec, u32 e, u32 pad, int c4) {
   u32 sid[P];
 #pragma unroll
-  for (int p = 0; p < P; ++p) sid[p] = static_cast<u32>(__shfl(static_cast<int>(e), 16 * p + g4));
+  for (int p = 0; p < P; ++p) sid[p] = quad_bcast(e, p);
 #pragma unroll
   for (int p = 0; p < P; ++p) issue_pass_u<D, E, P>(B, p, vec, sid[p], pad, c4);
 }
@@ -1019,11 +1032,13 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
   const u32 M0 = A.g.M0, pad = A.g.pad_node;
   const int ef = static_cast<int>(A.ef);
   const float INF = __builtin_inff();
-  const bool in_row = static_cast<u32>(lane) < M0;
-  const u32 row_lane = in_row ? static_cast<u32>(lane) : 0u;
-  // Unconditional, and never masked right after the load (that would wait for it): lanes beyond M0 hold a copy of
-  // entry 0 and are excluded where the list is used (the visited test; slots >= M0 are never fresh).
+  const u32 my_slot = 16u * static_cast<u32>(c4) + static_cast<u32>(g4);  // list slot of this lane (issue_list)
+  const bool in_row = c4 < P && my_slot < M0;
+  const u32 row_lane = in_row ? my_slot : 0u;
+  // Unconditional, and never masked right after the load (that would wait for it): lanes without a slot hold a copy
+  // of entry 0 and are excluded where the list is used (the visited test; they are never fresh).
   auto load_row = [&](u32 node) -> u32 { return adj0[static_cast<u64>(node) * M0 + row_lane]; };
+  auto slot_of = [](int l) { return 16 * (l & 3) + (l >> 2); };
 
   const u32 n_items = A.in_count ? *A.in_count : A.nq;
   for (;;) {
@@ -1069,7 +1084,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
     // prefetched list.  X is refilled for the next candidate as soon as the current distances have consumed it.
     NbrBuf<D, E, P> X;
     u32 e = load_row(status == 0 ? nn : pad);
-    issue_list<D, E, P>(X, vec, e, pad, g4, c4);
+    issue_list<D, E, P>(X, vec, e, pad, c4);
     u32 r_id = INV;
     float r_key = INF;
     u32 nid = nn;
@@ -1082,9 +1097,11 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       PHASE(8)
       bool cand = in_row && e != INV;
       if (!A.g.lists_unique) {  // first occurrence in list order wins (visited.insert order, :443)
-        for (u32 j = 0; j < M0; ++j) {
-          const u32 ej = __shfl(e, static_cast<int>(j));
-          if (j < static_cast<u32>(lane) && ej == e) cand = false;
+#pragma unroll 1
+        for (int j = 0; j < 4 * 16; ++j) {
+          const u32 ej = __shfl(e, j);
+          const u32 sj = static_cast<u32>(slot_of(j));
+          if ((j & 3) < P && sj < M0 && sj < my_slot && ej == e) cand = false;
         }
       }
       bool fresh = false, vovf = false;
@@ -1107,16 +1124,15 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       }
 
       PHASE(5)
-      float my_d = INF;  // lane j: distance of list slot j
+      float my_d = INF;  // distance of this lane's list slot
       u64 acc = 0;
       if (nf > 0) {
         float out[P];
         pass_dists<D, METRIC, E, P>(Q, X, out);
-        const int src = ((lane & 15) << 2) + 3;
 #pragma unroll
-        for (int p = 0; p < P; ++p) {
-          const float v = __shfl(out[p], src);
-          if ((lane >> 4) == p) my_d = v;
+        for (int p = 0; p < P; ++p) {  // the group's sum is complete in its lane 3 (fold8)
+          const float v = __uint_as_float(quad_bcast(__float_as_uint(out[p]), 3));
+          if (c4 == p) my_d = v;
         }
         if (!fresh) my_d = INF;
         if (fresh && my_d != my_d) {  // NaN: the reference's comparisons are all false; no ordered slot exists here
@@ -1135,15 +1151,22 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       if (acc) {
         const float fstar = wave_min(((acc >> lane) & 1ull) ? my_d : INF);
         const u64 hit = acc & __ballot(my_d == fstar);
-        if (r_id == INV || fstar <= r_key)
-          pid = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(e), 63 - static_cast<int>(__clzll(hit))));
+        if (r_id == INV || fstar <= r_key) {  // the last list slot among equals: highest p, then highest group
+          int hl = 0;
+#pragma unroll
+          for (int p = 0; p < P; ++p) {
+            const u64 m = hit & (0x1111111111111111ull << p);
+            if (m) hl = 63 - static_cast<int>(__clzll(m));
+          }
+          pid = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(e), hl));
+        }
       }
       if (pid == r_id) EVENT(9) else EVENT(10)
       const u32 prow = pid == r_id ? nrow : load_row(pid != INV ? pid : pad);  // a fresh f*: its list now
       // an entry already at its home slot of the visited table is not fresh: its row is not requested (one
       // read-only LDS probe; the visit proper still runs at the top of the next expansion)
       const bool seen = in_row && prow != INV && vis.at_home(prow);
-      issue_list<D, E, P>(X, vec, seen ? INV : prow, pad, g4, c4);
+      issue_list<D, E, P>(X, vec, seen ? INV : prow, pad, c4);
 
       // ---- merge (:456-465 over the whole list at once) ----------------------------------------------------------
       PHASE(6)
@@ -1164,7 +1187,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
             shift[r] += d <= ck[r] ? 1 : 0;
             below += __popcll(__ballot(ck[r] < d));
           }
-          frank += (d < my_d || (d == my_d && i > lane)) ? 1 : 0;
+          frank += (d < my_d || (d == my_d && slot_of(i) > static_cast<int>(my_slot))) ? 1 : 0;
           fbase = lane == i ? below : fbase;
         }
         const int total = cs + __popcll(acc);
@@ -1241,7 +1264,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       if (c != pid) {  // mispredicted (ties / NaN keys): fetch the picked candidate's list and vectors
         EVENT(11)
         erow = c == nid ? nrow : load_row(c);
-        issue_list<D, E, P>(X, vec, erow, pad, g4, c4);
+        issue_list<D, E, P>(X, vec, erow, pad, c4);
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this rare path leaves nothing in flight behind the prefetch
       }
       nid = c2 != INV ? c2 : c;

@@ -85,7 +85,7 @@ typedef struct shine_index_info {
   uint32_t placement;      /* SHINE_PLACE_* */
   uint32_t reserved0;
   uint64_t id_space;       /* device node-id range: num_nodes (replica) or n_gpus x ids_per_gpu (sharded) */
-  double cache_fraction;   /* sharded: share of every other GPU's records held in local HBM copies */
+  double cache_fraction;   /* sharded: share of every other GPU's record vectors held in local HBM copies */
   uint32_t cus;            /* compute units of GPU slot 0 (hipDeviceProp_t), used to size the launches */
   uint32_t lds_per_cu;     /* LDS bytes per CU of GPU slot 0 */
 } shine_index_info;
@@ -122,7 +122,8 @@ int shine_open_buffers(const uint8_t* const* dumps, const uint64_t* sizes, uint3
 
 /* shine_open / shine_open_buffers with an explicit placement (SHINE_PLACE_*).  gpu_ids may repeat a device (e.g.
  * {0, 0}): each slot then owns its own stripe on that device, which exercises the sharded layout on one GPU.
- * cache_fraction (sharded only, in [0, 1]; rounded to whole 2 MiB pages) replaces the compute node's record cache
+ * cache_fraction (sharded only, in [0, 1]; each array's share rounded up to whole 2 MiB pages of that array, and
+ * shine_index_info.cache_fraction reports the vectors' share after rounding) replaces the compute node's record cache
  * (cache::Cache, cache.hh:102-311, sized as a share of the index, compute_node.cc:40-56): each slot's records are
  * ordered hottest first (upper-level nodes, then level-0 in-degree; the reference always admits upper levels,
  * cache.hh:368) and every GPU keeps local copies of that leading share of every other GPU's records, so those

@@ -255,8 +255,9 @@ def test_release_stream_then_reuse(four_shards, gpu_available):
 
 @pytest.fixture(scope="module")
 def skew_index():
-    """200K DEEP-shaped records in 8 memory-node dumps: two slots of ~100K records, so a 0.15 cache (rounded up to
-    whole 2 MiB page steps of 16,384 rows) holds under a third of each stripe."""
+    """200K DEEP-shaped records in 8 memory-node dumps: two slots of ~100K records (stripes of 114,688 ids), so a 0.15
+    cache (each array's share rounded up to whole 2 MiB pages: 21,845 vector rows) holds under a fifth of each
+    stripe."""
     base = D.deep_like(200_000, seed=111, d=96)
     dumps, _ = shine_amd.build(base, 16, 100, 0, 8, seed=7, threads=16)
     pool = D.deep_like(3000, seed=112, d=96)
@@ -273,7 +274,7 @@ def test_cache_warmup_hit_rate_rises_with_skew_and_results_do_not_change(skew_in
     for alpha in (0.0, 1.0, 1.5):
         q, warm, _ = D.zipf_query_mix(pool, 3000, alpha, split=1000, seed=9)
         with shine_amd.Index.from_buffers(dumps, 96, 16, 0, gpus=[0, 0], placement="sharded", cache=0.15) as idx:
-            assert 0.2 < idx.info()["cache_fraction"] < 0.5
+            assert 0.15 <= idx.info()["cache_fraction"] < 0.25
             static = idx.knn(q, 10, 128)
             idx.cache_warmup(warm, 10, 128)
             warmed = idx.knn(q, 10, 128)
