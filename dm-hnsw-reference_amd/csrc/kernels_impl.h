@@ -609,10 +609,17 @@ struct VisitedLds<0> {
   }
   __device__ __forceinline__ void insert_first(u32 x) { t[vhash(x, shift)] = x; }  // the table is empty
   __device__ __forceinline__ bool at_home(u32 x) const { return t[vhash(x, shift)] == x; }
-  // one exit from the probe loop (an early return per outcome compiles to a branchier loop and more live SGPRs)
-  __device__ __forceinline__ bool test_and_set(u32 x, bool& /*ovf*/) {
+  // the word at x's home slot (one read); home_match: x sits at home in that word
+  __device__ __forceinline__ u32 probe(u32 x) const { return t[vhash(x, shift)]; }
+  __device__ __forceinline__ bool home_match(u32 x, u32 w) const { return w == x; }
+  // one exit from the probe loop (an early return per outcome compiles to a branchier loop and more live SGPRs).
+  // hint: the home word as probe() read it since the last insert (INV: unknown), so a key found at home costs no
+  // LDS operation and a home held by another key is skipped without a failed compare-and-swap
+  __device__ __forceinline__ bool test_and_set(u32 x, bool& /*ovf*/, u32 hint = INV) {
     u32 h = vhash(x, shift);
     bool fresh = false;
+    if (hint == x) return false;
+    if (hint != INV) h = (h + 1) & mask;  // slots are never freed: home still holds that other key
     for (;;) {
       const u32 old = atomicCAS(&t[h], INV, x);
       if (old == INV) {
@@ -654,9 +661,15 @@ struct VisitedLds<1> {
     const u32 h = image(x);
     return t16[h >> rbits] == static_cast<unsigned short>((h & rmask) << dbits);
   }
-  __device__ __forceinline__ bool test_and_set(u32 x, bool& ovf) {
+  __device__ __forceinline__ u32 probe(u32 x) const { return t[(image(x) >> rbits) >> 1]; }
+  __device__ __forceinline__ bool home_match(u32 x, u32 w) const {
+    const u32 h = image(x), s = h >> rbits;
+    return ((w >> ((s & 1u) << 4)) & 0xFFFFu) == ((h & rmask) << dbits);
+  }
+  // hint: the home word as probe() read it (INV: unknown); the first compare-and-swap expects it
+  __device__ __forceinline__ bool test_and_set(u32 x, bool& ovf, u32 hint = INV) {
     const u32 h = image(x);
-    u32 s = h >> rbits, disp = 0, cur = INV;  // first attempt: the word is assumed empty
+    u32 s = h >> rbits, disp = 0, cur = hint;  // first attempt: the home word as last seen (INV: assumed empty)
     const u32 rem = (h & rmask) << dbits;
     bool fresh = false;
     for (;;) {
@@ -1090,6 +1103,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
     u32 nid = nn;
     u32 nrow = load_row(nn);
     u32 cur = nn;  // the candidate whose list `e` is
+    u32 ehint = INV;  // this lane's home word of e as probed one expansion earlier (VisitedLds::test_and_set)
 
     while (status == 0) {
       ++st_ll0;  // read_neighborlist (:436-438)
@@ -1105,7 +1119,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
         }
       }
       bool fresh = false, vovf = false;
-      if (cand) fresh = vis.test_and_set(e, vovf);  // visited.contains / insert (:441-443)
+      if (cand) fresh = vis.test_and_set(e, vovf, ehint);  // visited.contains / insert (:441-443)
       if constexpr (VT == 1) {
         if (__ballot(vovf)) {  // an id too far from its home slot: the light pass re-runs the query
           status = ST_OVERFLOW;
@@ -1165,7 +1179,8 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       const u32 prow = pid == r_id ? nrow : load_row(pid != INV ? pid : pad);  // a fresh f*: its list now
       // an entry already at its home slot of the visited table is not fresh: its row is not requested (one
       // read-only LDS probe; the visit proper still runs at the top of the next expansion)
-      const bool seen = in_row && prow != INV && vis.at_home(prow);
+      const u32 pword = in_row && prow != INV ? vis.probe(prow) : INV;
+      const bool seen = in_row && prow != INV && vis.home_match(prow, pword);
       issue_list<D, E, P>(X, vec, seen ? INV : prow, pad, c4);
 
       // ---- merge (:456-465 over the whole list at once) ----------------------------------------------------------
@@ -1270,6 +1285,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       nid = c2 != INV ? c2 : c;
       nrow = load_row(nid);  // unconditional: always the youngest load
       e = erow;
+      ehint = c != pid ? INV : pword;  // the probe read prow's home words, and no insert has happened since
       cur = c;
       r_id = c2;
       r_key = k2;

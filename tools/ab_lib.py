@@ -6,7 +6,8 @@ pair of HIP streams; timed blocks alternate A, B, A, B, ... so box and clock dri
 entry points whose signatures are unchanged since round 1 are used (shine_open, shine_set_search_mode,
 shine_knn_batch_device, shine_close), so an older build can be the A side.
 
-Usage: python tools/ab_lib.py --libs _abl/libshine_r01.so,dm-hnsw-reference_amd/libshine_gpu.so --ef 32,128
+Usage: GPU_MAX_HW_QUEUES=16 python tools/ab_lib.py --libs _abl/libshine_r01.so,dm-hnsw-reference_amd/libshine_gpu.so --ef 32,128
+(with the default 4 hardware queues the streams of several sides share queues and one side can lose its overlap)
 Per-library environment (the SHINE_DEBUG_* hooks) goes after '@': --libs "a.so,b.so@SHINE_DEBUG_NO_SEEN=1".
 """
 from __future__ import annotations
