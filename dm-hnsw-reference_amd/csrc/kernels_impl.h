@@ -1202,7 +1202,9 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
             shift[r] += d <= ck[r] ? 1 : 0;
             below += __popcll(__ballot(ck[r] < d));
           }
-          frank += (d < my_d || (d == my_d && slot_of(i) > static_cast<int>(my_slot))) ? 1 : 0;
+          // non-short-circuit: three compares and two mask ops, no exec-mask branches inside the key loop
+          const bool before = (d < my_d) | ((d == my_d) & (slot_of(i) > static_cast<int>(my_slot)));
+          frank += before ? 1 : 0;
           fbase = lane == i ? below : fbase;
         }
         const int total = cs + __popcll(acc);
