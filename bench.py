@@ -385,6 +385,18 @@ def main():
         dist.destroy_process_group()
 
 
+def sharded_plan(slots: int, ndev: int, batch: int, nbatches: int):
+    """GPU of every slot of the sharded leg (slot s on device s % ndev, so N slots over N devices is one slot per
+    GPU and more slots than devices repeat them) and the query rows each slot answers in every batch: the
+    compute-node split by query id, id % slots (read_data.hh:57-58)."""
+    if slots < 1 or ndev < 1:
+        raise SystemExit("--placement sharded needs at least one slot and one GPU")
+    gpus = [s % ndev for s in range(slots)]
+    ids = [np.arange(b * batch, (b + 1) * batch) for b in range(nbatches)]
+    rows = [[ids[b][ids[b] % slots == s] for s in range(slots)] for b in range(nbatches)]
+    return gpus, rows
+
+
 def run_sharded(a):
     """cfg-4-shaped sharded leg: one process drives S GPU slots of one index in the sharded placement
     (include/shine_gpu.h SHINE_PLACE_SHARDED): memory node m lives on slot m % S only, every slot reads the others'
@@ -398,7 +410,7 @@ def run_sharded(a):
         raise SystemExit("--placement sharded runs as one process driving every GPU slot (not under torchrun)")
     ndev = torch.cuda.device_count()
     S = a.slots or a.gpus
-    gpus = [s % ndev for s in range(S)]
+    gpus, rows = sharded_plan(S, ndev, a.batch, a.nbatches)
     phys = len(set(gpus))
     dim, M, efc, ef, shards = 96, 16, 200, 128, 8
     key = hashlib.sha1(f"{a.n}-{dim}-{M}-{efc}-{shards}-deep_like-l2-v1".encode()).hexdigest()[:12]
@@ -420,7 +432,6 @@ def run_sharded(a):
     nb, B, k = a.nbatches, a.batch, a.k
     q = D.deep_like(B * nb, seed=2, d=dim)
     gt = ground_truth(torch, base, q, k, 0)
-    rows = [[np.arange(b * B, (b + 1) * B)[np.arange(B) % S == s] for s in range(S)] for b in range(nb)]
     qd, ids, qs, streams = [], [], [], []
     for s in range(S):
         dev = torch.device("cuda", gpus[s])

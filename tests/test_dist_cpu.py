@@ -82,3 +82,32 @@ def test_rank_queries_partition():
     rows = sorted(int(x) for p in parts for x in p[:, 0] // 2)
     assert rows == list(range(20))
     assert all((p[:, 0] // 2 % 3 == r).all() for r, p in enumerate(parts))
+
+
+@pytest.mark.parametrize("slots,ndev", [(8, 8), (8, 1), (4, 2), (3, 8), (1, 1)])
+def test_sharded_leg_slot_plan(slots, ndev):
+    """bench.py --placement sharded: slot s runs on device s % ndev (N slots over N GPUs = one per GPU; more slots
+    than GPUs repeat devices), and every batch's queries are split by id % slots, each exactly once."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    gpus, rows = bench.sharded_plan(slots, ndev, 1024, 3)
+    assert gpus == [s % ndev for s in range(slots)]
+    assert len(set(gpus)) == min(slots, ndev)
+    for b in range(3):
+        allq = np.sort(np.concatenate(rows[b]))
+        np.testing.assert_array_equal(allq, np.arange(b * 1024, (b + 1) * 1024))
+        for s in range(slots):
+            assert (rows[b][s] % slots == s).all()
+
+
+def test_sharded_leg_refuses_torchrun_and_empty_plans(monkeypatch):
+    sys.path.insert(0, str(ROOT))
+    import bench
+    with pytest.raises(SystemExit):
+        bench.sharded_plan(0, 8, 1024, 1)
+    monkeypatch.setenv("WORLD_SIZE", "2")
+
+    class A:
+        pass
+    with pytest.raises(SystemExit):
+        bench.run_sharded(A())
