@@ -19,6 +19,10 @@ the same streams, K steps; `value_host_api` is the synchronous C-ABI host call s
 and `cpu_baseline` (the CPU oracle — a C++ restatement of the reference's knn — built with the reference's flags on
 the host that runs it, on the host cores, bounded sample, rank 0 at N=1 only).
 
+Row storage: `value` is measured on f32 rows (the reference's records).  `other_rows` times the same fast-mode
+search on the narrowest lossless rows (u8: SIFT-shaped components are byte values, as in the reference's .u8bin
+inputs) and checks that ids, distances and counters are bitwise the same; it is 4x fewer bytes per distance.
+
 --placement sharded (one process, not torchrun) runs the cfg-4-shaped sharded leg instead: a DEEP-shaped 96-d L2
 index as 8 memory-node dumps over --slots GPU slots (slot s on GPU s % device_count; memory node m on slot m % S),
 every batch split id % S over the slots, and reports the share of reads that left a slot's stripe (xGMI) and the
@@ -40,6 +44,8 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "dm-hnsw-reference_amd"))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+ROW_NAMES = {0: "f32", 1: "f16", 2: "u8", 3: "i8"}  # shine_index_info.elem
+KERNEL_TYPE = {"f32": "float", "f16": "__half", "u8": "unsigned char", "i8": "signed char"}  # rocprof kernel names
 
 
 def log(msg):
@@ -117,6 +123,12 @@ def parse():
                    help="per-launch HBM bytes of the search kernel measured by rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                         "passes of this bench (tools/pmc.py; tools/gpu_round.sh)")
     p.add_argument("--no-host", action="store_true", help="skip the host-to-host and host-API legs")
+    p.add_argument("--rows", choices=["auto", "f32", "u8"], default="f32",
+                   help="record storage in HBM for `value` (include/shine_gpu.h SHINE_ELEM_*): f32 as the reference's "
+                        "records; auto = the narrowest lossless rows (u8 for SIFT-shaped records, whose components are "
+                        "byte values as in the reference's .u8bin inputs); results are bitwise the same")
+    p.add_argument("--no-rows-compare", action="store_true",
+                   help="skip timing fast mode on the other row storage (byte rows next to f32, or f32 next to bytes)")
     p.add_argument("--placement", choices=["replica", "sharded"], default="replica")
     p.add_argument("--slots", type=int, default=0, help="sharded leg: GPU slots (default --gpus)")
     p.add_argument("--cache-frac", type=float, default=0.0, help="sharded leg: share of other stripes cached locally")
@@ -155,10 +167,12 @@ def main():
         return dumps
 
     prepare_dumps(paths, rank, dist, build)
-    idx = shine_amd.Index.open(paths, a.dim, a.M, shine_amd.METRIC_L2, gpus=[local])
+    elem = {"auto": shine_amd.ELEM_AUTO, "f32": shine_amd.ELEM_F32, "u8": shine_amd.ELEM_U8}[a.rows]
+    idx = shine_amd.Index.open(paths, a.dim, a.M, shine_amd.METRIC_L2, elem=elem, gpus=[local])
     info = idx.info()
+    rows = ROW_NAMES[info["elem"]]
     log(f"rank {rank}: index on GPU {local}: {info['num_nodes']} nodes, max level {info['max_level']}, "
-        f"{info['device_bytes'] / 2**20:.0f} MiB; device {info['cus']} CUs, {info['lds_per_cu']} B LDS per CU")
+        f"{info['device_bytes'] / 2**20:.0f} MiB ({rows} rows); device {info['cus']} CUs, {info['lds_per_cu']} B LDS per CU")
 
     # queries: rank r takes ids ≡ r (mod G) of a common pool (read_data.hh:57-58)
     nq_rank = a.batch * a.nbatches
@@ -175,36 +189,38 @@ def main():
     streams = [torch.cuda.Stream() for _ in range(max(1, a.inflight))]
     torch.cuda.set_stream(streams[0])
 
-    def step(i, rec=None, ef=None):
+    def step(i, rec=None, ef=None, ix=None):
         b = i % a.nbatches
         stream = streams[i % len(streams)]
         if rec is not None:
             rec[0].record(stream)
-        idx.knn_device(qd[b * a.batch:(b + 1) * a.batch].data_ptr(), a.batch, a.k, ef or a.ef, ids[b].data_ptr(),
+        (ix or idx).knn_device(qd[b * a.batch:(b + 1) * a.batch].data_ptr(), a.batch, a.k, ef or a.ef, ids[b].data_ptr(),
                        dists[b].data_ptr(), qs[b].data_ptr(), stream=stream.cuda_stream)
         if rec is not None:
             rec[1].record(stream)
 
     gt = ground_truth(torch, base, q, a.k, 0)
 
-    def run_mode(mode):
+    def run_mode(mode, ix=None):
         """Validation pass over every batch (status, recall, algorithmic bytes), warmup, then exactly K timed
         steps between barriers; returns the measurements."""
-        idx.set_search_mode(mode)
+        ix = ix or idx
+        ix.set_search_mode(mode)
         for i in range(a.nbatches):
-            step(i)
+            step(i, ix=ix)
         torch.cuda.synchronize()
         qs_h = qs.cpu().numpy().view(np.uint32).reshape(-1, shine_amd.QS_WORDS).copy()
         n_bad = int((qs_h[:, 6] != 0).sum())
         if n_bad:
             raise SystemExit(f"{n_bad} queries did not complete (status {np.unique(qs_h[:, 6])})")
-        bq_batch = [idx.algorithmic_bytes(qs_h[b * a.batch:(b + 1) * a.batch]) for b in range(a.nbatches)]
+        bq_batch = [ix.algorithmic_bytes(qs_h[b * a.batch:(b + 1) * a.batch]) for b in range(a.nbatches)]
         res = ids.cpu().numpy().view(np.uint32).reshape(-1, a.k).copy()
+        res_d = dists.cpu().numpy().copy()
         recall = D.recall_at_k(res, gt, a.k)
         log(f"rank {rank}: mode {mode}: recall@{a.k} = {recall:.4f} over {nq_rank} queries; mean distcomps "
             f"{qs_h[:, 0].mean():.0f}, lists L0 {qs_h[:, 4].mean():.1f}")
         for i in range(a.warmup):
-            step(i)
+            step(i, ix=ix)
         torch.cuda.synchronize()
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
         if dist:
@@ -212,7 +228,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(a.steps):
-            step(a.warmup + i, evs[i])
+            step(a.warmup + i, evs[i], ix=ix)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         if dist:
@@ -222,7 +238,7 @@ def main():
         span_ms = max(evs[0][0].elapsed_time(e) for _, e in evs)  # first launch's start to the last one's end
         bytes_steps = [bq_batch[(a.warmup + i) % a.nbatches] for i in range(a.steps)]
         return dict(elapsed=elapsed, kern_ms=kern_ms, span_ms=span_ms, bytes_steps=bytes_steps, recall=recall,
-                    qs=qs_h, ids=res)
+                    qs=qs_h, ids=res, dists=res_d)
 
     def host_legs(mode):
         """SURVEY §8d's query phase, host to host: pinned host queries → H2D → knn → D2H of ids and distances, all
@@ -280,6 +296,27 @@ def main():
         raise SystemExit("--nbatches must be a multiple of --inflight (a batch's buffers stay on one stream)")
     modes = ["fast", "exact"] if a.mode == "both" else [a.mode]
     runs = {m: run_mode(shine_amd.MODE_FAST if m == "fast" else shine_amd.MODE_EXACT) for m in modes}
+    other_rows = None
+    if "fast" in runs and not a.no_rows_compare:
+        # the same search on the other row storage: f32 rows (4 B per component) next to byte rows, or the narrowest
+        # lossless rows next to f32; same results bit for bit, different bytes per distance
+        oelem = shine_amd.ELEM_F32 if rows != "f32" else shine_amd.ELEM_AUTO
+        with shine_amd.Index.open(paths, a.dim, a.M, shine_amd.METRIC_L2, elem=oelem, gpus=[local]) as io:
+            orows = ROW_NAMES[io.info()["elem"]]
+            ro = run_mode(shine_amd.MODE_FAST, io) if orows != rows else None
+        if ro is not None:
+            fr = runs["fast"]
+            other_rows = {"rows": orows, "value": a.steps * a.batch * world / ro["elapsed"],
+                          "ms_per_step": ro["elapsed"] * 1e3 / a.steps, "avg_launch_ms": float(np.mean(ro["kern_ms"])),
+                          "recall_at_10": ro["recall"],
+                          "roofline_frac": sum(ro["bytes_steps"]) / (ro["span_ms"] / 1e3) / 1e9 / HBM_PEAK_GBPS,
+                          "algorithmic_bytes_per_launch": float(np.mean(ro["bytes_steps"])),
+                          "kernel": f"search_fast_kernel<128,L2,{orows},R=2,P=2>",
+                          "same_ids_dists_counters": bool(
+                              (ro["ids"] == fr["ids"]).all() and (ro["dists"].view(np.uint32) == fr["dists"].view(np.uint32)).all()
+                              and (ro["qs"][:, :8] == fr["qs"][:, :8]).all())}
+            log(f"{orows} rows: {other_rows['value'] / 1e6:.2f}M QPS, frac {other_rows['roofline_frac']:.3f}, identical "
+                f"results: {other_rows['same_ids_dists_counters']}")
     host = None if a.no_host else host_legs(shine_amd.MODE_FAST if modes[0] == "fast" else shine_amd.MODE_EXACT)
     head = runs[modes[0]]
     elapsed, kern_ms, bytes_steps, recall, qs_h = (head[x] for x in ("elapsed", "kern_ms", "bytes_steps", "recall", "qs"))
@@ -334,7 +371,8 @@ def main():
     traffic, traffic_src = None, None
     if a.pmc_json and Path(a.pmc_json).exists():
         pmc = json.loads(Path(a.pmc_json).read_text())
-        if any(k.startswith("void shine::(anonymous namespace)::search_fast_kernel<128, 0, float, 2,") for k in pmc.get("kernels", [])):
+        want = f"void shine::(anonymous namespace)::search_fast_kernel<128, 0, {KERNEL_TYPE[rows]}, 2,"
+        if any(k.startswith(want) for k in pmc.get("kernels", [])):
             traffic = pmc.get("hbm_bytes_per_launch")
             traffic_src = str(Path(a.pmc_json).relative_to(ROOT)) if Path(a.pmc_json).is_relative_to(ROOT) else a.pmc_json
 
@@ -356,22 +394,25 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic SIFT-shaped (integer-valued f32, 1M x 128), random-seeded; index built in-run",
+            "rows": rows,
+            "data": "synthetic SIFT-shaped (byte-valued f32 records, 1M x 128, as SIFT's .u8bin), random-seeded; "
+                    "index built in-run",
             "recall_at_10": recall,
             **(host or {}),
             "search_mode": modes[0],
             "modes": mode_report,
+            "other_rows": other_rows,
             "ef_sweep": sweep or None,
             "best_at_recall_0.95": max((x for x in sweep if x["recall_at_10"] >= 0.95), key=lambda x: x["value"],
                                        default=None),
             "config": {"workload": "SIFT1M-shaped L2 knn, M=16 efC=200 ef=128 k=10", "n": a.n, "dim": a.dim,
                        "global_batch": a.batch * world, "batch_per_gpu": a.batch, "M": a.M, "efc": a.efc,
                        "ef": a.ef, "k": a.k, "shards": a.shards, "parallelism": f"replica{world}",
-                       "batches_in_flight": len(streams)},
+                       "batches_in_flight": len(streams), "rows": rows},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": ("search_fast_kernel<128,L2,f32,R=2,P=2>" if modes[0] == "fast"
-                                    else "search_kernel<128,L2,f32,0>"), "avg_launch_ms": avg_launch_ms,
+                         "kernel": (f"search_fast_kernel<128,L2,{rows},R=2,P=2>" if modes[0] == "fast"
+                                    else f"search_kernel<128,L2,{rows},0>"), "avg_launch_ms": avg_launch_ms,
                          "span_ms_per_launch": span_ms / a.steps, "batches_in_flight": len(streams),
                          "achieved_basis": "algorithmic bytes of the K timed launches / their GPU span (first "
                                            "launch start to last launch end, HIP events on the launch streams)",

@@ -361,11 +361,41 @@ int fill_copies(ShardedArray& A, const std::vector<int>& devs) {
   return 0;
 }
 
+// Every component is bit for bit the f32 image of a u8 (SHINE_ELEM_U8) / i8 (_I8) value (so -0.0 and NaN never
+// fit): the byte rows then give the kernels exactly the f32 operands the reference's records hold.
+bool fits_bytes(const std::vector<float>& v, int elem) {
+  const float lo = elem == SHINE_ELEM_U8 ? 0.f : -128.f, hi = elem == SHINE_ELEM_U8 ? 255.f : 127.f;
+  for (float x : v) {
+    if (!(x >= lo && x <= hi)) return false;
+    const float r = static_cast<float>(static_cast<int>(x));
+    uint32_t a, b;
+    std::memcpy(&a, &x, 4);
+    std::memcpy(&b, &r, 4);
+    if (a != b) return false;
+  }
+  return true;
+}
+
 // heat (nullable, indexed by graph node): warmup read counts that rank each stripe's level-0 records for the cache
 int make_index(HostGraph G, int elem, const int* gpu_ids, uint32_t n_gpus, int placement, double cache_fraction,
                shine_index_t* out, const std::vector<uint32_t>* heat = nullptr) {
   if (!out) return set_error(SHINE_ERR_ARG, "out is NULL");
-  if (elem != SHINE_ELEM_F32 && elem != SHINE_ELEM_F16) return set_error(SHINE_ERR_ARG, "elem must be 0 (f32) or 1 (f16)");
+  if (elem < SHINE_ELEM_F32 || elem > SHINE_ELEM_AUTO)
+    return set_error(SHINE_ERR_ARG, "elem must be one of SHINE_ELEM_F32 / _F16 / _U8 / _I8 / _AUTO");
+  if (elem == SHINE_ELEM_AUTO || elem_is_byte(elem)) {
+    // byte rows only where they reproduce every component bit for bit (so every distance is unchanged)
+    if (elem == SHINE_ELEM_AUTO) {
+      elem = SHINE_ELEM_F32;
+      for (int b : {SHINE_ELEM_U8, SHINE_ELEM_I8})
+        if (dim_supported(G.L.dim, b) && fits_bytes(G.vec, b)) {
+          elem = b;
+          break;
+        }
+    } else if (!fits_bytes(G.vec, elem)) {
+      return set_error(SHINE_ERR_ARG, std::string("a record component is not exactly a ") +
+                                          (elem == SHINE_ELEM_U8 ? "u8" : "i8") + " value: byte rows would change it");
+    }
+  }
   if (placement != SHINE_PLACE_REPLICA && placement != SHINE_PLACE_SHARDED && placement != SHINE_PLACE_SHARDED_REGIONS)
     return set_error(SHINE_ERR_ARG, "placement must be one of SHINE_PLACE_REPLICA / _SHARDED / _SHARDED_REGIONS");
   if (!(cache_fraction >= 0.0 && cache_fraction <= 1.0))
@@ -424,8 +454,7 @@ int make_index(HostGraph G, int elem, const int* gpu_ids, uint32_t n_gpus, int p
 
   const uint32_t dim = G.L.dim, M0 = h->M0, S = G.n_shards;
   const uint32_t slots = static_cast<uint32_t>(devs.size());
-  const size_t esz = elem == SHINE_ELEM_F16 ? sizeof(__half) : sizeof(float);
-  const uint64_t vrow = dim * esz, arow = 4ull * M0;
+  const uint64_t vrow = row_bytes(dim, elem), arow = 4ull * M0;
   const std::vector<uint64_t>& start = G.shard_start;
 
   // Device id space.  Replica: graph.cc's dense ids.  Sharded: slot o = s % slots owns memory node s; its records
@@ -520,17 +549,20 @@ int make_index(HostGraph G, int elem, const int* gpu_ids, uint32_t n_gpus, int p
   std::vector<uint32_t> inv(h->inv_size, kInvalid);
   for (uint64_t g = 0; g < G.N; ++g) inv[G.uid[g]] = dev_id(static_cast<uint32_t>(g));
 
-  // rows in the device layout (kernels.h permuted_index); config 5 converts records to fp16 at load
+  // rows in the device layout (kernels.h permuted_index / permuted_index_bytes); config 5 converts records to fp16
+  // at load, byte rows narrow them losslessly (checked above)
   std::vector<uint32_t> perm(dim);
-  for (uint32_t i = 0; i < dim; ++i) perm[i] = permuted_index(dim, i);
-  std::vector<uint8_t> vbytes(G.vec.size() * esz);
+  for (uint32_t i = 0; i < dim; ++i) perm[i] = elem_is_byte(elem) ? permuted_index_bytes(dim, i) : permuted_index(dim, i);
+  std::vector<uint8_t> vbytes(G.N * vrow, 0);
   {
     float* fp = reinterpret_cast<float*>(vbytes.data());
     __half* hp = reinterpret_cast<__half*>(vbytes.data());
     for (uint64_t n = 0; n < G.N; ++n) {
       const float* src = G.vec.data() + n * dim;
+      uint8_t* brow = vbytes.data() + n * vrow;
       for (uint32_t i = 0; i < dim; ++i) {
         if (elem == SHINE_ELEM_F16) hp[n * dim + perm[i]] = __float2half(src[i]);
+        else if (elem_is_byte(elem)) brow[perm[i]] = static_cast<uint8_t>(static_cast<int>(src[i]));
         else fp[n * dim + perm[i]] = src[i];
       }
     }
@@ -953,10 +985,11 @@ void print_phase_profile(const shine_index* h, const Replica& R) {  // SHINE_PHA
                  ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6], ph[7], ph[8], ph[9], ph[10], ph[11]);
 }
 
-uint64_t bq_bytes(const shine_index* h, const uint32_t* qs) {  // B_q
-  const uint64_t e = h->elem == SHINE_ELEM_F16 ? 2 : 4;
+// B_q, with the record's stored element width (f32 4, f16 2, byte rows 1) and the f32 query
+uint64_t bq_bytes(const shine_index* h, const uint32_t* qs) {
+  const uint64_t e = elem_bytes(h->elem);
   return qs[SHINE_QS_DISTCOMPS] * h->dim * e + qs[SHINE_QS_LISTS_L0] * (4ull + 4ull * h->M0) +
-         qs[SHINE_QS_LISTS_UPPER] * (4ull + 4ull * h->M) + h->dim * e;
+         qs[SHINE_QS_LISTS_UPPER] * (4ull + 4ull * h->M) + 4ull * h->dim;
 }
 
 uint64_t ref_read_bytes(const shine_index* h, const uint32_t* qs) {  // rdma_reads.hh:12,46 accounting
@@ -1131,7 +1164,7 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
   }
   int rc = SHINE_OK;
   shine_stats agg{};
-  const uint64_t e = h->elem == SHINE_ELEM_F16 ? 2 : 4;
+  const uint64_t e = elem_bytes(h->elem);
   for (uint32_t r = 0; r < G; ++r) {
     const Replica& R = h->reps[r];
     for (size_t j = 0; j < part[r].size(); ++j) {

@@ -102,6 +102,23 @@ __host__ __device__ inline uint32_t permuted_index(uint32_t dim, uint32_t i) {
   return (t >> 1) * 16u + (a >> 1) * 4u + (t & 1u) * 2u + (a & 1u);
 }
 
+// Byte rows (SHINE_ELEM_U8 / _I8): each lane's chunks are contiguous instead, chunk (t/2, c) at byte
+// (c * NCH + t/2) * 4 with NCH = (dim >> 4) chunks per lane, so a lane reads dim/4 contiguous bytes (two 16-byte
+// loads at dim 128) and the 4 lanes of a vector read the row's prefix as one 128-byte run; the tail follows at byte
+// dim >> 4 << 4, and rows are padded to 16 bytes.
+__host__ __device__ inline uint32_t permuted_index_bytes(uint32_t dim, uint32_t i) {
+  const uint32_t db = dim >> 4 << 4;
+  if (i >= db) return i;
+  const uint32_t a = i & 7u, t = i >> 3, nch = dim >> 4;
+  return ((a >> 1) * nch + (t >> 1)) * 4u + (t & 1u) * 2u + (a & 1u);
+}
+inline bool elem_is_byte(int elem) { return elem == 2 || elem == 3; }
+inline uint32_t elem_bytes(int elem) { return elem == 0 ? 4u : elem == 1 ? 2u : 1u; }
+// bytes of one device row
+inline uint64_t row_bytes(uint32_t dim, int elem) {
+  return elem_is_byte(elem) ? (static_cast<uint64_t>(dim) + 15) / 16 * 16 : static_cast<uint64_t>(dim) * elem_bytes(elem);
+}
+
 bool dim_supported(uint32_t dim, int elem);
 
 // The compiled vector dimensions: one translation unit each (kernels_dim.hip built with -DSHINE_DIM=D), so the
@@ -112,6 +129,15 @@ bool dim_supported(uint32_t dim, int elem);
   hipError_t launch_distance_d##DD(int metric, int elem, const DistArgs& a, hipStream_t s);
 SHINE_DIMS(SHINE_DECLARE_DIM)
 #undef SHINE_DECLARE_DIM
+// byte rows: one translation unit per (dimension, signedness), kernels_dim.hip with -DSHINE_BYTES=2 (u8) / 3 (i8)
+#define SHINE_BYTE_DIMS(X) X(100) X(128)
+#define SHINE_DECLARE_BDIM(DD)                                                                                      \
+  hipError_t launch_search_d##DD##_e2(int metric, uint32_t grid, const SearchArgs& a, hipStream_t s);              \
+  hipError_t launch_search_d##DD##_e3(int metric, uint32_t grid, const SearchArgs& a, hipStream_t s);              \
+  hipError_t launch_distance_d##DD##_e2(int metric, const DistArgs& a, hipStream_t s);                             \
+  hipError_t launch_distance_d##DD##_e3(int metric, const DistArgs& a, hipStream_t s);
+SHINE_BYTE_DIMS(SHINE_DECLARE_BDIM)
+#undef SHINE_DECLARE_BDIM
 
 // Returns hipSuccess or the launch error.  grid = number of persistent search slots (one wavefront each).
 hipError_t launch_search(uint32_t dim, int metric, int elem, uint32_t grid, const SearchArgs& a, hipStream_t s);

@@ -10,14 +10,24 @@ bool dim_supported(uint32_t dim, int elem) {
   if (dim == DD) return true;
   if (elem == 0) {
     SHINE_DIMS(SHINE_CASE)
-  } else if (dim == 96 || dim == 128 || dim == 200) {
-    return true;
+  } else if (elem == 1) {
+    return dim == 96 || dim == 128 || dim == 200;
+  } else if (elem_is_byte(elem)) {
+    SHINE_BYTE_DIMS(SHINE_CASE)
   }
 #undef SHINE_CASE
   return false;
 }
 
 hipError_t launch_search(uint32_t dim, int metric, int elem, uint32_t grid, const SearchArgs& a, hipStream_t s) {
+  if (elem_is_byte(elem)) {
+#define SHINE_CASE(DD)                                                                                     \
+  if (dim == DD)                                                                                           \
+    return elem == 2 ? launch_search_d##DD##_e2(metric, grid, a, s) : launch_search_d##DD##_e3(metric, grid, a, s);
+    SHINE_BYTE_DIMS(SHINE_CASE)
+#undef SHINE_CASE
+    return hipErrorInvalidValue;
+  }
 #define SHINE_CASE(DD) \
   if (dim == DD) return launch_search_d##DD(metric, elem, grid, a, s);
   SHINE_DIMS(SHINE_CASE)
@@ -26,6 +36,13 @@ hipError_t launch_search(uint32_t dim, int metric, int elem, uint32_t grid, cons
 }
 
 hipError_t launch_distance(uint32_t dim, int metric, int elem, const DistArgs& a, hipStream_t s) {
+  if (elem_is_byte(elem)) {
+#define SHINE_CASE(DD) \
+  if (dim == DD) return elem == 2 ? launch_distance_d##DD##_e2(metric, a, s) : launch_distance_d##DD##_e3(metric, a, s);
+    SHINE_BYTE_DIMS(SHINE_CASE)
+#undef SHINE_CASE
+    return hipErrorInvalidValue;
+  }
 #define SHINE_CASE(DD) \
   if (dim == DD) return launch_distance_d##DD(metric, elem, a, s);
   SHINE_DIMS(SHINE_CASE)

@@ -61,6 +61,8 @@ __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
 
 __device__ __forceinline__ float to_f32(float x) { return x; }
 __device__ __forceinline__ float to_f32(__half x) { return __half2float(x); }
+__device__ __forceinline__ float to_f32(uint8_t x) { return static_cast<float>(x); }
+__device__ __forceinline__ float to_f32(int8_t x) { return static_cast<float>(x); }
 
 // ------------------------------------------------------------------------------------------------------------
 // Heaps of packed {dist, id} entries in LDS.
@@ -258,7 +260,14 @@ __device__ __forceinline__ void load_query(const float* __restrict__ q, int lane
   for (int t = 0; t < TAIL; ++t) Q.qt[t] = q[DB + t];
 }
 
-// One chunk = elements (t, t+1) of accumulators (2c, 2c+1): f32 → 4 floats, f16 → 4 halves in 2 words.
+// One chunk = elements (t, t+1) of accumulators (2c, 2c+1): f32 → 4 floats, f16 → 4 halves in 2 words, bytes →
+// one word.
+template <typename E>
+constexpr bool kByte = std::is_same_v<E, uint8_t> || std::is_same_v<E, int8_t>;
+// elements of one device row (byte rows are padded to 16 bytes, kernels.h row_bytes)
+template <int D, typename E>
+constexpr int kRowElems = kByte<E> ? (D + 15) / 16 * 16 : D;
+
 template <typename E>
 struct ChunkT {
   using type = f32x4;
@@ -269,25 +278,72 @@ struct ChunkT<__half> {
 };
 
 // The neighbour vectors of P passes (16 slots each) in VGPRs.
-template <int D, typename E, int P>
+template <int D, typename E, int P, bool BYTES = kByte<E>>
 struct NbrBuf {
   using L = Lay<D, E>;
   typename ChunkT<E>::type x[P][L::NCH];
   float xt[P][L::TAILA];  // scalar tail, lane c = 3 only
 };
+// Byte rows: the lane's NCH chunk words (contiguous in the row, kernels.h permuted_index_bytes) and the tail bytes
+// as whole words; widened to f32 where the distances consume them.
+template <int D, typename E, int P>
+struct NbrBuf<D, E, P, true> {
+  using L = Lay<D, E>;
+  static constexpr int TW = L::TAIL > 0 ? (L::TAIL + 3) / 4 : 1;
+  u32 x[P][L::NCH];
+  u32 xt[P][TW];
+};
+
+// This lane's part of one byte row: NCH words at byte c4 * NCH * 4 in the widest aligned loads, then the tail words.
+template <int D, typename E, int P>
+__device__ __forceinline__ void load_byte_row(NbrBuf<D, E, P>& B, int p, const E* __restrict__ row, int c4) {
+  using L = Lay<D, E>;
+  constexpr int NCH = L::NCH;
+  const unsigned char* rb = reinterpret_cast<const unsigned char*>(row);
+  const unsigned char* base = rb + c4 * NCH * 4;
+  if constexpr (NCH % 4 == 0) {
+#pragma unroll
+    for (int v = 0; v < NCH / 4; ++v) {
+      const uint4 w = reinterpret_cast<const uint4*>(base)[v];
+      B.x[p][4 * v] = w.x;
+      B.x[p][4 * v + 1] = w.y;
+      B.x[p][4 * v + 2] = w.z;
+      B.x[p][4 * v + 3] = w.w;
+    }
+  } else if constexpr (NCH % 2 == 0) {
+#pragma unroll
+    for (int v = 0; v < NCH / 2; ++v) {
+      const uint2 w = reinterpret_cast<const uint2*>(base)[v];
+      B.x[p][2 * v] = w.x;
+      B.x[p][2 * v + 1] = w.y;
+    }
+  } else {
+#pragma unroll
+    for (int v = 0; v < NCH; ++v) B.x[p][v] = reinterpret_cast<const u32*>(base)[v];
+  }
+  if constexpr (L::TAIL > 0) {
+    const u32* tw = reinterpret_cast<const u32*>(rb + L::DB);
+#pragma unroll
+    for (int t = 0; t < NbrBuf<D, E, P>::TW; ++t) B.xt[p][t] = tw[t];
+  }
+}
 
 // Issue the loads of pass p: this lane's group evaluates node `id` (INV: nothing to load).
 template <int D, typename E, int P>
 __device__ __forceinline__ void issue_pass(NbrBuf<D, E, P>& B, int p, const E* __restrict__ vec, u32 id, int c4) {
   using L = Lay<D, E>;
-  using C = typename ChunkT<E>::type;
   if (id != INV) {
-    const E* row = vec + static_cast<u64>(id) * D;
+    const E* row = vec + static_cast<u64>(id) * kRowElems<D, E>;
+    if constexpr (kByte<E>) {
+      load_byte_row<D, E, P>(B, p, row, c4);
+    } else {
+      using C = typename ChunkT<E>::type;
 #pragma unroll
-    for (int u = 0; u < L::NCH; ++u) B.x[p][u] = *reinterpret_cast<const C*>(row + u * 16 + c4 * 4);
-    if (c4 == 3) {
+      for (int u = 0; u < L::NCH; ++u) B.x[p][u] = *reinterpret_cast<const C*>(row + u * 16 + c4 * 4);
+      if (c4 == 3) {
 #pragma unroll
-      for (int t = 0; t < L::TAIL; ++t) B.xt[p][t] = to_f32(row[L::DB + t]);
+        for (int t = 0; t < L::TAIL; ++t) B.xt[p][t] = to_f32(row[L::DB + t]);
+      }
     }
   }
 }
@@ -298,12 +354,23 @@ template <int D, typename E, int P>
 __device__ __forceinline__ void issue_pass_u(NbrBuf<D, E, P>& B, int p, const E* __restrict__ vec, u32 id, u32 pad,
                                              int c4) {
   using L = Lay<D, E>;
-  using C = typename ChunkT<E>::type;
-  const E* row = vec + static_cast<u64>(id == INV ? pad : id) * D;
+  const E* row = vec + static_cast<u64>(id == INV ? pad : id) * kRowElems<D, E>;
+  if constexpr (kByte<E>) {
+    load_byte_row<D, E, P>(B, p, row, c4);
+  } else {
+    using C = typename ChunkT<E>::type;
 #pragma unroll
-  for (int u = 0; u < L::NCH; ++u) B.x[p][u] = *reinterpret_cast<const C*>(row + u * 16 + c4 * 4);
+    for (int u = 0; u < L::NCH; ++u) B.x[p][u] = *reinterpret_cast<const C*>(row + u * 16 + c4 * 4);
 #pragma unroll
-  for (int t = 0; t < L::TAIL; ++t) B.xt[p][t] = to_f32(row[L::DB + t]);
+    for (int t = 0; t < L::TAIL; ++t) B.xt[p][t] = to_f32(row[L::DB + t]);
+  }
+}
+
+// byte i of word w widened to f32 (exact): v_cvt_f32_ubyte{i} for u8, a sign-extending extract + convert for i8
+template <typename E>
+__device__ __forceinline__ float byte_f32(u32 w, int i) {
+  if constexpr (std::is_same_v<E, uint8_t>) return static_cast<float>((w >> (8 * i)) & 0xFFu);
+  else return static_cast<float>(static_cast<int>(w << (24 - 8 * i)) >> 24);
 }
 
 __device__ __forceinline__ f32x2 half2_to_f32x2(u32 w) {
@@ -363,6 +430,10 @@ __device__ __forceinline__ void pass_dists(const QueryRegs<D>& Q, const NbrBuf<D
       if constexpr (std::is_same_v<E, float>) {
         x0 = B.x[p][u].xy;
         x1 = B.x[p][u].zw;
+      } else if constexpr (kByte<E>) {
+        const u32 w = B.x[p][u];
+        x0 = f32x2{byte_f32<E>(w, 0), byte_f32<E>(w, 1)};
+        x1 = f32x2{byte_f32<E>(w, 2), byte_f32<E>(w, 3)};
       } else {
         x0 = half2_to_f32x2(B.x[p][u].x);
         x1 = half2_to_f32x2(B.x[p][u].y);
@@ -372,7 +443,16 @@ __device__ __forceinline__ void pass_dists(const QueryRegs<D>& Q, const NbrBuf<D
     }
   }
 #pragma unroll
-  for (int p = 0; p < P; ++p) out[p] = add_tail<D, METRIC>(Q, B.xt[p], fold8(acc[p]));
+  for (int p = 0; p < P; ++p) {
+    if constexpr (kByte<E>) {
+      float xt[L::TAILA];
+#pragma unroll
+      for (int t = 0; t < L::TAILA; ++t) xt[t] = L::TAIL > 0 ? byte_f32<E>(B.xt[p][t >> 2], t & 3) : 0.f;
+      out[p] = add_tail<D, METRIC>(Q, xt, fold8(acc[p]));
+    } else {
+      out[p] = add_tail<D, METRIC>(Q, B.xt[p], fold8(acc[p]));
+    }
+  }
 }
 
 // sc_d[j] = dist(q, vec[sc_ids[j]]) for j < n.  All 64 lanes must call it.

@@ -16,7 +16,7 @@ HEADER = REPO_ROOT / "include" / "shine_gpu.h"
 
 OK, ERR_ARG, ERR_IO, ERR_FORMAT, ERR_HIP, ERR_NOMEM, ERR_OVERFLOW = range(7)
 METRIC_L2, METRIC_IP = 0, 1
-ELEM_F32, ELEM_F16 = 0, 1
+ELEM_F32, ELEM_F16, ELEM_U8, ELEM_I8, ELEM_AUTO = 0, 1, 2, 3, 4
 QS_DISTCOMPS, QS_VISITED_UPPER, QS_VISITED_L0, QS_LISTS_UPPER, QS_LISTS_L0, QS_MAX_NEXT, QS_STATUS, QS_NRESULT = range(8)
 QS_REMOTE_VEC, QS_REMOTE_LIST, QS_CACHED_VEC, QS_CACHED_LIST = range(8, 12)
 QS_WORDS = 12

@@ -34,6 +34,15 @@ extern "C" {
 
 #define SHINE_ELEM_F32 0 /* element_t = f32 (src/common/types.hh:9) */
 #define SHINE_ELEM_F16 1 /* vectors converted to fp16 at load (config 5); distances still accumulate in f32 */
+/* Byte rows: lossless narrow storage of records whose every component is exactly a byte value, as the reference's
+ * .u8bin / .i8bin inputs are before read_data converts them element-wise to f32 (read_data.hh:21-28,
+ * deserializer.hh:24-44).  The kernels widen each byte back to f32 and run the same f32 distance arithmetic, so
+ * results are bitwise those of SHINE_ELEM_F32; a record with any other component value is SHINE_ERR_ARG at open.
+ * Rows are padded to 16 bytes.  Compiled for dim 100 and 128 (SPACEV-style i8, SIFT/BIGANN-style u8). */
+#define SHINE_ELEM_U8 2  /* components in {0, ..., 255} */
+#define SHINE_ELEM_I8 3  /* components in {-128, ..., 127} */
+/* The narrowest lossless of U8, I8 and F32 for this index (never F16); shine_index_info.elem reports the choice. */
+#define SHINE_ELEM_AUTO 4
 
 /* Per-query counter layout (u32 words), identical in the oracle and on the GPU. */
 #define SHINE_QS_DISTCOMPS 0     /* stats.distcomps                         (hnsw.hh:272,286,376,459) */

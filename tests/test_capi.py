@@ -118,3 +118,37 @@ def test_null_arguments_are_arg_errors():
 def test_algorithmic_bytes_formula_needs_handle():
     qs = np.zeros((2, 8), np.uint32)
     assert L.lib().shine_algorithmic_bytes(None, qs.ctypes.data_as(C.c_void_p), 2) == 0
+
+
+def test_byte_rows_refuse_components_they_would_change(small_dumps):
+    """SHINE_ELEM_U8 / _I8 store a record only if every component is exactly a byte value (checked before any
+    device work): sift-like records exceed 127 (not i8), deep-like records are fractions (neither)."""
+    with pytest.raises(shine_amd.ShineError) as e:
+        shine_amd.Index.from_buffers(small_dumps, 128, 8, 0, elem=L.ELEM_I8, gpus=[0])
+    assert e.value.code == L.ERR_ARG and "i8" in str(e.value)
+    deep, _, _ = O.build(D.deep_like(300, seed=2, d=128), 8, 32, 0, 1, seed=3)
+    with pytest.raises(shine_amd.ShineError) as e:
+        shine_amd.Index.from_buffers(deep, 128, 8, 0, elem=L.ELEM_U8, gpus=[0])
+    assert e.value.code == L.ERR_ARG and "u8" in str(e.value)
+    with pytest.raises(shine_amd.ShineError) as e:
+        shine_amd.Index.from_buffers(small_dumps, 128, 8, 0, elem=5, gpus=[0])
+    assert e.value.code == L.ERR_ARG
+
+
+def test_byte_row_layout_is_lane_contiguous():
+    """kernels.h permuted_index_bytes: element a + 8t of the 16-aligned prefix at byte ((a>>1)*NCH + t//2)*4 +
+    (t&1)*2 + (a&1), NCH = dim >> 4 (each of the 4 lanes of a vector reads dim/4 contiguous bytes); restated here
+    and checked to be a permutation of the prefix with the tail in place."""
+    for dim in (100, 128):
+        nch = dim >> 4
+        pos = []
+        for i in range(dim):
+            if i >= dim >> 4 << 4:
+                pos.append(i)
+                continue
+            a, t = i & 7, i >> 3
+            pos.append(((a >> 1) * nch + (t >> 1)) * 4 + (t & 1) * 2 + (a & 1))
+        assert sorted(pos) == list(range(dim))
+        # lane c's chunks: accumulators 2c, 2c+1 only
+        for i in range(dim >> 4 << 4):
+            assert pos[i] // (4 * nch) == (i & 7) >> 1
