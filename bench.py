@@ -4,9 +4,10 @@
 Workload (one "step" = one batch): 1,024 queries through HNSW::knn (k=10, ef=128) against a 1M x 128-d L2 index
 built with M=16, efC=200 by the parallel restatement of HNSW::insert, in the reference's dump layout.  Data are
 synthetic SIFT-shaped vectors (shine_amd.datasets.sift_like; no datasets can be fetched).  Queries and outputs
-are resident in HBM when the timed region starts; value = queries / wall time over exactly K steps.  Two batches
-are in flight per GPU (--inflight; step i is enqueued on HIP stream i % 2), as a serving loop keeps them: the
-last, longest queries of one batch overlap the first of the next instead of leaving CUs idle.
+are resident in HBM when the timed region starts; value = queries / wall time over exactly K steps.  Four batches
+are in flight per GPU (--inflight; step i is enqueued on HIP stream i % 4, one per hardware queue of HIP's default
+four), as a serving loop keeps them: the last, longest queries of one batch overlap the next batches' first ones
+instead of leaving CUs idle (profiles/r02/inflight_scan_*.jsonl: 2 → 4 in flight is +27 % at ef = 128).
 
 Multi-GPU (torchrun, one process per GPU): every rank holds a full replica of the 0.75 GiB index and answers its
 own batches (queries split id % G, read_data.hh:57-58) — weak scaling, no data-path collective.  Rank 0 builds
@@ -103,7 +104,7 @@ def parse():
     p.add_argument("--n", type=int, default=1_000_000)
     p.add_argument("--dim", type=int, default=128)
     p.add_argument("--batch", type=int, default=1024)
-    p.add_argument("--nbatches", type=int, default=10, help="distinct query batches per rank (cycled)")
+    p.add_argument("--nbatches", type=int, default=12, help="distinct query batches per rank (cycled)")
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--ef", type=int, default=128)
     p.add_argument("--M", type=int, default=16)
@@ -111,7 +112,7 @@ def parse():
     p.add_argument("--shards", type=int, default=1, help="memory-node dumps the index is spread over")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of the CPU-baseline sample")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--inflight", type=int, default=2,
+    p.add_argument("--inflight", type=int, default=4,
                    help="query batches in flight per GPU, each on its own HIP stream (step i runs on stream i %% S), "
                         "so one batch's last queries overlap the next batch's first")
     p.add_argument("--ef-sweep", default="32,48,64,96",

@@ -709,13 +709,13 @@ LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds
     return std::min<uint64_t>(target, lds_per_cu / search_fast_lds_bytes(t, ef, entry_bytes));
   };
   const uint32_t t32 = table_for(4), t16 = table_for(2);
-  const bool can16 = env_int("SHINE_DEBUG_VIS16", 1) != 0 && bits <= log2u(t16) + 11;
+  const bool can16 = env_int("SHINE_DEBUG_VIS16", 1) != 0 && bits <= log2u(t16) + 10;
   const uint64_t w32 = resident(t32, 4), w16 = can16 ? resident(t16, 2) : 0;
   sh.vis16 = can16 && (w16 > w32 || (w16 == w32 && t16 > t32)) ? 1 : 0;
   if (env_int("SHINE_DEBUG_VIS16", -1) == 1 && can16) sh.vis16 = 1;  // test hook: force the u16 entries
   sh.vis_cap = sh.vis16 ? t16 : t32;
   sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
-  if (sh.vis16 && bits > log2u(sh.vis_cap) + 11) sh.vis16 = 0;  // a forced small table: back to u32 entries
+  if (sh.vis16 && bits > log2u(sh.vis_cap) + 10) sh.vis16 = 0;  // a forced small table: back to u32 entries
   sh.vis_bits = std::max(bits, log2u(sh.vis_cap) + 1);
   const uint64_t need = search_fast_lds_bytes(sh.vis_cap, ef, sh.vis16 ? 2 : 4);
   const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(lds_per_cu / need));
@@ -766,7 +766,7 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
     const uint32_t w16 = waves(search_lds_bytes(ef, 5 * ef, sh.vis_cap, 2));
     uint32_t bits = 14;
     while (bits < 32 && (1ull << bits) < h->id_space) ++bits;
-    const bool can16 = env_int("SHINE_DEBUG_VIS16", 1) != 0 && bits <= log2_ceil(sh.vis_cap) + 11;
+    const bool can16 = env_int("SHINE_DEBUG_VIS16", 1) != 0 && bits <= log2_ceil(sh.vis_cap) + 10;
     sh.vis16 = can16 && (w16 > w32 || env_int("SHINE_DEBUG_VIS16", -1) == 1) ? 1 : 0;
     sh.vis_bits = std::max(bits, log2_ceil(sh.vis_cap) + 1);
     wpc = sh.vis16 ? w16 : w32;

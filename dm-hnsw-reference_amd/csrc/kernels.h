@@ -59,7 +59,7 @@ struct SearchArgs {
   uint32_t sort_out;        // heap kernel writes ascending order (fast-mode fixup passes)
   uint32_t global_heaps;    // 1: heap kernel with both heaps in HBM (last fallback pass; vis_cap must be 0)
   uint32_t vis16;           // LDS visited table of u16 quotient entries (kernels_impl.h VisitedLds<1>)
-  uint32_t vis_bits;        // ... bits of the id space the multiply permutes (vis_bits - log2(vis_cap) <= 11)
+  uint32_t vis_bits;        // ... bits of the id space the multiply permutes (vis_bits - log2(vis_cap) <= 10: buckets of 8, >= 3 distance bits)
   uint32_t vis_mul;         // ... odd multiplier
 };
 

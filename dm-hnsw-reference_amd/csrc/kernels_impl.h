@@ -95,6 +95,36 @@ __device__ __forceinline__ u64 heap_push(u64* h, int n, u64 v, u64 root0, int la
   return fin == 0 ? v : root0;
 }
 
+// heap_push on next_candidates (min-heap `hn`, size nn) and on top_candidates (max-heap `ht`, size nt) in one LDS
+// round: lanes 0..31 play hn's ancestors, lanes 32..63 ht's.  The two heaps are independent, so this is the two
+// std::push_heap calls in either order, at the LDS latency of one.
+__device__ __forceinline__ void heap_push2(u64* hn, int nn, u64* ht, int nt, u64 v, u64& root_n, u64& root_t,
+                                           int lane) {
+  const bool second = lane >= 32;
+  const int l = lane & 31;
+  u64* h = second ? ht : hn;
+  const int n = second ? nt : nn;
+  const float vd = key(v);
+  const int L = 31 - __clz(n + 1);
+  u64 ent = 0;
+  bool c = false;
+  if (l < L) {
+    ent = h[((n + 1) >> (l + 1)) - 1];
+    c = second ? hcmp<true>(key(ent), vd) : hcmp<false>(key(ent), vd);
+  }
+  const u64 C = __ballot(c);
+  const int sn = static_cast<int>(__builtin_ctz(~static_cast<u32>(C)));
+  const int st = static_cast<int>(__builtin_ctz(~static_cast<u32>(C >> 32)));
+  const int s = second ? st : sn;
+  if (l < s) h[l == 0 ? n : ((n + 1) >> l) - 1] = ent;
+  const int fin = s == 0 ? n : ((n + 1) >> s) - 1;
+  if (l == 0) h[fin] = v;
+  wave_sync();
+  const int fin_n = sn == 0 ? nn : ((nn + 1) >> sn) - 1, fin_t = st == 0 ? nt : ((nt + 1) >> st) - 1;
+  if (fin_n == 0) root_n = v;
+  if (fin_t == 0) root_t = v;
+}
+
 // General form (any keys, NaN included): the value's landing slot is found bottom-up like std::__push_heap.
 // std::pop_heap on h[0..n) followed by pop_back  ≡  std::__adjust_heap(h, 0, n-1, h[n-1]).  Returns the new
 // root (meaningless when n <= 1).
@@ -683,6 +713,8 @@ struct VisitedLds<0> {
   __device__ __forceinline__ VisitedLds(void* base, const SearchArgs& A)
       : t(static_cast<u32*>(base)), mask(A.vis_cap - 1), shift(32 - (31 - __clz(static_cast<int>(A.vis_cap)))) {}
   static constexpr u32 kBytes = 4;
+  using Hint = u32;  // the id's home word
+  static __device__ __forceinline__ Hint unknown() { return INV; }
   __device__ __forceinline__ void clear(const SearchArgs& A, int lane) {
     uint4* t4 = reinterpret_cast<uint4*>(t);
     for (u32 i = lane; i < A.vis_cap / 4; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
@@ -716,11 +748,11 @@ struct VisitedLds<0> {
 template <>
 struct VisitedLds<1> {
   u32* t;
-  unsigned short* t16;
-  u32 mask, mul, bmask, rbits, rmask, dbits, dmax;
-  __device__ __forceinline__ VisitedLds(void* base, const SearchArgs& A)
-      : t(static_cast<u32*>(base)), t16(static_cast<unsigned short*>(base)), mask(A.vis_cap - 1), mul(A.vis_mul) {
-    const u32 tb = 31 - __clz(static_cast<int>(A.vis_cap));
+  u32 bmask_b, mul, bmask, rbits, rmask, dbits, dmax;
+  using Hint = uint4;  // a copy of the id's home bucket (4 words, 8 entries)
+  __device__ __forceinline__ VisitedLds(void* base, const SearchArgs& A) : t(static_cast<u32*>(base)), mul(A.vis_mul) {
+    const u32 tb = 31 - __clz(static_cast<int>(A.vis_cap >> 3));  // buckets of 8 entries
+    bmask_b = (A.vis_cap >> 3) - 1;
     bmask = A.vis_bits >= 32 ? ~0u : (1u << A.vis_bits) - 1;
     rbits = A.vis_bits - tb;
     rmask = (1u << rbits) - 1;
@@ -728,51 +760,65 @@ struct VisitedLds<1> {
     dmax = (1u << dbits) - 2;  // an all-ones entry is the empty marker
   }
   static constexpr u32 kBytes = 2;
+  // not read yet: assume an empty bucket (a wrong guess costs one failed compare-and-swap and a read)
+  static __device__ __forceinline__ Hint unknown() { return make_uint4(INV, INV, INV, INV); }
   __device__ __forceinline__ void clear(const SearchArgs& A, int lane) {
     uint4* t4 = reinterpret_cast<uint4*>(t);
     for (u32 i = lane; i < A.vis_cap / 8; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
   }
   __device__ __forceinline__ u32 image(u32 x) const { return (x * mul) & bmask; }
-  __device__ __forceinline__ void insert_first(u32 x) {
+  __device__ __forceinline__ void insert_first(u32 x) {  // the table is empty: entry 0 of the home bucket
     const u32 h = image(x);
-    t16[h >> rbits] = static_cast<unsigned short>((h & rmask) << dbits);
+    t[(h >> rbits) * 4] = 0xFFFF0000u | ((h & rmask) << dbits);
   }
-  __device__ __forceinline__ bool at_home(u32 x) const {
+  __device__ __forceinline__ uint4 bucket(u32 b) const { return reinterpret_cast<const uint4*>(t)[b]; }
+  static __device__ __forceinline__ bool has(u32 w, u32 e) { return (w & 0xFFFFu) == e || (w >> 16) == e; }
+  static __device__ __forceinline__ bool has(const uint4& w, u32 e) { return (has(w.x, e) || has(w.y, e)) || (has(w.z, e) || has(w.w, e)); }
+  // the home bucket (one ds_read_b128); home_match: x sits in it
+  __device__ __forceinline__ Hint probe(u32 x) const { return bucket(image(x) >> rbits); }
+  __device__ __forceinline__ bool home_match(u32 x, const Hint& w) const {
     const u32 h = image(x);
-    return t16[h >> rbits] == static_cast<unsigned short>((h & rmask) << dbits);
+    return has(w, (h & rmask) << dbits);
   }
-  __device__ __forceinline__ u32 probe(u32 x) const { return t[(image(x) >> rbits) >> 1]; }
-  __device__ __forceinline__ bool home_match(u32 x, u32 w) const {
-    const u32 h = image(x), s = h >> rbits;
-    return ((w >> ((s & 1u) << 4)) & 0xFFFFu) == ((h & rmask) << dbits);
-  }
-  // hint: the home word as probe() read it (INV: unknown); the first compare-and-swap expects it
-  __device__ __forceinline__ bool test_and_set(u32 x, bool& ovf, u32 hint = INV) {
+  // Buckets of 8 entries, probed linearly: x's entry (its remainder and its bucket's distance from home) is looked for
+  // in one bucket read at a time and goes to the bucket's first empty entry.  Entries are never removed, so a bucket
+  // with an empty entry ends the search.  cur: the home bucket as last read (probe) or unknown().
+  __device__ __forceinline__ bool test_and_set(u32 x, bool& ovf, Hint cur = unknown()) {
     const u32 h = image(x);
-    u32 s = h >> rbits, disp = 0, cur = hint;  // first attempt: the home word as last seen (INV: assumed empty)
+    u32 b = h >> rbits, disp = 0;
     const u32 rem = (h & rmask) << dbits;
     bool fresh = false;
     for (;;) {
-      const u32 sh = (s & 1u) << 4;
-      const u32 half = (cur >> sh) & 0xFFFFu;
-      const u32 entry = rem | disp;
-      if (half == 0xFFFFu) {
-        const u32 want = (cur & ~(0xFFFFu << sh)) | (entry << sh);
-        const u32 old = atomicCAS(&t[s >> 1], cur, want);
-        if (old == cur) {
+      const u32 e = rem | disp;
+      if (has(cur, e)) break;  // same bucket distance, same remainder: this id
+      // first empty entry in bucket order: word j, high half k
+      const u32 w[4] = {cur.x, cur.y, cur.z, cur.w};
+      int j = -1;
+      u32 k = 0;
+#pragma unroll
+      for (int i = 3; i >= 0; --i) {
+        const bool lo = (w[i] & 0xFFFFu) == 0xFFFFu, hi = (w[i] >> 16) == 0xFFFFu;
+        if (lo | hi) {
+          j = i;
+          k = lo ? 0u : 1u;
+        }
+      }
+      if (j >= 0) {
+        const u32 old_w = j == 0 ? cur.x : j == 1 ? cur.y : j == 2 ? cur.z : cur.w;
+        const u32 want = k ? ((old_w & 0xFFFFu) | (e << 16)) : ((old_w & 0xFFFF0000u) | e);
+        if (atomicCAS(&t[b * 4 + static_cast<u32>(j)], old_w, want) == old_w) {
           fresh = true;
           break;
         }
-        cur = old;  // the word was not as assumed: look at this slot again
+        cur = bucket(b);  // the bucket changed under us (or was not as guessed): read it
         continue;
       }
-      if (half == entry) break;  // same home, same remainder: this id
-      s = (s + 1) & mask;
+      b = (b + 1) & bmask_b;  // full bucket: the next one
       if (++disp > dmax) {
         ovf = true;
         break;
       }
-      if ((s & 1u) == 0) cur = INV;  // a new word: assume it empty again
+      cur = bucket(b);
     }
     return fresh;
   }
@@ -967,12 +1013,11 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
             if (nnext >= cap) { status = ST_OVERFLOW; break; }
             const u32 id = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(my_id), j));
             const u64 en = mk(d, id);
-            PHASE(8)
-            nroot = heap_push<false>(nxt, nnext, en, nroot, lane);
-            hfence();
-            if (ntop < ef) {  // heap.hh:34-41 push_k
+            // next_candidates.push (:462) and top_candidates.push_k (heap.hh:34-41) touch different heaps: the
+            // pop of a full top goes first, then both pushes share one LDS round (heap_push2)
+            if (ntop < ef) {
               PHASE(10)
-              troot = heap_push<true>(top, ntop, en, troot, lane);
+              heap_push2(nxt, nnext, top, ntop, en, nroot, troot, lane);
               hfence();
               ++ntop;
             } else {  // d < top().distance holds: it is the accept test with the top full
@@ -980,7 +1025,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
               troot = nan_keys ? heap_pop_any<true>(top, ntop, lane) : heap_pop<true>(top, ntop, lane);
               hfence();
               PHASE(10)
-              troot = heap_push<true>(top, ntop - 1, en, troot, lane);
+              heap_push2(nxt, nnext, top, ntop - 1, en, nroot, troot, lane);
               hfence();
             }
             PHASE(6)
@@ -1183,7 +1228,8 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
     u32 nid = nn;
     u32 nrow = load_row(nn);
     u32 cur = nn;  // the candidate whose list `e` is
-    u32 ehint = INV;  // this lane's home word of e as probed one expansion earlier (VisitedLds::test_and_set)
+    typename VisitedLds<VT>::Hint ehint = VisitedLds<VT>::unknown();  // e's home word / bucket as probed one
+                                                                      // expansion earlier (VisitedLds::test_and_set)
 
     while (status == 0) {
       ++st_ll0;  // read_neighborlist (:436-438)
@@ -1259,7 +1305,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       const u32 prow = pid == r_id ? nrow : load_row(pid != INV ? pid : pad);  // a fresh f*: its list now
       // an entry already at its home slot of the visited table is not fresh: its row is not requested (one
       // read-only LDS probe; the visit proper still runs at the top of the next expansion)
-      const u32 pword = in_row && prow != INV ? vis.probe(prow) : INV;
+      const typename VisitedLds<VT>::Hint pword = in_row && prow != INV ? vis.probe(prow) : VisitedLds<VT>::unknown();
       const bool seen = in_row && prow != INV && vis.home_match(prow, pword);
       issue_list<D, E, P>(X, vec, seen ? INV : prow, pad, c4);
 
@@ -1367,7 +1413,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       nid = c2 != INV ? c2 : c;
       nrow = load_row(nid);  // unconditional: always the youngest load
       e = erow;
-      ehint = c != pid ? INV : pword;  // the probe read prow's home words, and no insert has happened since
+      ehint = c != pid ? VisitedLds<VT>::unknown() : pword;  // the probe read prow's home bucket, no insert since
       cur = c;
       r_id = c2;
       r_key = k2;
