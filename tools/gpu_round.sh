@@ -5,6 +5,7 @@ set -o pipefail
 TAG=${1:-run}; STEPS=${2:-20}
 O=gpurun_out/$TAG; mkdir -p $O
 export TMPDIR=/tmp
+export GPU_MAX_HW_QUEUES=8  # as bench.py sets for itself: under rocprofv3 HIP may start before bench.py runs
 timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -30 $O/gpu_tests.log; exit 1; }
 tail -3 $O/gpu_tests.log
 timeout -k 10 500 python -u bench.py --steps $STEPS --warmup 5 > $O/bench.json 2> $O/bench.log || { echo bench failed; tail -30 $O/bench.log; exit 1; }
