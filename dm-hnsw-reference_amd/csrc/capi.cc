@@ -721,7 +721,9 @@ LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds
   const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(lds_per_cu / need));
   const uint32_t wpc = std::max<uint32_t>(1, std::min<uint32_t>({(nq + cus - 1) / cus, 16u, fit}));
   sh.cap = 0;
-  sh.vis_limit = sh.vis_cap / 8 * 7;
+  // test hook: the table's load limit in 1/1000 (a query that visits more goes to the light pass)
+  const int64_t load = env_int("SHINE_DEBUG_VISLOAD", 875);
+  sh.vis_limit = static_cast<uint32_t>(std::min<int64_t>(sh.vis_cap - 64, static_cast<int64_t>(sh.vis_cap) * load / 1000));
   sh.grid = std::max<uint32_t>(1, std::min<uint32_t>(nq, cus * wpc));
   return sh;
 }

@@ -3,7 +3,7 @@
 
 For every setting: QPS over --steps batches with --inflight batches on as many streams, and the share of queries the
 main pass handed on to the light pass (shine_knn_batch's overflow_retries over one batch).  Settings are
-'rows:inflight:viscap' (viscap 0 = the library's own choice), e.g. --settings f32:2:0,u8:3:4096.
+'rows:inflight:viscap[:load]' (viscap 0 = the library's own choice; load: SHINE_DEBUG_VISLOAD), e.g. --settings f32:2:0,u8:3:4096.
 """
 from __future__ import annotations
 
@@ -54,8 +54,12 @@ def main():
     idx = {}
     lines = []
     for spec in a.settings.split(","):
-        rows, inflight, viscap = spec.split(":")
+        rows, inflight, viscap, *rest = spec.split(":")
         inflight, viscap = int(inflight), int(viscap)
+        if rest:
+            os.environ["SHINE_DEBUG_VISLOAD"] = rest[0]
+        else:
+            os.environ.pop("SHINE_DEBUG_VISLOAD", None)
         if rows not in idx:
             elem = shine_amd.ELEM_U8 if rows == "u8" else shine_amd.ELEM_F32
             idx[rows] = shine_amd.Index.open(paths, 128, 16, shine_amd.METRIC_L2, elem=elem, gpus=[0])
