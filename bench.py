@@ -5,8 +5,8 @@ Workload (one "step" = one batch): 1,024 queries through HNSW::knn (k=10, ef=128
 built with M=16, efC=200 by the parallel restatement of HNSW::insert, in the reference's dump layout.  Data are
 synthetic SIFT-shaped vectors (shine_amd.datasets.sift_like; no datasets can be fetched).  Queries and outputs
 are resident in HBM when the timed region starts; value = queries / wall time over exactly K steps.  Four batches
-are in flight per GPU (--inflight; step i is enqueued on HIP stream i % 4, one per hardware queue of HIP's default
-four), as a serving loop keeps them: the last, longest queries of one batch overlap the next batches' first ones
+are in flight per GPU (--inflight; step i is enqueued on HIP stream i % 4, each on a hardware queue of its own),
+as a serving loop keeps them: the last, longest queries of one batch overlap the next batches' first ones
 instead of leaving CUs idle (profiles/r02/inflight_scan_*.jsonl: 2 → 4 in flight is +27 % at ef = 128).
 
 Multi-GPU (torchrun, one process per GPU): every rank holds a full replica of the 0.75 GiB index and answers its
@@ -15,8 +15,9 @@ the index once and shares the dump files; the max over ranks of the timed wall t
 
 Also reported: `roofline` for the search kernel (algorithmic bytes of the K launches / their GPU span from HIP
 events vs 8 TB/s; `avg_launch_ms` is the per-launch event time, which rocprofv3's average duration matches),
-`value_host_to_host` (SURVEY §8d's query phase: pinned host queries → H2D → knn → D2H of the ids, pipelined on
-the same streams, K steps; `value_host_api` is the synchronous C-ABI host call shine_knn_batch, one batch at a time)
+`value_host_to_host` (SURVEY §8d's query phase: queries and results in pinned host memory that the kernels read and
+write over PCIe, K steps, batches in flight as above; `value_host_to_host_copies` the same with copy-engine H2D / D2H;
+`value_host_api` is the synchronous C-ABI host call shine_knn_batch, one batch at a time)
 and `cpu_baseline` (the CPU oracle — a C++ restatement of the reference's knn — built with the reference's flags on
 the host that runs it, on the host cores, bounded sample, rank 0 at N=1 only).
 
@@ -63,13 +64,21 @@ def log(msg):
 def host_threads():
     """This process's CPU share: OMP_NUM_THREADS when the launcher sets it (the GPU box grants 16 CPUs per GPU
     while sched_getaffinity lists the whole machine), else the affinity mask."""
+    try:
+        aff = max(1, len(os.sched_getaffinity(0)))
+    except Exception:
+        aff = os.cpu_count() or 1
     env = os.environ.get("OMP_NUM_THREADS")
     if env and env.isdigit() and int(env) > 0:
-        return int(env)
-    try:
-        return max(1, len(os.sched_getaffinity(0)))
-    except Exception:
-        return os.cpu_count() or 1
+        n = int(env)
+        # torchrun sets OMP_NUM_THREADS=1 for every rank unless the caller set it: rank 0's one-off index build (the
+        # others wait at a barrier) would then run on one thread; it builds for the whole node, so it takes the
+        # node's share (16 CPUs per GPU on this pool) instead
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+        if n == 1 and local_world > 1 and os.environ.get("TORCHELASTIC_RUN_ID"):
+            return max(1, min(aff, 16 * local_world))
+        return n
+    return aff
 
 
 def rank_queries(pool: np.ndarray, rank: int, world: int, n: int) -> np.ndarray:
@@ -248,19 +257,26 @@ def main():
         return dict(elapsed=elapsed, kern_ms=kern_ms, span_ms=span_ms, bytes_steps=bytes_steps, recall=recall,
                     qs=qs_h, ids=res, dists=res_d)
 
-    def host_legs(mode):
-        """SURVEY §8d's query phase, host to host: pinned host queries → H2D → knn → D2H of ids and distances, all
-        on the step's stream (two batches in flight), K steps between barriers; then the synchronous C-ABI host
-        call (shine_knn_batch: pinned staging inside the library), one batch at a time."""
+    def host_legs(mode, ref_ids):
+        """SURVEY §8d's query phase, host to host, K steps between barriers, batches in flight as above:
+        zero copy (`value_host_to_host`): queries in pinned host memory, the kernels read them and write ids and
+        distances into pinned host memory over PCIe (the device address space maps it); copy engine
+        (`value_host_to_host_copies`): pinned H2D → knn → D2H on the step's stream; then the synchronous C-ABI host
+        call (shine_knn_batch, zero-copy staging inside the library), one batch at a time.  The zero-copy answers
+        are checked against the HBM-resident run's."""
         idx.set_search_mode(mode)
         q_host = torch.from_numpy(q).pin_memory()
         ids_host = torch.empty((a.nbatches, a.batch, a.k), dtype=torch.int32).pin_memory()
         d_host = torch.empty((a.nbatches, a.batch, a.k), dtype=torch.float32).pin_memory()
         qbuf = [torch.empty((a.batch, a.dim), dtype=torch.float32, device="cuda") for _ in streams]
 
-        def hstep(i):
+        def hstep(i, copies):
             b, si = i % a.nbatches, i % len(streams)
             st = streams[si]
+            if not copies:
+                idx.knn_device(q_host[b * a.batch:(b + 1) * a.batch].data_ptr(), a.batch, a.k, a.ef,
+                               ids_host[b].data_ptr(), d_host[b].data_ptr(), qs[b].data_ptr(), stream=st.cuda_stream)
+                return
             with torch.cuda.stream(st):
                 qbuf[si].copy_(q_host[b * a.batch:(b + 1) * a.batch], non_blocking=True)
                 idx.knn_device(qbuf[si].data_ptr(), a.batch, a.k, a.ef, ids[b].data_ptr(), dists[b].data_ptr(),
@@ -268,21 +284,29 @@ def main():
                 ids_host[b].copy_(ids[b], non_blocking=True)
                 d_host[b].copy_(dists[b], non_blocking=True)
 
-        for i in range(a.warmup):
-            hstep(i)
-        torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(a.steps):
-            hstep(a.warmup + i)
-        torch.cuda.synchronize()
-        el = max_over_ranks(time.perf_counter() - t0, dist, "cuda")
-        got = ids_host.numpy().view(np.uint32).reshape(-1, a.k)
-        rec = D.recall_at_k(got[:a.batch * min(a.nbatches, a.steps + a.warmup)], gt, a.k)
+        def timed(copies):
+            for i in range(a.nbatches):  # every batch once: the answers checked below
+                hstep(i, copies)
+            torch.cuda.synchronize()
+            got = ids_host.numpy().view(np.uint32).reshape(-1, a.k).copy()
+            for i in range(a.warmup):
+                hstep(i, copies)
+            torch.cuda.synchronize()
+            if dist:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(a.steps):
+                hstep(a.warmup + i, copies)
+            torch.cuda.synchronize()
+            return max_over_ranks(time.perf_counter() - t0, dist, "cuda"), got
+
+        el, got = timed(False)
         out = {"value_host_to_host": a.steps * a.batch * world / el, "ms_per_step_host_to_host": el * 1e3 / a.steps,
-               "recall_at_10_host_to_host": rec}
+               "host_to_host_same_ids_as_device": bool(ref_ids is not None and (got == ref_ids).all()),
+               "recall_at_10_host_to_host": D.recall_at_k(got, gt, a.k)}
+        el, _ = timed(True)
+        out["value_host_to_host_copies"] = a.steps * a.batch * world / el
         # the synchronous host API (no batches in flight: it returns when the batch's results are on the host)
         steps_api = max(1, min(a.steps, 20))
         for i in range(2):
@@ -296,7 +320,8 @@ def main():
         el = max_over_ranks(time.perf_counter() - t0, dist, "cuda")
         out["value_host_api"] = steps_api * a.batch * world / el
         out["ms_per_step_host_api"] = el * 1e3 / steps_api
-        log(f"host legs: host-to-host {out['value_host_to_host'] / 1e6:.2f}M QPS (recall {rec:.4f}), "
+        log(f"host legs: host-to-host zero copy {out['value_host_to_host'] / 1e6:.2f}M QPS (same ids as on HBM: "
+            f"{out['host_to_host_same_ids_as_device']}), copy engine {out['value_host_to_host_copies'] / 1e6:.2f}M, "
             f"shine_knn_batch {out['value_host_api'] / 1e6:.2f}M QPS")
         return out
 
@@ -325,7 +350,8 @@ def main():
                               and (ro["qs"][:, :8] == fr["qs"][:, :8]).all())}
             log(f"{orows} rows: {other_rows['value'] / 1e6:.2f}M QPS, frac {other_rows['roofline_frac']:.3f}, identical "
                 f"results: {other_rows['same_ids_dists_counters']}")
-    host = None if a.no_host else host_legs(shine_amd.MODE_FAST if modes[0] == "fast" else shine_amd.MODE_EXACT)
+    host = None if a.no_host else host_legs(shine_amd.MODE_FAST if modes[0] == "fast" else shine_amd.MODE_EXACT,
+                                            runs[modes[0]]["ids"])
     head = runs[modes[0]]
     elapsed, kern_ms, bytes_steps, recall, qs_h = (head[x] for x in ("elapsed", "kern_ms", "bytes_steps", "recall", "qs"))
     # launches overlap when batches are in flight on several streams: the rate is the K launches' algorithmic bytes

@@ -149,18 +149,21 @@ int shine_open_buffers_ex(const uint8_t* const* dumps, const uint64_t* sizes, ui
  * (the compute-node split, read_data.hh:57-58), or on slot i % n_gpus when NULL.
  * out_ids: nq × k uids, in the reference's result order (top_candidates heap-array order, hnsw.hh:300-303).
  * out_dists (nullable): nq × k.  qstats (nullable): nq × SHINE_QS_WORDS.  stats (nullable): aggregates.
- * Requires ef >= k (hnsw.hh:36).  Synchronous: every slot's batch is staged through pinned host memory and enqueued
- * (H2D, search passes, D2H) before the call waits. */
+ * Requires ef >= k (hnsw.hh:36).  Synchronous: every slot's batch is staged in pinned host memory mapped into the
+ * GPU's address space (the kernels read the queries and write the results over PCIe themselves, no copy engine) and
+ * enqueued before the call waits. */
 int shine_knn_batch(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
                     uint32_t ef, uint32_t* out_ids, float* out_dists, uint32_t* qstats, shine_stats* stats);
 
 /* Same with device-resident inputs/outputs on GPU `gpu_slot` of the handle, enqueued on `stream`
  * (hipStream_t; NULL = the handle's stream).  Asynchronous: returns after enqueue.  qstats (device,
- * nullable).  Queries whose candidate queue overflowed are flagged in qstats[SHINE_QS_STATUS]; use
+ * nullable).  The pointers may also be pinned host memory the device can address (hipHostMalloc, torch
+ * pin_memory): the kernels then read queries / write results over PCIe (zero copy; bench.py value_host_to_host).
+ * Queries whose candidate queue overflowed are flagged in qstats[SHINE_QS_STATUS]; use
  * shine_knn_batch (or check qstats) when exactness under overflow must be guaranteed.
  * Batches enqueued on different streams run concurrently: the handle keeps its search scratch (work-queue
  * heads, fixup lists, visited bitmaps) per stream, so a serving loop may keep several batches in flight
- * (bench.py keeps two).  Calls on one stream are ordered as usual.
+ * (bench.py keeps four).  Calls on one stream are ordered as usual.
  * Stream lifetime: the handle keeps per-stream scratch keyed by the stream; a caller stream must stay valid until
  * shine_release_stream(h, stream) or shine_close(h), and must be released before it is destroyed if its handle
  * value may be reused while h is open. */
