@@ -1007,7 +1007,12 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
 
         // accept / push / push_k in list order (:456-465)
         PHASE(6)
-        for (int j = 0; j < nf; ++j) {
+        // keys that fail the accept test against the current top fail it later too (the farthest distance only
+        // shrinks once the top is full), so only the lanes one ballot lets through are visited, in list order
+        u64 pass = __ballot(lane < nf && (my_d < key(troot) || ntop < ef));
+        while (pass) {
+          const int j = static_cast<int>(__builtin_ctzll(pass));
+          pass &= pass - 1;
           const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_d), j));
           if (d < key(troot) || ntop < ef) {
             if (nnext >= cap) { status = ST_OVERFLOW; break; }
