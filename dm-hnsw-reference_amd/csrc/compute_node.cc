@@ -13,7 +13,7 @@
 //   statistics         one JSON document on stdout under the reference's names (statistics.hh:122-130,
 //                      compute_node.cc:549-556, 478-497): build / queries / cache / meta / hnsw_parameters / timings
 // Transport flags of the RDMA deployment (--servers, --port, ...) have no meaning here; GPU placement flags are
-// added (--gpus, --placement, --search-mode, --batch, --memory-nodes).  Errors print "[ERROR]: ..." and exit 1,
+// added (--gpus, --placement, --search-mode, --rows, --batch, --memory-nodes).  Errors print "[ERROR]: ..." and exit 1,
 // as lib_assert / exit_with_help_message do (utils.hh:17-23, configuration.hh:88-113).
 #include <algorithm>
 #include <chrono>
@@ -65,7 +65,7 @@ struct Config {
   uint32_t num_clients = 1, client_id = 0;
   // GPU placement (include/shine_gpu.h)
   std::vector<int> gpus{0};
-  std::string placement = "replica", search_mode = "exact";
+  std::string placement = "replica", search_mode = "exact", rows = "f32";
   uint32_t batch = 1024, memory_nodes = 1;
 };
 
@@ -94,6 +94,8 @@ const char* kHelp =
     "      --placement P          replica | sharded (default replica)\n"
     "      --memory-nodes N       memory-node dumps to build / load (default 1)\n"
     "      --search-mode M        exact (reference heap order) | fast (default exact)\n"
+    "      --rows R               record storage in HBM: f32 | auto (u8 / i8 rows where every component is a byte\n"
+    "                             value, bitwise the same results) (default f32)\n"
     "      --batch N              queries per shine_knn_batch call (default 1024)\n";
 
 [[noreturn]] void exit_with_help(const std::string& msg) {
@@ -150,6 +152,7 @@ Config parse(int argc, char** argv) {
     else if (a == "--memory-nodes") c.memory_nodes = static_cast<uint32_t>(parse_uint(a, v));
     else if (a == "--placement") c.placement = v;
     else if (a == "--search-mode") c.search_mode = v;
+    else if (a == "--rows") c.rows = v;
     else if (a == "--gpus") {
       c.gpus.clear();
       std::stringstream ss(v);
@@ -177,6 +180,7 @@ Config parse(int argc, char** argv) {
   if (c.num_clients == 0 || c.client_id >= c.num_clients) exit_with_help("--client-id must be < --num-clients");
   if (c.placement != "replica" && c.placement != "sharded") exit_with_help("--placement must be replica or sharded");
   if (c.search_mode != "exact" && c.search_mode != "fast") exit_with_help("--search-mode must be exact or fast");
+  if (c.rows != "f32" && c.rows != "auto") exit_with_help("--rows must be f32 or auto");
   if (c.batch == 0 || c.memory_nodes == 0) exit_with_help("--batch and --memory-nodes must be > 0");
   return c;
 }
@@ -381,7 +385,8 @@ int run(const Config& c) {
                                                   : SHINE_PLACE_SHARDED;
   const double cache_fraction = c.use_cache && placement != SHINE_PLACE_REPLICA ? c.cache_size_ratio / 100.0 : 0.0;
   shine_index_t h = nullptr;
-  check(shine_open_buffers_ex(ptrs.data(), sizes.data(), c.memory_nodes, dim, c.m, metric, SHINE_ELEM_F32,
+  check(shine_open_buffers_ex(ptrs.data(), sizes.data(), c.memory_nodes, dim, c.m, metric,
+                              c.rows == "auto" ? SHINE_ELEM_AUTO : SHINE_ELEM_F32,
                               c.gpus.data(), static_cast<uint32_t>(c.gpus.size()), placement,
                               std::min(1.0, cache_fraction), &h),
         "shine_open");
@@ -473,6 +478,7 @@ int run(const Config& c) {
   gj.str("placement", c.placement + (c.routing ? "+routing" : ""));
   gj.num("cache_fraction", info.cache_fraction);
   gj.str("search_mode", c.search_mode);
+  gj.str("rows", info.elem == SHINE_ELEM_U8 ? "u8" : info.elem == SHINE_ELEM_I8 ? "i8" : "f32");
   gj.num("kernel_ms", th.stats.kernel_ms);
   gj.num("algorithmic_bytes", th.stats.algorithmic_bytes);
   gj.num("remote_reads_in_bytes", th.stats.remote_reads_in_bytes);

@@ -35,6 +35,7 @@ def _run(args, timeout=600):
      "--routing can only be used in conjunction with --cache"),
     (["-d", "/x", "-q", "a", "-t", "1", "--ef-search", "5", "-k", "10"], "ef_search must be >= k"),
     (["-d", "/x", "-q", "a", "-t", "1", "--ef-search", "10", "-k", "10", "--bogus", "1"], "unknown option --bogus"),
+    (["-d", "/x", "-q", "a", "-t", "1", "--ef-search", "10", "-k", "10", "--rows", "u4"], "--rows must be f32 or auto"),
 ])
 def test_flag_validation_matches_reference(args, msg):
     r = _run(args)
@@ -116,6 +117,13 @@ def test_end_to_end_on_golden_fixtures(tmp_path, gpu_available):
         assert s["hnsw_parameters"] == {"k": c["k"], "m": c["M"], "ef_search": c["ef"], "ef_construction": c["efc"]}
         for key in ("hits_total", "misses_total", "hit_rate"):
             assert key in s["cache"]
+    # --rows auto: the .u8bin base is byte-valued, so the records sit in HBM as u8 rows; same searches, same answers
+    r = _run(common + ["-l", "--rows", "auto"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    s = json.loads(r.stdout)
+    assert s["gpu"]["rows"] == "u8"
+    assert s["queries"]["dist_comps"] == int(exp["qstats"][:, 0].sum())
+    assert abs(s["queries"]["recall"] - want_recall) < 1e-12
     # --store-index wrote the reference's dump name, byte-identical to the oracle's build (one thread)
     dump = data / "dump" / f"index_m{c['M']}_efc{c['efc']}_node1_of1.dat"
     import hashlib
