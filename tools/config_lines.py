@@ -255,7 +255,7 @@ def main():
     p.add_argument("--nbatches", type=int, default=4)
     p.add_argument("--ef", default="", help="comma list overriding the workload's ef (recall / QPS trade-off)")
     p.add_argument("--modes", default="fast,exact")
-    p.add_argument("--inflight", type=int, default=2, help="batches in flight per GPU slot (HIP streams)")
+    p.add_argument("--inflight", type=int, default=4, help="batches in flight per GPU slot (HIP streams)")
     p.add_argument("--cache", default=os.environ.get("SHINE_CFG_CACHE", "/tmp/shine_cfg"))
     p.add_argument("--out", default=str(ROOT / "gpurun_out" / "config_lines.jsonl"))
     p.add_argument("--alphas", default="0,0.5,1.0,1.5", help="cfg5skew: Zipf exponents")
