@@ -46,11 +46,11 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "dm-hnsw-reference_amd"))
 
 # Batches in flight only overlap on distinct hardware queues.  HIP maps streams to its GPU_MAX_HW_QUEUES queues (4 by
-# default) round-robin in creation order, and torch's stream pool handed this bench's four streams two queues
-# (rocprofv3 kernel trace: queue ids 3 and 4 only), so pairs of batches ran back to back: 4.88 M QPS at ef = 128
-# against 6.23 M with 8 queues (profiles/r02/hwq_streams.txt).  Set before torch initialises HIP; an explicit
-# setting from the caller wins.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# default, and the GPU boxes export 4) round-robin in creation order, and torch's stream pool handed this bench's
+# four streams two queues (rocprofv3 kernel trace: queue ids 3 and 4 only), so pairs of batches ran back to back:
+# 4.88 M QPS at ef = 128 against 6.23 M with 8 queues (profiles/r02/hwq_streams.txt).  The bench configures its own
+# process for 8 queues (SHINE_BENCH_HW_QUEUES overrides), before torch initialises HIP.
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("SHINE_BENCH_HW_QUEUES", "8")
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ROW_NAMES = {0: "f32", 1: "f16", 2: "u8", 3: "i8"}  # shine_index_info.elem

@@ -785,7 +785,10 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
   sh.grid = std::max<uint32_t>(1, std::min<uint32_t>(nq, cus * wpc));
   if (pass == PASS_LIGHT) {
     sh.grid = std::min(sh.grid, bitmap_slot_cap(h));
-    const uint64_t want = std::max<uint64_t>(cus, (2ull * handed + 63) / 64 * 64);
+    // at least 64 slots: a call whose main pass hands on nothing launches few workgroups that exit at once (64
+    // instead of one per CU: +0.8 % at ef = 128 with four batches in flight, profiles/r02/fallback_launch_cost.txt)
+    const uint64_t floor_grid = static_cast<uint64_t>(std::max<int64_t>(1, env_int("SHINE_DEBUG_LIGHT_MIN_GRID", 64)));
+    const uint64_t want = std::max<uint64_t>(floor_grid, (2ull * handed + 63) / 64 * 64);
     sh.grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(sh.grid, want)));
   }
   return sh;

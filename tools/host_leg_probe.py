@@ -19,7 +19,7 @@ import sys
 import time
 from pathlib import Path
 
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+os.environ["GPU_MAX_HW_QUEUES"] = "8"  # as bench.py
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "dm-hnsw-reference_amd"))
 sys.path.insert(0, str(ROOT))
