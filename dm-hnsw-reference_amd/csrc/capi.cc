@@ -129,12 +129,16 @@ struct ShardedArray {
 struct Scratch {
   DevBuf<uint32_t> visited, vlog, counter, ovf, qs;
   DevBuf<unsigned long long> heaps;  // global-heap pass
-  // host memory the last pass of every call writes: the queries each pass handed on, and [3] = 1 once written
-  // (sizes the next call's light pass; may be stale while a call is in flight)
+  // host memory the last pass of every call writes: [0..2] the queries each pass handed on, [3] = 1 once written,
+  // [4] the most nodes a query of that call marked visited (sizes the next call's light pass and visited tables;
+  // may be stale while a call is in flight)
   HostBuf<uint32_t> seen;
   uint32_t* seen_dev = nullptr;  // its device address
   bool counters_zero = false;    // the last call's last pass zeroed the counter words (finish_call)
   uint32_t slots = 0;
+  uint32_t last_table = 0;       // visited-table entries of the last call's main pass, and whether they were learned
+  bool last_learned = false;
+  uint32_t table_floor = 0;      // a learned table that overflowed is never learned again below twice its size
   void release() {
     for (auto* b : {&visited, &vlog, &counter, &ovf, &qs}) b->release();
     heaps.release();
@@ -684,13 +688,27 @@ int64_t env_int(const char* name, int64_t dflt) {
 // the id space fits them — the largest table that allows that many wavefronts per CU is taken, and the width with
 // more resident wavefronts, then the larger table, wins; u32 on a tie (its inserts take fewer LDS round trips:
 // measured 8.7 M vs 6.0 M QPS at ef = 32, where both fit; 4.26 M vs 3.89 M at ef = 128, where only u16 does).
-LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds_per_cu, uint64_t id_space) {
+// Visited-table entries learned from the previous call on a stream: the most nodes one of its queries marked visited,
+// with room to spare (tables are used to 7/8 and the next batch may visit more: >= 1.625x), never below the floor a
+// learned table that overflowed has set; 0 when there is nothing to learn from (first call on the stream, or its main
+// pass handed queries on).  Fixed shapes size tables from ef alone (pow2(40·ef) at least): DEEP-shaped 1M records at
+// ef = 256 visit at most ~3.8K nodes, and 8K entries instead of 16K run 1.8x faster (profiles/r02/cfg3_table_size.txt).
+uint32_t learned_table(const Scratch& S, uint32_t handed) {
+  if (!S.seen.p || !S.seen.p[3] || handed != 0 || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
+  const uint32_t vmax = S.seen.p[4];
+  if (vmax == 0) return 0;
+  return std::max<uint32_t>({1024u, S.table_floor, pow2_at_least(vmax + vmax / 2 + vmax / 8)});
+}
+
+LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds_per_cu, uint64_t id_space,
+                            uint32_t learned = 0) {
   LaunchShape sh{};
   const uint32_t want = std::max<uint32_t>(1, std::min<uint32_t>(16, (nq + cus - 1) / cus));
   const uint32_t target = std::min<uint32_t>(16, 2 * want);
   // a table below pow2(40·ef) entries sends a measurable share of queries to the light pass (ef = 128 on the bench's
   // index: 4,096 entries gave 1.1 M QPS against 4.2 M for 8,192), whatever residency it buys
-  const uint32_t lo = std::min<uint32_t>(16384, std::max<uint32_t>(2048, pow2_at_least(40 * ef)));
+  uint32_t lo = std::min<uint32_t>(16384, std::max<uint32_t>(2048, pow2_at_least(40 * ef)));
+  if (learned) lo = std::min(lo, learned);  // the previous call's queries fit a smaller table
   const uint32_t hi = std::min<uint32_t>(16384, std::max<uint32_t>(lo, pow2_at_least(48 * ef)));
   uint32_t bits = 14;
   while (bits < 32 && (1ull << bits) < id_space) ++bits;
@@ -738,7 +756,7 @@ uint32_t bitmap_slot_cap(const shine_index* h) {
 // that (at least one per CU, at most what LDS shares and bitmap memory allow): its workgroups of a call with few
 // overflows exit at once, and a launch of thousands of them delays the stream's next batch (-7 % QPS at ef = 32).
 LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint32_t ef, int pass,
-                       uint32_t handed = 0xFFFFFFFFu) {
+                       uint32_t handed = 0xFFFFFFFFu, uint32_t learned = 0) {
   LaunchShape sh{};
   const uint64_t top_bytes = align16(8ull * ef);
   const uint32_t cus = R.cus, lds = R.lds_per_cu;
@@ -754,6 +772,7 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
     // u16 quotient entries (VisitedLds<1>) when the id space fits them and they let more wavefronts share a CU with
     // next_candidates still >= 5·ef entries (u32: 4·ef)
     sh.vis_cap = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(48 * ef)));
+    if (learned) sh.vis_cap = std::min(sh.vis_cap, learned);  // the previous call's queries fit a smaller table
     sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
     // aim at the wavefronts of two batches in flight being resident together, as pick_fast_shape does
     const uint32_t want = std::min<uint32_t>(2 * ((nq + cus - 1) / cus), 16u);
@@ -826,7 +845,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   if (S.ovf.n < 3ull * nq) HIP_TRY(hipStreamSynchronize(s));  // a reallocation must not pull the list from under
   if (int rc = S.ovf.grow(3ull * nq)) return rc;                // an earlier call on this stream
   if (!S.seen_dev) {
-    if (int rc = S.seen.grow(4, hipHostMallocMapped | hipHostMallocPortable)) return rc;
+    if (int rc = S.seen.grow(8, hipHostMallocMapped | hipHostMallocPortable)) return rc;
     void* dp = nullptr;
     HIP_TRY(hipHostGetDevicePointer(&dp, S.seen.p, 0));
     S.seen_dev = static_cast<uint32_t*>(dp);
@@ -839,6 +858,8 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   const bool fast_mode = h->search_mode == SHINE_MODE_FAST;
   const bool fast_kernel = fast_mode && ef <= kFastMaxEf && h->M0 <= 64;
   const uint32_t handed = S.seen.p[3] ? S.seen.p[0] : 0;  // [3] = 1 once a call has written the counts
+  if (handed && S.last_learned) S.table_floor = std::max(S.table_floor, 2 * S.last_table);  // it was too small
+  const uint32_t learned = learned_table(S, handed);
   int chain[3], n_pass = 0;
   if (start <= 0) chain[n_pass++] = fast_kernel ? PASS_FAST : PASS_LDS;
   else if (start == 1) chain[n_pass++] = PASS_WHOLE_CU;
@@ -847,8 +868,16 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   for (int i = 0; i < n_pass; ++i) {
     const int pass = chain[i];
     const LaunchShape sh =
-        pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu, h->id_space)
-                          : pick_shape(h, R, nq, ef, pass, handed);
+        pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu, h->id_space, learned)
+                          : pick_shape(h, R, nq, ef, pass, handed, learned);
+    if (i == 0) {
+      S.last_table = sh.vis_cap;
+      S.last_learned = learned != 0;
+      if (env_int("SHINE_DEBUG_SHAPE", 0))  // diagnostics: the main pass's shape and what it was learned from
+        std::fprintf(stderr, "shape: pass %d nq %u ef %u table %u vis16 %u grid %u learned %u vmax %u handed %u floor %u\n",
+                     pass, nq, ef, sh.vis_cap, sh.vis16, sh.grid, learned, S.seen.p[3] ? S.seen.p[4] : 0u, handed,
+                     S.table_floor);
+    }
     SearchArgs a{};
     a.g = dev_graph(h, R);
     if (!a.g.vec || !a.g.adj0 || !a.g.uid || !a.g.up_base)
@@ -880,6 +909,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     a.vlog = S.vlog.p;
     a.log_cap = kLogCap;
     a.counter = S.counter.p + i;
+    a.vis_max = S.counter.p + 3;
     a.fast = pass == PASS_FAST ? 1u : 0u;
     a.vis16 = sh.vis16;
     a.vis_bits = sh.vis_bits;

@@ -52,8 +52,11 @@ struct SearchArgs {
   uint64_t heap_stride;
   uint32_t* access;          // cache warmup (nullable): per device id, reads of the record (vector or list)
   uint32_t* call_counters;   // last pass of a call (nullable): the call's 8 counter words; the last workgroup to
-  uint32_t* host_counts;     // finish copies words 4..6 to host_counts[0..2] (host memory), sets host_counts[3] = 1
-                             // and zeroes the 8 words for the next call on the stream (word 7 counts finished groups)
+  uint32_t* host_counts;     // finish copies words 4..6 to host_counts[0..2] (host memory), sets host_counts[3] = 1,
+                             // copies word 3 to host_counts[4] and zeroes the 8 words for the next call on the stream
+                             // (word 7 counts finished groups)
+  uint32_t* vis_max;         // every pass (nullable): the call's counter word 3, the most nodes any query marked
+                             // visited (atomicMax per query) — sizes the next call's visited tables
   unsigned long long* prof; // diagnostics (nullable): per-phase shader-clock totals, PROF kernel variant only
   uint32_t fast;            // 1: sorted-list kernel (SHINE_MODE_FAST; ef <= kFastMaxEf, vis_cap > 0)
   uint32_t sort_out;        // heap kernel writes ascending order (fast-mode fixup passes)

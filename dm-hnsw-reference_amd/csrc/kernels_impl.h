@@ -841,6 +841,7 @@ __device__ __forceinline__ void finish_call(const SearchArgs& A, int lane) {
   host[0] = h0;
   host[1] = h1;
   host[2] = h2;
+  host[4] = __atomic_load_n(&c[3], __ATOMIC_RELAXED);
   host[3] = 1u;
 #pragma unroll
   for (int i = 0; i < 8; ++i) __atomic_store_n(&c[i], 0u, __ATOMIC_RELAXED);
@@ -1076,6 +1077,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
       if (A.out_dists) A.out_dists[obase + slot] = d;
     }
     if (status == ST_OVERFLOW && A.out_list && lane == 0) A.out_list[atomicAdd(A.out_count, 1u)] = qi;
+    if (A.vis_max && lane == 0) atomicMax(A.vis_max, nvis);  // visited-table occupancy, for the next call's shape
     if (A.qstats && lane == 0) {
       u32* qs = A.qstats + static_cast<u64>(qi) * kQsWords;
       qs[0] = st_dist;
@@ -1447,6 +1449,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       }
     }
     if (status == ST_OVERFLOW && A.out_list && lane == 0) A.out_list[atomicAdd(A.out_count, 1u)] = qi;
+    if (A.vis_max && lane == 0) atomicMax(A.vis_max, nvis);  // visited-table occupancy, for the next call's shape
     if (A.qstats && lane == 0) {
       u32* qs = A.qstats + static_cast<u64>(qi) * kQsWords;
       qs[0] = st_dist;

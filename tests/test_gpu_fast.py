@@ -208,3 +208,25 @@ def test_fast_mode_visited_entry_widths_agree(vis16, gpu_available, monkeypatch)
     monkeypatch.setenv("SHINE_DEBUG_VISCAP", "4096")
     r = _fast_knn(dumps, 96, 16, 0, q, 10, 128)
     _check_tie_free_exact(r, ref, 0.95)
+
+
+@pytest.mark.parametrize("mode", [L.MODE_FAST, L.MODE_EXACT])
+def test_learned_table_sizes_keep_results(mode, gpu_available):
+    """The visited tables of a call are sized from the previous call's most-visited query on the same stream
+    (capi.cc learned_table): repeated calls on one handle run on learned (smaller) tables and must return what the
+    first call, on the fixed shape, returned — and what the oracle returns."""
+    base = D.deep_like(6000, seed=81, d=96)
+    q = D.deep_like(300, seed=82, d=96)
+    dumps, _, _ = O.build(base, 16, 100, 1, 1, seed=8)
+    ref = O.OracleIndex(dumps, 96, 16, 1).knn(q, 10, 256, threads=8)
+    with shine_amd.Index.from_buffers(dumps, 96, 16, 1, gpus=[0]) as idx:
+        idx.set_search_mode(mode)
+        runs = [idx.knn(q, 10, 256) for _ in range(3)]
+    for r in runs[1:]:
+        np.testing.assert_array_equal(r.ids, runs[0].ids)
+        np.testing.assert_array_equal(r.dists.view(np.uint32), runs[0].dists.view(np.uint32))
+        assert (r.qstats[:, L.QS_STATUS] == 0).all()
+    if mode == L.MODE_EXACT:
+        np.testing.assert_array_equal(runs[-1].ids, ref[0])
+    else:
+        _check_tie_free_exact(runs[-1], ref, 0.95)

@@ -170,6 +170,9 @@ def run(name, a):
             "ms_per_batch": el * 1e3 / a.steps, "avg_launch_ms": float(np.mean(kern)),
             "span_ms_per_batch": span / a.steps, "batches_in_flight": a.inflight, "recall_at_10": recall,
             "failed_queries": bad, "mean_distcomps": float(qs_h[:, 0].mean()),
+            # nodes a query marks visited (upper levels + level 0): what its LDS visited table must hold
+            "visited_p99": float(np.percentile(qs_h[:, 1].astype(np.int64) + qs_h[:, 2], 99)),
+            "visited_max": int((qs_h[:, 1].astype(np.int64) + qs_h[:, 2]).max()),
             "queries_with_ties": float((qs_h[:, 5] > 0).mean()) if mode_name == "fast" else None,
             "dtype": "f16 records, f32 accumulate" if elem else "f32",
             "config": {"generator": gen, "n": n, "dim": dim, "metric": "IP" if metric else "L2", "M": M, "efc": efc,
