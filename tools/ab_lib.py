@@ -1,6 +1,10 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of two builds of libshine_gpu.so in ONE process (diagnostics).
 
+Caution (round 2): with four streams per side the second side's streams collide on the process's hardware queues and
+it measures up to 28 % slower whichever build it is (profiles/r02/ab_order_bias.txt); compare builds one process
+each with tools/lib_probe.py instead, alternating builds on one box.
+
 Each library opens the bench's dump by itself (shine_open, fast mode) and answers the same query batches on its own
 pair of HIP streams; timed blocks alternate A, B, A, B, ... so box and clock drift hit both equally.  Only the
 entry points whose signatures are unchanged since round 1 are used (shine_open, shine_set_search_mode,
