@@ -780,6 +780,36 @@ struct VisitedLds<1> {
     const u32 h = image(x);
     return has(w, (h & rmask) << dbits);
   }
+  // The common case of test_and_set when `cur` IS x's home bucket as it stands (the look-ahead probe, no insert
+  // since): the answer follows from `cur` alone — x sits in it (0), or the bucket has an empty entry, so x is absent
+  // and fresh (1) — and the compare-and-swap recording x is issued without waiting for it (word pw, expected pexp,
+  // its return in pold); finish() checks it after the distances.  2: a full bucket, use test_and_set.
+  __device__ __forceinline__ int begin(u32 x, const Hint& cur, u32& pw, u32& pexp, u32& pold) {
+    const u32 h = image(x);
+    const u32 e = (h & rmask) << dbits;
+    if (has(cur, e)) return 0;
+    const u32 w[4] = {cur.x, cur.y, cur.z, cur.w};
+    int j = -1;
+    u32 k = 0;
+#pragma unroll
+    for (int i = 3; i >= 0; --i) {
+      const bool lo = (w[i] & 0xFFFFu) == 0xFFFFu, hi = (w[i] >> 16) == 0xFFFFu;
+      if (lo | hi) {
+        j = i;
+        k = lo ? 0u : 1u;
+      }
+    }
+    if (j < 0) return 2;
+    pexp = j == 0 ? cur.x : j == 1 ? cur.y : j == 2 ? cur.z : cur.w;
+    pw = (h >> rbits) * 4 + static_cast<u32>(j);
+    pold = atomicCAS(&t[pw], pexp, k ? ((pexp & 0xFFFFu) | (e << 16)) : ((pexp & 0xFFFF0000u) | e));
+    return 1;
+  }
+  // another lane of the wave took that word first (two list entries, one home bucket): x is still absent and is
+  // inserted again from its home bucket as it is now
+  __device__ __forceinline__ void finish(u32 x, u32 pexp, u32 pold, bool& ovf) {
+    if (pold != pexp) (void)test_and_set(x, ovf, bucket(image(x) >> rbits));
+  }
   // Buckets of 8 entries, probed linearly: x's entry (its remainder and its bucket's distance from home) is looked for
   // in one bucket read at a time and goes to the bucket's first empty entry.  Entries are never removed, so a bucket
   // with an empty entry ends the search.  cur: the home bucket as last read (probe) or unknown().
@@ -1235,6 +1265,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
     u32 nid = nn;
     u32 nrow = load_row(nn);
     u32 cur = nn;  // the candidate whose list `e` is
+    bool ehint_known = false;  // ehint is e's home bucket as it stands (not a guess)
     typename VisitedLds<VT>::Hint ehint = VisitedLds<VT>::unknown();  // e's home word / bucket as probed one
                                                                       // expansion earlier (VisitedLds::test_and_set)
 
@@ -1251,13 +1282,22 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
           if ((j & 3) < P && sj < M0 && sj < my_slot && ej == e) cand = false;
         }
       }
+      // visited.contains / insert (:441-443); u16 table with e's home bucket known from the look-ahead probe: the
+      // answer without an LDS round trip, the recording compare-and-swap checked after the distances (+1.2 % at
+      // ef = 128, profiles/r02/lib_probe_deferred_insert.jsonl)
       bool fresh = false, vovf = false;
-      if (cand) fresh = vis.test_and_set(e, vovf, ehint);  // visited.contains / insert (:441-443)
+      u32 pw = INV, pexp = 0, pold = 0;
       if constexpr (VT == 1) {
-        if (__ballot(vovf)) {  // an id too far from its home slot: the light pass re-runs the query
+        if (cand) {
+          const int r = ehint_known ? vis.begin(e, ehint, pw, pexp, pold) : 2;
+          fresh = r == 2 ? vis.test_and_set(e, vovf, ehint) : r == 1;
+        }
+        if (__ballot(vovf)) {
           status = ST_OVERFLOW;
           break;
         }
+      } else {
+        if (cand) fresh = vis.test_and_set(e, vovf, ehint);
       }
       const u64 fm = __ballot(fresh);
       const int nf = __popcll(fm);
@@ -1287,6 +1327,14 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
           ++ties;
         }
         acc = __ballot(fresh && (cs < ef || my_d < cmax));  // fresh keys that can enter (:461)
+      }
+
+      if constexpr (VT == 1) {  // the deferred compare-and-swaps, before the table is probed again
+        if (pw != INV) vis.finish(e, pexp, pold, vovf);
+        if (__ballot(vovf)) {
+          status = ST_OVERFLOW;
+          break;
+        }
       }
 
       // ---- the next candidate, known before the merge ----------------------------------------------------------
@@ -1421,6 +1469,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       nrow = load_row(nid);  // unconditional: always the youngest load
       e = erow;
       ehint = c != pid ? VisitedLds<VT>::unknown() : pword;  // the probe read prow's home bucket, no insert since
+      ehint_known = c == pid;
       cur = c;
       r_id = c2;
       r_key = k2;
