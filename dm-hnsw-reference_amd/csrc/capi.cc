@@ -688,27 +688,29 @@ int64_t env_int(const char* name, int64_t dflt) {
 // the id space fits them — the largest table that allows that many wavefronts per CU is taken, and the width with
 // more resident wavefronts, then the larger table, wins; u32 on a tie (its inserts take fewer LDS round trips:
 // measured 8.7 M vs 6.0 M QPS at ef = 32, where both fit; 4.26 M vs 3.89 M at ef = 128, where only u16 does).
-// Visited-table entries learned from the previous call on a stream: the most nodes one of its queries marked visited,
-// with room to spare (tables are used to 7/8 and the next batch may visit more: >= 1.625x), never below the floor a
-// learned table that overflowed has set; 0 when there is nothing to learn from (first call on the stream, or its main
-// pass handed queries on).  Fixed shapes size tables from ef alone (pow2(40·ef) at least): DEEP-shaped 1M records at
-// ef = 256 visit at most ~3.8K nodes, and 8K entries instead of 16K run 1.8x faster (profiles/r02/cfg3_table_size.txt).
-uint32_t learned_table(const Scratch& S, uint32_t handed) {
-  if (!S.seen.p || !S.seen.p[3] || handed != 0 || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
+// Visited-table entries learned from the previous call on a stream: the most nodes one of its queries marked visited
+// (queries the main pass handed on count in full: the fallback passes record them too), with room to spare (tables
+// are used to 7/8 and the next batch may visit more: >= 1.625x), never below the floor a learned table that
+// overflowed has set; 0 when there is nothing to learn from (first call on the stream).  Fixed shapes size tables
+// from ef alone: DEEP-shaped 1M records at ef = 256 visit at most ~3.8K nodes, and 8K entries instead of 16K run
+// 1.6-1.8x faster (profiles/r02/cfg3_table_size.txt); SIFT-shaped at ef = 32 outgrow the fixed 2K entries.
+uint32_t learned_table(const Scratch& S) {
+  if (!S.seen.p || !S.seen.p[3] || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
   const uint32_t vmax = S.seen.p[4];
   if (vmax == 0) return 0;
-  return std::max<uint32_t>({1024u, S.table_floor, pow2_at_least(vmax + vmax / 2 + vmax / 8)});
+  return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, pow2_at_least(vmax + vmax / 2 + vmax / 8)}));
 }
 
 LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds_per_cu, uint64_t id_space,
-                            uint32_t learned = 0) {
+                            uint32_t learned = 0, bool grow = false) {
   LaunchShape sh{};
   const uint32_t want = std::max<uint32_t>(1, std::min<uint32_t>(16, (nq + cus - 1) / cus));
   const uint32_t target = std::min<uint32_t>(16, 2 * want);
   // a table below pow2(40·ef) entries sends a measurable share of queries to the light pass (ef = 128 on the bench's
   // index: 4,096 entries gave 1.1 M QPS against 4.2 M for 8,192), whatever residency it buys
   uint32_t lo = std::min<uint32_t>(16384, std::max<uint32_t>(2048, pow2_at_least(40 * ef)));
-  if (learned) lo = std::min(lo, learned);  // the previous call's queries fit a smaller table
+  // what the previous call's queries needed: a smaller table, or a larger one once the fixed size overflowed
+  if (learned && (learned < lo || grow)) lo = learned;
   const uint32_t hi = std::min<uint32_t>(16384, std::max<uint32_t>(lo, pow2_at_least(48 * ef)));
   uint32_t bits = 14;
   while (bits < 32 && (1ull << bits) < id_space) ++bits;
@@ -772,7 +774,7 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
     // u16 quotient entries (VisitedLds<1>) when the id space fits them and they let more wavefronts share a CU with
     // next_candidates still >= 5·ef entries (u32: 4·ef)
     sh.vis_cap = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(48 * ef)));
-    if (learned) sh.vis_cap = std::min(sh.vis_cap, learned);  // the previous call's queries fit a smaller table
+    if (learned && (learned < sh.vis_cap || (handed != 0xFFFFFFFFu && handed > 0))) sh.vis_cap = learned;  // as fast
     sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
     // aim at the wavefronts of two batches in flight being resident together, as pick_fast_shape does
     const uint32_t want = std::min<uint32_t>(2 * ((nq + cus - 1) / cus), 16u);
@@ -859,7 +861,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   const bool fast_kernel = fast_mode && ef <= kFastMaxEf && h->M0 <= 64;
   const uint32_t handed = S.seen.p[3] ? S.seen.p[0] : 0;  // [3] = 1 once a call has written the counts
   if (handed && S.last_learned) S.table_floor = std::max(S.table_floor, 2 * S.last_table);  // it was too small
-  const uint32_t learned = learned_table(S, handed);
+  const uint32_t learned = learned_table(S);
   int chain[3], n_pass = 0;
   if (start <= 0) chain[n_pass++] = fast_kernel ? PASS_FAST : PASS_LDS;
   else if (start == 1) chain[n_pass++] = PASS_WHOLE_CU;
@@ -868,7 +870,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   for (int i = 0; i < n_pass; ++i) {
     const int pass = chain[i];
     const LaunchShape sh =
-        pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu, h->id_space, learned)
+        pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu, h->id_space, learned, handed > 0)
                           : pick_shape(h, R, nq, ef, pass, handed, learned);
     if (i == 0) {
       S.last_table = sh.vis_cap;
