@@ -874,7 +874,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
                           : pick_shape(h, R, nq, ef, pass, handed, learned);
     if (i == 0) {
       S.last_table = sh.vis_cap;
-      S.last_learned = learned != 0;
+      S.last_learned = learned != 0 && sh.vis_cap == learned;  // the table came from learning, not the fixed rule
       if (env_int("SHINE_DEBUG_SHAPE", 0))  // diagnostics: the main pass's shape and what it was learned from
         std::fprintf(stderr, "shape: pass %d nq %u ef %u table %u vis16 %u grid %u learned %u vmax %u handed %u floor %u\n",
                      pass, nq, ef, sh.vis_cap, sh.vis16, sh.grid, learned, S.seen.p[3] ? S.seen.p[4] : 0u, handed,
