@@ -485,27 +485,35 @@ __device__ __forceinline__ void pass_dists(const QueryRegs<D>& Q, const NbrBuf<D
   }
 }
 
-// sc_d[j] = dist(q, vec[sc_ids[j]]) for j < n.  All 64 lanes must call it.
+// slots p0 .. p0 + 16P - 1 of the list (those below n)
+template <int D, int METRIC, typename E, int P>
+__device__ __forceinline__ void dist_chunk(const E* __restrict__ vec, const QueryRegs<D>& Q, const u32* sc_ids,
+                                           float* sc_d, int p0, int n, int lane) {
+  const int g4 = lane >> 2, c4 = lane & 3;
+  NbrBuf<D, E, P> B;
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int slot = p0 + 16 * p + g4;
+    issue_pass<D, E, P>(B, p, vec, slot < n ? sc_ids[slot] : INV, c4);
+  }
+  float out[P];
+  pass_dists<D, METRIC, E, P>(Q, B, out);
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int slot = p0 + 16 * p + g4;
+    if (c4 == 3 && slot < n) sc_d[slot] = out[p];
+  }
+}
+
+// sc_d[j] = dist(q, vec[sc_ids[j]]) for j < n.  All 64 lanes must call it.  Two passes (32 slots) at a time while
+// more than 16 remain, then one: a list of <= 16 fresh nodes (an upper-level
+// list, most level-0 expansions of the heap kernel) costs one pass of VALU instead of two.
 template <int D, int METRIC, typename E>
 __device__ __forceinline__ void dist_list(const E* __restrict__ vec, const QueryRegs<D>& Q, const u32* sc_ids,
                                           float* sc_d, int n, int lane) {
-  constexpr int P = 2;
-  const int g4 = lane >> 2, c4 = lane & 3;
-  for (int p0 = 0; p0 < n; p0 += 16 * P) {
-    NbrBuf<D, E, P> B;
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-      const int slot = p0 + 16 * p + g4;
-      issue_pass<D, E, P>(B, p, vec, slot < n ? sc_ids[slot] : INV, c4);
-    }
-    float out[P];
-    pass_dists<D, METRIC, E, P>(Q, B, out);
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-      const int slot = p0 + 16 * p + g4;
-      if (c4 == 3 && slot < n) sc_d[slot] = out[p];
-    }
-  }
+  int p0 = 0;
+  for (; n - p0 > 16; p0 += 32) dist_chunk<D, METRIC, E, 2>(vec, Q, sc_ids, sc_d, p0, n, lane);
+  if (p0 < n) dist_chunk<D, METRIC, E, 1>(vec, Q, sc_ids, sc_d, p0, n, lane);
 }
 
 // Exact visited set (hashset_t<RemotePtr>, types.hh:14-15) on dense node ids.
