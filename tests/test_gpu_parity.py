@@ -289,3 +289,25 @@ def test_nan_distances_follow_reference(gpu_available):
     np.testing.assert_array_equal(np.isnan(r.dists), nan)  # NaN sign/payload is not specified by IEEE 754
     np.testing.assert_array_equal(r.dists[~nan].view(np.uint32), ref[1][~nan].view(np.uint32))
     np.testing.assert_array_equal(r.qstats[:, :5], ref[2][:, :5])
+
+
+def test_device_api_zero_copy_pinned_host_buffers(gpu_available):
+    """shine_knn_batch_device on pinned host memory (queries read and results written by the kernels over PCIe,
+    bench.py value_host_to_host): the oracle's answers, bitwise, in exact mode."""
+    import torch
+    base = D.sift_like(3000, seed=61)
+    qn = D.sift_like(200, seed=62)
+    dumps, _, _ = O.build(base, 16, 80, 0, 1, seed=6)
+    ref_ids, ref_d, ref_qs = O.OracleIndex(dumps, 128, 16, 0).knn(qn, 10, 64)
+    with shine_amd.Index.from_buffers(dumps, 128, 16, 0, gpus=[0]) as idx:
+        qh = torch.from_numpy(qn).pin_memory()
+        ids = torch.empty((200, 10), dtype=torch.int32).pin_memory()
+        dd = torch.empty((200, 10), dtype=torch.float32).pin_memory()
+        qs = torch.empty((200, shine_amd.QS_WORDS), dtype=torch.int32).pin_memory()
+        st = torch.cuda.Stream()
+        idx.knn_device(qh.data_ptr(), 200, 10, 64, ids.data_ptr(), dd.data_ptr(), qs.data_ptr(), stream=st.cuda_stream)
+        st.synchronize()
+        idx.release_stream(st.cuda_stream)
+    np.testing.assert_array_equal(ids.numpy().view(np.uint32), ref_ids)
+    np.testing.assert_array_equal(dd.numpy().view(np.uint32), ref_d.view(np.uint32))
+    np.testing.assert_array_equal(qs.numpy().view(np.uint32)[:, :8], ref_qs[:, :8])
