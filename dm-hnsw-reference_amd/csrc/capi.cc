@@ -139,6 +139,7 @@ struct Scratch {
   uint32_t last_table = 0;       // visited-table entries of the last call's main pass, and whether they were learned
   bool last_learned = false;
   uint32_t table_floor = 0;      // a learned table that overflowed is never learned again below twice its size
+  uint32_t last_ef = 0;          // ef of the last call: what it visited says nothing about another ef
   void release() {
     for (auto* b : {&visited, &vlog, &counter, &ovf, &qs}) b->release();
     heaps.release();
@@ -691,7 +692,8 @@ int64_t env_int(const char* name, int64_t dflt) {
 // Visited-table entries learned from the previous call on a stream: the most nodes one of its queries marked visited
 // (queries the main pass handed on count in full: the fallback passes record them too), with room to spare (tables
 // are used to 7/8 and the next batch may visit more: >= 1.625x), never below the floor a learned table that
-// overflowed has set; 0 when there is nothing to learn from (first call on the stream).  Fixed shapes size tables
+// overflowed has set; 0 when there is nothing to learn from (first call on the stream, or the previous one ran at
+// another ef).  Fixed shapes size tables
 // from ef alone: DEEP-shaped 1M records at ef = 256 visit at most ~3.8K nodes, and 8K entries instead of 16K run
 // 1.6-1.8x faster (profiles/r02/cfg3_table_size.txt); SIFT-shaped at ef = 32 outgrow the fixed 2K entries.
 uint32_t learned_table(const Scratch& S) {
@@ -861,7 +863,9 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   const bool fast_kernel = fast_mode && ef <= kFastMaxEf && h->M0 <= 64;
   const uint32_t handed = S.seen.p[3] ? S.seen.p[0] : 0;  // [3] = 1 once a call has written the counts
   if (handed && S.last_learned) S.table_floor = std::max(S.table_floor, 2 * S.last_table);  // it was too small
-  const uint32_t learned = learned_table(S);
+  if (ef != S.last_ef) S.table_floor = 0;
+  const uint32_t learned = ef == S.last_ef ? learned_table(S) : 0;
+  S.last_ef = ef;
   int chain[3], n_pass = 0;
   if (start <= 0) chain[n_pass++] = fast_kernel ? PASS_FAST : PASS_LDS;
   else if (start == 1) chain[n_pass++] = PASS_WHOLE_CU;
