@@ -48,13 +48,31 @@ sys.path.insert(0, str(ROOT / "dm-hnsw-reference_amd"))
 # Batches in flight only overlap on distinct hardware queues.  HIP maps streams to its GPU_MAX_HW_QUEUES queues (4 by
 # default, and the GPU boxes export 4) round-robin in creation order, and torch's stream pool handed this bench's
 # four streams two queues (rocprofv3 kernel trace: queue ids 3 and 4 only), so pairs of batches ran back to back:
-# 4.88 M QPS at ef = 128 against 6.23 M with 8 queues (profiles/r02/hwq_streams.txt).  The bench configures its own
-# process for 8 queues (SHINE_BENCH_HW_QUEUES overrides), before torch initialises HIP.
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("SHINE_BENCH_HW_QUEUES", "8")
+# 4.88 M QPS at ef = 128 against 6.23 M with 8 queues (profiles/r02/hwq_streams.txt).  The bench therefore creates its
+# in-flight streams itself, directly through HIP and before any other stream of the process (`hip_streams`), so the
+# round-robin hands them distinct queues under the box's own setting; the JSON line records that setting.
+HW_QUEUES = os.environ.get("GPU_MAX_HW_QUEUES")
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ROW_NAMES = {0: "f32", 1: "f16", 2: "u8", 3: "i8"}  # shine_index_info.elem
 KERNEL_TYPE = {"f32": "float", "f16": "__half", "u8": "unsigned char", "i8": "signed char"}  # rocprof kernel names
+
+
+def hip_streams(torch, n: int, device: int):
+    """n non-blocking HIP streams created directly (hipStreamCreateWithFlags), wrapped as torch ExternalStreams.
+    Created first in the process, they take n distinct hardware queues of the round-robin (n <= GPU_MAX_HW_QUEUES)."""
+    import ctypes
+    torch.cuda.set_device(device)
+    torch.cuda.init()
+    hip = ctypes.CDLL("libamdhip64.so")
+    out = []
+    for _ in range(n):
+        s = ctypes.c_void_p()
+        rc = hip.hipStreamCreateWithFlags(ctypes.byref(s), ctypes.c_uint(1))  # hipStreamNonBlocking
+        if rc != 0:
+            raise SystemExit(f"hipStreamCreateWithFlags failed: {rc}")
+        out.append(torch.cuda.ExternalStream(s.value, device=torch.device("cuda", device)))
+    return out
 
 
 def log(msg):
@@ -148,19 +166,103 @@ def parse():
                    help="skip timing fast mode on the other row storage (byte rows next to f32, or f32 next to bytes)")
     p.add_argument("--placement", choices=["replica", "sharded"], default="replica")
     p.add_argument("--slots", type=int, default=0, help="sharded leg: GPU slots (default --gpus)")
-    p.add_argument("--cache-frac", type=float, default=0.0, help="sharded leg: share of other stripes cached locally")
-    return p.parse_args()
+    p.add_argument("--cache-frac", type=float, default=0.05,
+                   help="sharded leg: share of other stripes cached locally (the reference's default --cache-ratio 5)")
+    p.add_argument("--sharded-leg", choices=["auto", "on", "off"], default="auto",
+                   help="after the replica measurement, run the cfg-4-shaped sharded leg over the same N GPUs in a child "
+                        "process and carry it in the same JSON line (auto: when N > 1)")
+    p.add_argument("--sharded-n", type=int, default=2_000_000, help="sharded leg: records of the DEEP-shaped index")
+    # the launcher hands its flags to the rank processes through the environment: torch.distributed.run's own parser
+    # would take bench.py's abbreviations (--n) for its options
+    extra = json.loads(os.environ.get("SHINE_BENCH_ARGV", "[]"))
+    return p.parse_args(sys.argv[1:] + extra)
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def child_json(cmd, env=None, timeout=None):
+    """Run a child process (never exec: the parent may have touched the GPU); return its last stdout line parsed as
+    JSON.  Its stderr passes through."""
+    import subprocess
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, env=env, timeout=timeout)
+    if r.returncode != 0:
+        raise SystemExit(f"child {cmd[:4]}... exited with {r.returncode}")
+    lines = [x for x in r.stdout.splitlines() if x.strip().startswith("{")]
+    if not lines:
+        raise SystemExit(f"child {cmd[:4]}... printed no JSON line")
+    return json.loads(lines[-1])
+
+
+def forwarded_args(a, drop=("gpus",)):
+    """This run's arguments as a command line for a child (bench.py's own flags, `drop` left out)."""
+    out = []
+    for k, v in vars(a).items():
+        if k in drop:
+            continue
+        flag = "--" + k.replace("_", "-")
+        if isinstance(v, bool):
+            if v:
+                out.append(flag)
+        else:
+            out += [flag, str(v)]
+    return out
+
+
+def launch(a):
+    """`python bench.py --gpus N` (N > 1) without torchrun: this parent never touches the GPU.  It starts
+    torch.distributed.run as a child process with N rank processes (one per GPU, rendezvous on 127.0.0.1), which run
+    the replica measurement (and, on rank 0, the sharded leg), and relays rank 0's JSON line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(Path(__file__).resolve()),
+           "--gpus", str(a.gpus)]
+    env = dict(os.environ)
+    env["SHINE_BENCH_ARGV"] = json.dumps(forwarded_args(a))
+    env.setdefault("OMP_NUM_THREADS", str(host_threads()))
+    log(f"launching {a.gpus} rank processes: {' '.join(cmd[2:])}")
+    line = child_json(cmd, env=env)
+    line["launcher"] = "bench.py --gpus N: torch.distributed.run child, one process per GPU"
+    print(json.dumps(line), flush=True)
+
+
+def sharded_leg(a, world: int):
+    """The cfg-4-shaped sharded leg over the same GPUs, in a child process (one process drives every GPU slot, so the
+    slots' stripes are read over xGMI): a compact summary for the replica line."""
+    cmd = [sys.executable, str(Path(__file__).resolve()), "--placement", "sharded", "--gpus", str(world),
+           "--slots", str(world), "--n", str(a.sharded_n), "--steps", str(a.steps), "--warmup", str(a.warmup),
+           "--batch", str(a.batch), "--nbatches", str(a.nbatches), "--inflight", str(a.inflight), "--mode", "fast",
+           "--cache", a.cache, "--cache-frac", str(a.cache_frac)]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
+                                                           "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID",
+                                                           "SHINE_BENCH_ARGV")}
+    env["OMP_NUM_THREADS"] = str(max(1, min(host_threads(), 16 * world)))
+    t0 = time.time()
+    r = child_json(cmd, env=env)
+    keys = ("value", "ms_per_step", "n_gpus", "gpu_slots", "recall_at_10", "search_mode", "scaling", "one_gpu_value",
+            "speedup_vs_one_gpu", "reads", "bounds", "config", "data", "stub")
+    out = {k: r[k] for k in keys if k in r}
+    out["wall_s"] = time.time() - t0
+    return out
 
 
 def main():
     a = parse()
     if a.placement == "sharded":
         return run_sharded(a)
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return launch(a)
+    if os.environ.get("SHINE_BENCH_STUB"):
+        return stub_rank(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
-    torch.cuda.set_device(local)
+    # the in-flight streams first of all streams of the process: distinct hardware queues (hip_streams)
+    streams = hip_streams(torch, max(1, a.inflight), local)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -203,7 +305,6 @@ def main():
     # stream, so batches on different streams run concurrently
     if a.nbatches < a.inflight:
         raise SystemExit("--nbatches must be >= --inflight (batches in flight write distinct output buffers)")
-    streams = [torch.cuda.Stream() for _ in range(max(1, a.inflight))]
     torch.cuda.set_stream(streams[0])
 
     def step(i, rec=None, ef=None, ix=None):
@@ -421,7 +522,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
-        cpu = cpu_baseline(paths, q, a, recall)
+        cpu = cpu_baseline(paths, q, a, gt, runs["exact"]["ids"] if "exact" in runs else None)
 
     if rank == 0:
         total_q = a.steps * a.batch * world
@@ -461,11 +562,43 @@ def main():
                          "algorithmic_bytes_per_launch": float(np.mean(bytes_steps)),
                          "mean_distcomps_per_query": float(qs_h[:, 0].mean())},
             "cpu_baseline": cpu,
+            "hw_queues": HW_QUEUES or "HIP default (4)",
         }
-        print(json.dumps(out), flush=True)
     idx.close()
     if dist:
         dist.destroy_process_group()
+    if rank == 0:
+        if a.sharded_leg == "on" or (a.sharded_leg == "auto" and world > 1):
+            del qd, ids, dists, qs
+            torch.cuda.empty_cache()
+            out["sharded"] = sharded_leg(a, world)
+        print(json.dumps(out), flush=True)
+
+
+def stub_rank(a):
+    """SHINE_BENCH_STUB=1 (CPU tests of the launcher): each rank joins a gloo group instead of doing GPU work; rank 0
+    counts the ranks with an all-reduce, runs the sharded-leg child (itself a stub) and prints a line of the real
+    line's shape."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        seen = int(t.item())
+        dist.destroy_process_group()
+    else:
+        seen = 1
+    if rank != 0:
+        return
+    out = {"metric": "QPS at recall@10>=0.95, SIFT1M d=128 batch=1024", "value": 0.0, "unit": "queries/s",
+           "n_gpus": world, "ranks_seen": seen, "stub": True, "scaling": "weak",
+           "config": {"parallelism": f"replica{world}"}}
+    if a.sharded_leg == "on" or (a.sharded_leg == "auto" and world > 1):
+        out["sharded"] = sharded_leg(a, world)
+    print(json.dumps(out), flush=True)
 
 
 def sharded_plan(slots: int, ndev: int, batch: int, nbatches: int):
@@ -486,14 +619,18 @@ def run_sharded(a):
     stripes through its own virtual view (xGMI when the slots are distinct GPUs), queries split id % S.  Reports
     QPS, recall, the share of the algorithmic bytes that left the answering slot's stripe (qstats words 8-11) and the
     xGMI bound that share implies (7 links x 153 GB/s inbound per GPU)."""
+    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+        raise SystemExit("--placement sharded runs as one process driving every GPU slot (not under torchrun)")
+    if os.environ.get("SHINE_BENCH_STUB"):
+        print(json.dumps({"value": 0.0, "n_gpus": a.gpus, "gpu_slots": a.slots or a.gpus, "stub": True}), flush=True)
+        return
     import torch
     import shine_amd
     from shine_amd import datasets as D
-    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
-        raise SystemExit("--placement sharded runs as one process driving every GPU slot (not under torchrun)")
     ndev = torch.cuda.device_count()
     S = a.slots or a.gpus
-    gpus, rows = sharded_plan(S, ndev, a.batch, a.nbatches)
+    # every slot answers a.batch queries per step (global batch a.batch x S, split id % S): per-GPU work is fixed
+    gpus, rows = sharded_plan(S, ndev, a.batch * S, a.nbatches)
     phys = len(set(gpus))
     dim, M, efc, ef, shards = 96, 16, 200, 128, 8
     key = hashlib.sha1(f"{a.n}-{dim}-{M}-{efc}-{shards}-deep_like-l2-v1".encode()).hexdigest()[:12]
@@ -512,7 +649,7 @@ def run_sharded(a):
     info = idx.info()
     log(f"sharded index: {info['num_nodes']} nodes over {S} slots ({phys} GPUs), id space {info['id_space']}, "
         f"{info['device_bytes'] / 2**20:.0f} MiB per GPU, cache fraction {info['cache_fraction']:.3f}")
-    nb, B, k = a.nbatches, a.batch, a.k
+    nb, B, k = a.nbatches, a.batch * S, a.k
     q = D.deep_like(B * nb, seed=2, d=dim)
     gt = ground_truth(torch, base, q, k, 0)
     qd, ids, qs, streams = [], [], [], []
@@ -564,22 +701,32 @@ def run_sharded(a):
         el = time.perf_counter() - t0
         algo = idx.algorithmic_bytes(st) / st.shape[0]
         remote = (st[:, 8].astype(np.float64) * dim * 4 + st[:, 9].astype(np.float64) * 4 * 2 * M).mean()
-        hits, misses = st[:, 10:12].sum(), st[:, 8:10].sum()
+        vec_hits, vec_remote = int(st[:, 10].sum()), int(st[:, 8].sum())
+        hits, misses = int(st[:, 10:12].sum()), int(st[:, 8:10].sum())
+        node_reads = int(st[:, 0].sum())  # every distance computation reads one record (rdma::read_node)
         qps = a.steps * B / el
+        one = one_gpu_rate(a, torch, shine_amd, paths, dim, M, ef, k, q, rows, mode) if mode_name == "fast" else None
         xgmi_in = 7 * 153e9
         line = {
             "metric": "QPS at recall@10, cfg4-shaped sharded index (DEEP-like 96-d L2, 8 memory-node dumps)",
             "value": qps, "unit": "queries/s", "n_gpus": phys, "gpu_slots": S, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": el * 1e3 / a.steps, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "ms_per_step": el * 1e3 / a.steps, "higher_is_better": True, "vs_baseline": None,
+            "scaling": "weak in queries (a.batch per slot per step) over one fixed index",
+            "one_gpu_value": one, "speedup_vs_one_gpu": (qps / one) if one else None,
             "dtype": "f32", "search_mode": mode_name, "recall_at_10": recall,
             "data": f"synthetic DEEP-shaped (L2-normalised f32, {a.n} x 96; N reduced from 100M), index built in-run",
             "config": {"workload": "cfg4-shaped sharded knn, M=16 efC=200 ef=128 k=10", "n": a.n, "dim": dim,
-                       "M": M, "efc": efc, "ef": ef, "k": k, "shards": shards, "batch": B, "placement": "sharded",
-                       "gpus": gpus, "cache_fraction": info["cache_fraction"],
+                       "M": M, "efc": efc, "ef": ef, "k": k, "shards": shards, "batch": B, "batch_per_slot": a.batch,
+                       "placement": "sharded", "gpus": gpus, "cache_fraction": info["cache_fraction"],
                        "batches_in_flight": max(1, a.inflight)},
             "reads": {"algorithmic_bytes_per_query": algo, "off_stripe_bytes_per_query": remote,
-                      "off_stripe_share": remote / algo, "cache_hit_rate": hits / max(1, hits + misses),
-                      "cache_hits": int(hits), "cache_misses": int(misses)},
+                      "off_stripe_share": remote / algo,
+                      # statistics.hh:171-173: hits over every record lookup (the reference reads every record
+                      # remotely, so every node read is a cache lookup there)
+                      "cache_hit_rate": vec_hits / max(1, node_reads),
+                      "off_stripe_hit_rate": vec_hits / max(1, vec_hits + vec_remote),
+                      "node_reads": node_reads, "cache_hits": vec_hits, "cache_misses": node_reads - vec_hits,
+                      "off_stripe_record_hits": hits, "off_stripe_record_misses": misses},
             "bounds": {"hbm_qps": phys * HBM_PEAK_GBPS * 1e9 / algo,
                        "xgmi_qps": (phys * xgmi_in / remote) if phys > 1 and remote > 0 else None,
                        "note": "xgmi_qps: every GPU's off-stripe reads at 7 x 153 GB/s inbound; with repeated slots "
@@ -589,6 +736,40 @@ def run_sharded(a):
         lines.append(line)
     idx.close()
     print(json.dumps(lines[0]), flush=True)
+
+
+def one_gpu_rate(a, torch, shine_amd, paths, dim, M, ef, k, q, rows, mode):
+    """The same dumps as a replica on GPU 0, the same global batches (each slot's share one launch, in flight on
+    rotating streams): the one-GPU rate the sharded leg's speedup is quoted against."""
+    nb, S = len(rows), len(rows[0])
+    with shine_amd.Index.open(paths, dim, M, shine_amd.METRIC_L2, gpus=[0]) as ix:
+        ix.set_search_mode(mode)
+        with torch.cuda.device(0):
+            streams = [torch.cuda.Stream() for _ in range(max(1, a.inflight))]
+            qd = [[torch.from_numpy(np.ascontiguousarray(q[rows[b][s]])).cuda() for s in range(S)] for b in range(nb)]
+            ids = [[torch.empty((len(rows[b][s]), k), dtype=torch.int32, device="cuda") for s in range(S)]
+                   for b in range(nb)]
+        n_launch = [0]
+
+        def step(i):
+            b = i % nb
+            for s in range(S):
+                n = len(rows[b][s])
+                if n:
+                    ix.knn_device(qd[b][s].data_ptr(), n, k, ef, ids[b][s].data_ptr(), None, None,
+                                  stream=streams[n_launch[0] % len(streams)].cuda_stream)
+                    n_launch[0] += 1
+
+        for i in range(nb + a.warmup):
+            step(i)
+        torch.cuda.synchronize(0)
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            step(a.warmup + i)
+        torch.cuda.synchronize(0)
+        el = time.perf_counter() - t0
+    B = sum(len(r) for r in rows[0])
+    return a.steps * B / el
 
 
 def ground_truth(torch, base, q, k, metric):
@@ -639,35 +820,89 @@ def native_oracle():
         return False
 
 
-def cpu_baseline(paths, q, a, gpu_recall):
-    """The oracle (C++ restatement of the reference's knn) on this host's cores, same dump, same queries."""
+def granted_cpus(n: int):
+    """The first n CPUs of this process's affinity mask (the CPUs the box grants this job)."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except Exception:
+        cpus = list(range(os.cpu_count() or 1))
+    return cpus[:max(1, n)]
+
+
+def fp_order_probe(O, native, dumps, dim, M, metric, q, k, ef, threads, cpus, gpu_ids=None):
+    """The -ffast-math question: the oracle built with the reference's flags against the portable checker
+    build (explicit FMA chain, fixed left-to-right horizontal sum) on the same queries and dump."""
+    chk = O.OracleIndex(dumps, dim, M, metric)
+    ci, cd, _ = chk.knn(q, k, ef, threads=threads, cpus=cpus)
+    chk.close()
+    out = {"queries": int(q.shape[0])}
+    if native:
+        nat = O.OracleIndex(dumps, dim, M, metric, native=True)
+        ni, nd, _ = nat.knn(q, k, ef, threads=threads, cpus=cpus)
+        nat.close()
+        out["native_same_ids"] = float((ni == ci).all(1).mean())
+        out["native_same_id_sets"] = float((np.sort(ni, 1) == np.sort(ci, 1)).all(1).mean())
+        same = ni == ci  # positions holding the same record in both builds
+        out["native_dist_bitwise_rate"] = float((nd.view(np.uint32) == cd.view(np.uint32))[same].mean())
+        ulp = np.abs(nd.view(np.int32).astype(np.int64) - cd.view(np.int32).astype(np.int64))[same]
+        out["native_max_ulp_diff"] = int(ulp.max()) if ulp.size else 0
+        out["native_max_abs_dist_diff"] = float(np.abs(nd.astype(np.float64) - cd)[same].max()) if same.any() else 0.0
+    if gpu_ids is not None:
+        out["checker_same_ids_as_gpu_exact"] = float((gpu_ids[:q.shape[0]] == ci).all(1).mean())
+    return out, ci
+
+
+def cpu_baseline(paths, q, a, gt, gpu_exact_ids=None):
+    """The oracle (C++ restatement of the reference's knn) on this host's cores, same dump, same queries: built with
+    the reference's flags (-O3 -march=native -ffast-math -mavx2) for this host, one worker per granted CPU, each
+    pinned to its CPU (compute_node.cc:362-380).  Also reported: its recall on the sample, and the fp-order probe —
+    the native build against the portable checker build on this sample and on a float-valued DEEP-shaped
+    inner-product index, where -ffast-math could reorder the distance sums."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle as O
+    from shine_amd import datasets as D
+    import shine_amd
     native = native_oracle()
     dumps = [np.fromfile(p, dtype=np.uint8) for p in paths]
-    I = O.OracleIndex(dumps, a.dim, a.M, 0, native=native)
     th = host_threads()
+    cpus = granted_cpus(th)
+    th = len(cpus)
+    I = O.OracleIndex(dumps, a.dim, a.M, 0, native=native)
     n = min(q.shape[0], 512)
     t0 = time.perf_counter()
-    I.knn(q[:n], a.k, a.ef, threads=th)
+    I.knn(q[:n], a.k, a.ef, threads=th, cpus=cpus)
     probe = time.perf_counter() - t0
     reps = max(1, int(a.cpu_seconds / max(probe, 1e-3)))
     t0 = time.perf_counter()
-    done = 0
+    done, got = 0, {}
     for r in range(reps):
         s = (r * n) % max(1, q.shape[0] - n + 1)
-        I.knn(q[s:s + n], a.k, a.ef, threads=th)
+        ids, _, _ = I.knn(q[s:s + n], a.k, a.ef, threads=th, cpus=cpus)
         done += n
+        got.setdefault(s, ids)
     el = time.perf_counter() - t0
     I.close()
+    rows = sorted(got)
+    cpu_ids = np.concatenate([got[s] for s in rows])
+    cpu_gt = np.concatenate([gt[s:s + n] for s in rows])
+    recall = D.recall_at_k(cpu_ids, cpu_gt, a.k)
+    probe_sift, _ = fp_order_probe(O, native, dumps, a.dim, a.M, 0, q[:n], a.k, a.ef, th, cpus,
+                                   gpu_ids=gpu_exact_ids)
+    # float data: a DEEP-shaped inner-product index (cfg 3's metric), 20K records, 1,024 queries at ef = 256
+    base_f = D.deep_like(20_000, seed=31, d=96)
+    q_f = D.deep_like(1024, seed=32, d=96)
+    dumps_f, _ = shine_amd.build(base_f, 16, 100, shine_amd.METRIC_IP, 1, seed=1234, threads=th)
+    probe_deep, _ = fp_order_probe(O, native, dumps_f, 96, 16, 1, q_f, a.k, 256, th, cpus)
     hw = host_cpu_info()
-    log(f"cpu baseline: {done} queries in {el:.1f}s on {th} threads ({hw})")
+    log(f"cpu baseline: {done} queries in {el:.1f}s on {th} pinned threads, recall {recall:.4f} ({hw}); fp-order "
+        f"probe sift {probe_sift}, deep-ip {probe_deep}")
     return {"value": done / el, "unit": "queries/s", "cores": th, "kind": "port",
             "flags": O.NATIVE_FLAGS if native else "-O3 -march=x86-64-v3 -ffp-contract=off (portable checker build)",
-            "host": hw, "pinned": False,
+            "host": hw, "pinned": True, "cpus": cpus, "recall_at_10": recall,
+            "fp_order_probe": {"sift_sample": probe_sift, "deep_ip_20k": probe_deep},
             "label": "reference-equivalent CPU path (restated), not the RDMA deployment",
             "sample": f"{done} queries (batches of {n} from the bench's query set, k={a.k}, ef={a.ef}) on the "
-                      f"same dump, {th} threads (this job's CPU share of the host), ~{a.cpu_seconds:.0f}s"}
+                      f"same dump, {th} worker threads pinned one per granted CPU, ~{a.cpu_seconds:.0f}s"}
 
 
 if __name__ == "__main__":

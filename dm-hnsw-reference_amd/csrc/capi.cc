@@ -641,9 +641,11 @@ int make_index(HostGraph G, int elem, const int* gpu_ids, uint32_t n_gpus, int p
     h->device_bytes = vlen + 4 * G.adj0.size() + replicated;
   }
   if (sharded) {
-    h->dev_of = std::move(newid);
-    h->host = std::move(G);
     h->devs = devs;
+    if (h->cached_rows || h->cached_list_rows) {  // a warmup may re-rank the stripes: keep what it relays out
+      h->dev_of = std::move(newid);
+      h->host = std::move(G);
+    }
   }
   *out = h.release();
   return SHINE_OK;
@@ -1158,6 +1160,22 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
   route_batch(h, queries, query_ids, nq, dest.data());
   std::vector<std::vector<uint32_t>> part(G);
   for (uint32_t i = 0; i < nq; ++i) part[dest[i]].push_back(i);
+  // the staging buffers below are written by plain host stores and may be regrown: nothing on a slot's stream may
+  // still read them (an earlier call that failed after enqueueing, or device-API work on the handle's stream)
+  for (uint32_t r = 0; r < G; ++r) {
+    if (part[r].empty()) continue;
+    HIP_TRY(hipSetDevice(h->reps[r].device));
+    HIP_TRY(hipStreamSynchronize(h->reps[r].stream));
+  }
+  // on an error after the first enqueue, the slots already enqueued are drained before returning
+  auto drain = [&](uint32_t upto, int rc) {
+    for (uint32_t r = 0; r < upto; ++r) {
+      if (part[r].empty()) continue;
+      (void)hipSetDevice(h->reps[r].device);
+      (void)hipStreamSynchronize(h->reps[r].stream);
+    }
+    return rc;
+  };
   // every slot's batch is staged through pinned host memory and enqueued before any wait
   for (uint32_t r = 0; r < G; ++r) {
     const uint32_t n = static_cast<uint32_t>(part[r].size());
@@ -1169,20 +1187,21 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     // per batch (copy -> kernel -> copy) that held the host back until each kernel finished: 3.0 M against 6.1 M QPS
     // with four batches in flight (profiles/r02/host_leg_probe.jsonl)
     constexpr unsigned kMapped = hipHostMallocMapped | hipHostMallocPortable;
-    if (int rc = R.hq.grow(n * d, kMapped)) return rc;
-    if (int rc = R.hids.grow(static_cast<size_t>(n) * k, kMapped)) return rc;
-    if (int rc = R.hd.grow(static_cast<size_t>(n) * k, kMapped)) return rc;
-    if (int rc = R.hqs.grow(static_cast<size_t>(n) * kQsWords + 8, kMapped)) return rc;
+    if (int rc = R.hq.grow(n * d, kMapped)) return drain(r, rc);
+    if (int rc = R.hids.grow(static_cast<size_t>(n) * k, kMapped)) return drain(r, rc);
+    if (int rc = R.hd.grow(static_cast<size_t>(n) * k, kMapped)) return drain(r, rc);
+    if (int rc = R.hqs.grow(static_cast<size_t>(n) * kQsWords + 8, kMapped)) return drain(r, rc);
     for (uint32_t j = 0; j < n; ++j)
       std::memcpy(R.hq.p + j * d, queries + static_cast<size_t>(part[r][j]) * d, d * sizeof(float));
     float *dq = nullptr, *dd = nullptr;
     uint32_t *dids = nullptr, *dqs = nullptr;
-    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&dq), R.hq.p, 0));
-    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&dids), R.hids.p, 0));
-    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&dd), R.hd.p, 0));
-    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&dqs), R.hqs.p, 0));
+    hipError_t pe = hipHostGetDevicePointer(reinterpret_cast<void**>(&dq), R.hq.p, 0);
+    if (pe == hipSuccess) pe = hipHostGetDevicePointer(reinterpret_cast<void**>(&dids), R.hids.p, 0);
+    if (pe == hipSuccess) pe = hipHostGetDevicePointer(reinterpret_cast<void**>(&dd), R.hd.p, 0);
+    if (pe == hipSuccess) pe = hipHostGetDevicePointer(reinterpret_cast<void**>(&dqs), R.hqs.p, 0);
+    if (pe != hipSuccess) return drain(r, set_error(SHINE_ERR_HIP, std::string("hipHostGetDevicePointer: ") + hipGetErrorString(pe)));
     if (int rc = enqueue_search(h, R, dq, n, k, ef, dids, dd, dqs, R.stream, true, access ? (*access)[r].p : nullptr))
-      return rc;
+      return drain(r + 1, rc);
   }
   double kernel_ms = 0;
   uint64_t retries = 0;
@@ -1238,7 +1257,12 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
 extern "C" {
 
 int shine_knn_batch(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
-                    uint32_t ef, uint32_t* out_ids, float* out_dists, uint32_t* qstats, shine_stats* stats) {
+                    uint32_t ef, uint32_t* out_ids, float* out_dists, shine_stats* stats) {
+  return shine_knn_batch_ex(h, queries, query_ids, nq, k, ef, out_ids, out_dists, nullptr, stats);
+}
+
+int shine_knn_batch_ex(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
+                       uint32_t ef, uint32_t* out_ids, float* out_dists, uint32_t* qstats, shine_stats* stats) {
   if (int rc = check_knn_args(h, k, ef)) return rc;
   if (stats) std::memset(stats, 0, sizeof(*stats));
   if (nq == 0) return SHINE_OK;
@@ -1285,7 +1309,12 @@ int shine_cache_warmup(shine_index_t h, const float* queries, const uint32_t* qu
   // 3. the same stripes re-laid out hottest first (a new layout beside the old one, then moved in)
   shine_index_t nh = nullptr;
   const std::vector<int> devs = h->devs;
-  if (int rc = make_index(std::move(h->host), h->elem, devs.data(), static_cast<uint32_t>(devs.size()), h->placement,
+  // the host graph moves into the new layout; if building it fails, the handle keeps its old layout and no host graph
+  // (a later warmup reports that instead of relaying out from emptied arrays)
+  HostGraph hg = std::move(h->host);
+  h->host = HostGraph{};
+  h->dev_of.clear();
+  if (int rc = make_index(std::move(hg), h->elem, devs.data(), static_cast<uint32_t>(devs.size()), h->placement,
                           h->cache_requested, &nh, &heat))
     return rc;
   nh->search_mode = h->search_mode;

@@ -409,7 +409,7 @@ int run(const Config& c) {
       ids.resize(static_cast<size_t>(n) * c.k);
       shine_stats st{};
       check(shine_knn_batch(h, db.comps.data() + static_cast<size_t>(s) * db.dim, db.ids.data() + s, n, c.k,
-                            c.ef_search, ids.data(), nullptr, nullptr, &st),
+                            c.ef_search, ids.data(), nullptr, &st),
             "shine_knn_batch");
       add(th.stats, st);
       for (uint32_t j = 0; j < n; ++j)
@@ -422,8 +422,9 @@ int run(const Config& c) {
     status("cache warmup");
     Interval& t_warm = interval("warmup_routing");
     t_warm.start();
-    ComputeThread warm;
-    run_batches(warmup, warm);
+    // the warmup split's record reads rank what every GPU caches (shine_cache_warmup; a no-op without a cache)
+    check(shine_cache_warmup(h, warmup.comps.data(), warmup.ids.data(), warmup.num_read(), c.k, c.ef_search),
+          "shine_cache_warmup");
     t_warm.stop();
   }
 

@@ -106,7 +106,8 @@ PROTOTYPES = {
                             C.POINTER(P)]),
     "shine_open_buffers_ex": (I32, [C.POINTER(PU8), C.POINTER(U64), U32, U32, U32, I32, I32, C.POINTER(I32), U32, I32,
                                     C.c_double, C.POINTER(P)]),
-    "shine_knn_batch": (I32, [P, P, P, U32, U32, U32, P, P, P, C.POINTER(Stats)]),
+    "shine_knn_batch": (I32, [P, P, P, U32, U32, U32, P, P, C.POINTER(Stats)]),  # SURVEY.md §8b's 9 arguments
+    "shine_knn_batch_ex": (I32, [P, P, P, U32, U32, U32, P, P, P, C.POINTER(Stats)]),
     "shine_release_stream": (I32, [P, P]),
     "shine_cache_warmup": (I32, [P, P, P, U32, U32, U32]),
     "shine_knn_batch_device": (I32, [P, U32, P, U32, U32, U32, P, P, P, P]),

@@ -115,7 +115,7 @@ class Index:
 
     # ---- queries -----------------------------------------------------------------------------------------
     def knn(self, queries: np.ndarray, k: int, ef: int, query_ids: np.ndarray | None = None) -> KnnResult:
-        """shine_knn_batch: query i is answered on GPU slot query_ids[i] % n_gpus (position when None)."""
+        """shine_knn_batch_ex (shine_knn_batch plus per-query counters): query i is answered on GPU slot query_ids[i] % n_gpus (position when None)."""
         q = np.ascontiguousarray(queries, dtype=np.float32)
         if q.ndim != 2 or q.shape[1] != self.dim:
             raise ValueError(f"queries must be (nq, {self.dim})")
@@ -127,7 +127,7 @@ class Index:
         dists = np.empty((nq, k), dtype=np.float32)
         qs = np.empty((nq, L.QS_WORDS), dtype=np.uint32)
         st = L.Stats()
-        L.check(L.lib().shine_knn_batch(self._h, _ptr(q), _ptr(qid), nq, k, ef, _ptr(ids), _ptr(dists), _ptr(qs),
+        L.check(L.lib().shine_knn_batch_ex(self._h, _ptr(q), _ptr(qid), nq, k, ef, _ptr(ids), _ptr(dists), _ptr(qs),
                                         C.byref(st)))
         return KnnResult(ids, dists, qs, st.as_dict())
 

@@ -148,12 +148,16 @@ int shine_open_buffers_ex(const uint8_t* const* dumps, const uint64_t* sizes, ui
  * query_ids (nullable): the queries' ids (HNSW::knn's q_id); query i is answered on GPU slot query_ids[i] % n_gpus
  * (the compute-node split, read_data.hh:57-58), or on slot i % n_gpus when NULL.
  * out_ids: nq × k uids, in the reference's result order (top_candidates heap-array order, hnsw.hh:300-303).
- * out_dists (nullable): nq × k.  qstats (nullable): nq × SHINE_QS_WORDS.  stats (nullable): aggregates.
+ * out_dists (nullable): nq × k.  stats (nullable): aggregates.  The signature is SURVEY.md §8b's.
  * Requires ef >= k (hnsw.hh:36).  Synchronous: every slot's batch is staged in pinned host memory mapped into the
  * GPU's address space (the kernels read the queries and write the results over PCIe themselves, no copy engine) and
  * enqueued before the call waits. */
 int shine_knn_batch(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
-                    uint32_t ef, uint32_t* out_ids, float* out_dists, uint32_t* qstats, shine_stats* stats);
+                    uint32_t ef, uint32_t* out_ids, float* out_dists, shine_stats* stats);
+
+/* shine_knn_batch with the per-query counters as well: qstats (nullable) nq × SHINE_QS_WORDS, query i's row. */
+int shine_knn_batch_ex(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
+                       uint32_t ef, uint32_t* out_ids, float* out_dists, uint32_t* qstats, shine_stats* stats);
 
 /* Same with device-resident inputs/outputs on GPU `gpu_slot` of the handle, enqueued on `stream`
  * (hipStream_t; NULL = the handle's stream).  Asynchronous: returns after enqueue.  qstats (device,

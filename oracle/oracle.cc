@@ -16,12 +16,19 @@
 //  compute-node cache (hit/miss does not change results), routing.
 //
 //  Distance FP order.  The reference computes L2 / IP with hnswlib's AVX2 kernels under -O3 -march=native
-//  -ffast-math (src/hnsw/distance.hh:11-151, CMakeLists.txt:16): 8 lane accumulators, lane j summing elements
-//  i ≡ j (mod 8) of each 16-wide block, multiply-add contracted to FMA (GCC's default -ffp-contract=fast),
-//  then TmpRes[0..7] summed, then the scalar tail.  -ffast-math leaves the final horizontal-sum order to the
-//  compiler, so this restatement FIXES it as left-to-right (TmpRes[0]+TmpRes[1]+...+TmpRes[7]) and is compiled
-//  with -ffp-contract=off + explicit fmaf / _mm256_fmadd_ps so the order is exactly what is written.  On
-//  integer-valued data (SIFT-like) every partial sum is exact (< 2^24) and the order is irrelevant.
+//  -ffast-math (src/hnsw/distance.hh:11-151, CMakeLists.txt:16), so their rounding is whatever GCC makes of the
+//  expressions, and that is not one fixed order: `l2_as_written` / `ip_as_written` below restate the expressions
+//  with no order pinned, and GCC 11.4 -ffast-math reassociates them (per 16-wide block t = fma(x0, y0, rn(x1*y1)),
+//  acc += t; the eight lanes summed as a tree whose pairing changes with the inlining context, e.g.
+//  ((t0+t1)+(t2+t3))+((t4+t5)+(t6+t7)) inlined, ((t3+t4)+(t5+t7))+((t0+t2)+(t1+t6)) out of line; IP's
+//  `1 - (sum + tail)` distributed into a chain of subtractions).  The reference's own call sites (inlined into
+//  search_for_one / search_level) may each round differently, so no restatement can reproduce its float roundings
+//  bit for bit (tests/test_fp_order.py).  This restatement therefore FIXES one order — 8 lane
+//  accumulators, lane j an fma chain over elements i ≡ j (mod 8) of the 16-aligned prefix, the lanes added left to
+//  right, then the scalar tail — compiled with -ffp-contract=off + explicit fmaf / _mm256_fmadd_ps so the order is
+//  exactly what is written; the GPU kernels and the builder use the same order.  The reference-flags build
+//  (`make native`, bench.py's CPU baseline) evaluates the as-written form instead, as the reference's build does.
+//  On integer-valued data (SIFT-like) every partial sum is exact (< 2^24) and all of these agree bit for bit.
 //
 //  Parity status: the reference ships no tests, fixtures or golden vectors, and compiling/running it in this
 //  pipeline was refused.  The heap / sort / RNG behaviour is pinned against libstdc++ itself
@@ -35,6 +42,9 @@
 #include <cstring>
 #include <random>
 #include <thread>
+
+#include <pthread.h>
+#include <sched.h>
 #include <unordered_set>
 #include <vector>
 
@@ -106,8 +116,56 @@ static f32 ip_distance(const f32* a, const f32* b, size_t dim) {
   return 1.0f - (res + res_tail);                                                  // distance.hh:141
 }
 
+// ---- The same two distances in the reference's expression shape (distance.hh:11-76, 80-151), with no FP order
+// pinned: per 16-wide step two 8-lane updates `acc = acc + d * d` (`acc + a * b`), the eight lanes summed in one
+// expression, then the scalar tail as a running `+=`.  How these round is left to the compiler: under the
+// reference's flags (-O3 -march=native -ffast-math -mavx2, CMakeLists.txt:16) GCC contracts and reassociates
+// them.  The native (reference-flags) build of the oracle evaluates these, the CPU baseline times them, and
+// tests/test_fp_order.py checks that the fixed-order functions above reproduce them bit for bit.
+#ifdef ORACLE_AVX2
+static f32 l2_as_written(const f32* a, const f32* b, size_t dim) {
+  const size_t q16 = dim >> 4 << 4;
+  __m256 acc = _mm256_setzero_ps();
+  for (size_t i = 0; i < q16; i += 16) {
+    __m256 d = _mm256_sub_ps(_mm256_loadu_ps(a + i), _mm256_loadu_ps(b + i));
+    acc = _mm256_add_ps(acc, _mm256_mul_ps(d, d));
+    d = _mm256_sub_ps(_mm256_loadu_ps(a + i + 8), _mm256_loadu_ps(b + i + 8));
+    acc = _mm256_add_ps(acc, _mm256_mul_ps(d, d));
+  }
+  alignas(32) f32 t[8];
+  _mm256_store_ps(t, acc);
+  f32 r = t[0] + t[1] + t[2] + t[3] + t[4] + t[5] + t[6] + t[7];
+  for (size_t i = q16; i < dim; ++i) {
+    const f32 d = a[i] - b[i];
+    r += d * d;
+  }
+  return r;
+}
+
+static f32 ip_as_written(const f32* a, const f32* b, size_t dim) {
+  const size_t q16 = dim >> 4 << 4;
+  __m256 acc = _mm256_setzero_ps();
+  for (size_t i = 0; i < q16; i += 16) {
+    acc = _mm256_add_ps(acc, _mm256_mul_ps(_mm256_loadu_ps(a + i), _mm256_loadu_ps(b + i)));
+    acc = _mm256_add_ps(acc, _mm256_mul_ps(_mm256_loadu_ps(a + i + 8), _mm256_loadu_ps(b + i + 8)));
+  }
+  alignas(32) f32 t[8];
+  _mm256_store_ps(t, acc);
+  const f32 r = t[0] + t[1] + t[2] + t[3] + t[4] + t[5] + t[6] + t[7];
+  f32 tail = 0;
+  for (size_t i = q16; i < dim; ++i) tail += a[i] * b[i];
+  return 1.0f - (r + tail);
+}
+#endif
+
+// L2Distance / IPDistance (distance.hh:153-161).  The reference-flags build (CPU baseline) evaluates the
+// as-written form, as the reference's own build does; the checker evaluates the fixed order.
 static inline f32 distance(int metric, const f32* a, const f32* b, size_t dim) {
-  return metric == 1 ? ip_distance(a, b, dim) : l2(a, b, dim);  // L2Distance / IPDistance (distance.hh:153-161)
+#if defined(__FAST_MATH__) && defined(ORACLE_AVX2)
+  return metric == 1 ? ip_as_written(a, b, dim) : l2_as_written(a, b, dim);
+#else
+  return metric == 1 ? ip_distance(a, b, dim) : l2(a, b, dim);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -565,12 +623,21 @@ void oracle_free(void* h) { delete static_cast<Index*>(h); }
 
 // knn over a batch; queries are processed by n_threads worker threads (one query per thread at a time,
 // like `--threads T --coroutines 1`), each with its own SearchState.  stats: nq × 8 u32 (QS_* layout).
-int oracle_knn(void* h, const float* queries, uint32_t nq, uint32_t k, uint32_t ef, uint32_t* out_ids,
-               float* out_dists, uint32_t* stats, uint32_t n_threads) {
+// cpus (nullable): worker t is pinned to CPU cpus[t] (the reference pins its compute threads to cores,
+// compute_node.cc:362-380, core_assignment.hh:22-44); timing only, results do not depend on it.
+int oracle_knn_pinned(void* h, const float* queries, uint32_t nq, uint32_t k, uint32_t ef, uint32_t* out_ids,
+                      float* out_dists, uint32_t* stats, uint32_t n_threads, const int32_t* cpus) {
   const Index& I = *static_cast<Index*>(h);
   if (ef < k) return 1;  // hnsw.hh:36 lib_assert(ef_search >= k)
   if (I.ep_ptr() == 0) return 2;
   std::atomic<u32> next{0};
+  auto pin = [&](u32 t) {
+    if (!cpus) return;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(cpus[t], &set);
+    pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+  };
   auto worker = [&]() {
     SearchState st;
     for (;;) {
@@ -581,20 +648,42 @@ int oracle_knn(void* h, const float* queries, uint32_t nq, uint32_t k, uint32_t 
       if (stats) std::memcpy(stats + static_cast<size_t>(qi) * QS_WORDS, st.qs, sizeof(st.qs));
     }
   };
-  if (n_threads <= 1) {
+  if (n_threads <= 1 && !cpus) {
     worker();
   } else {
     std::vector<std::thread> ts;
-    for (u32 t = 0; t < n_threads; ++t) ts.emplace_back(worker);
+    for (u32 t = 0; t < std::max<u32>(1, n_threads); ++t) ts.emplace_back([&, t]() { pin(t); worker(); });
     for (auto& t : ts) t.join();
   }
   return 0;
+}
+
+int oracle_knn(void* h, const float* queries, uint32_t nq, uint32_t k, uint32_t ef, uint32_t* out_ids,
+               float* out_dists, uint32_t* stats, uint32_t n_threads) {
+  return oracle_knn_pinned(h, queries, nq, k, ef, out_ids, out_dists, stats, n_threads, nullptr);
 }
 
 // Distances of explicit (query, node-uid) pairs, for distance-kernel parity.  node_uids index the dense
 // record order of shard 0..n (the order records appear in the dumps).
 float oracle_distance(int metric, const float* a, const float* b, uint32_t dim) {
   return distance(metric, a, b, dim);
+}
+
+// The as-written form (its rounding is whatever this build's flags make of it; see l2_as_written), called out of
+// line, one pair per call.
+__attribute__((noinline)) float oracle_distance_as_written(int metric, const float* a, const float* b, uint32_t dim) {
+#ifdef ORACLE_AVX2
+  return metric == 1 ? ip_as_written(a, b, dim) : l2_as_written(a, b, dim);
+#else
+  return distance(metric, a, b, dim);
+#endif
+}
+
+// The same as-written form in another context: distance() inlined into a loop over n pairs, as the reference's
+// search loops call Distance::dist (hnsw.hh:376, 458).  Under -ffast-math the two contexts may round differently.
+void oracle_distances_in_loop(int metric, const float* a, const float* b, uint32_t n, uint32_t dim, float* out) {
+  for (uint32_t i = 0; i < n; ++i)
+    out[i] = distance(metric, a + static_cast<size_t>(i) * dim, b + static_cast<size_t>(i) * dim, dim);
 }
 
 // ---- libstdc++ pinning hooks: run the SAME std:: calls on caller data so the tests can compare the GPU's

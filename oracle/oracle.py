@@ -42,6 +42,8 @@ def lib(path: Path = LIB_PATH):
         L.oracle_free.argtypes = [P]
         L.oracle_knn.restype = I32
         L.oracle_knn.argtypes = [P, P, U32, U32, U32, P, P, P, U32]
+        L.oracle_knn_pinned.restype = I32
+        L.oracle_knn_pinned.argtypes = [P, P, U32, U32, U32, P, P, P, U32, P]
         L.oracle_distance.restype = C.c_float
         L.oracle_distance.argtypes = [I32, P, P, U32]
         L.oracle_selftest_heap.restype = I32
@@ -86,13 +88,19 @@ class OracleIndex:
         self._h = self._lib.oracle_open(ptrs, sizes, len(dumps), dim, M, metric)
         self.dim = dim
 
-    def knn(self, queries, k, ef, threads=1):
+    def knn(self, queries, k, ef, threads=1, cpus=None):
+        """cpus: pin worker t to CPU cpus[t] (len(cpus) == threads)."""
         q = np.ascontiguousarray(queries, dtype=np.float32)
         nq = q.shape[0]
         ids = np.empty((nq, k), np.uint32)
         dd = np.empty((nq, k), np.float32)
         qs = np.empty((nq, QS_WORDS), np.uint32)
-        rc = self._lib.oracle_knn(self._h, _p(q), nq, k, ef, _p(ids), _p(dd), _p(qs), threads)
+        if cpus is not None:
+            cp = np.ascontiguousarray(cpus, np.int32)
+            assert cp.size == threads
+            rc = self._lib.oracle_knn_pinned(self._h, _p(q), nq, k, ef, _p(ids), _p(dd), _p(qs), threads, _p(cp))
+        else:
+            rc = self._lib.oracle_knn(self._h, _p(q), nq, k, ef, _p(ids), _p(dd), _p(qs), threads)
         if rc != 0:
             raise RuntimeError(f"oracle_knn failed: {rc}")
         return ids, dd, qs

@@ -109,7 +109,8 @@ def test_missing_file_is_io_error(tmp_path):
 def test_null_arguments_are_arg_errors():
     lib = L.lib()
     assert lib.shine_open_buffers(None, None, 1, 128, 8, 0, 0, None, 0, None) == L.ERR_ARG
-    assert lib.shine_knn_batch(None, None, None, 1, 10, 10, None, None, None, None) == L.ERR_ARG
+    assert lib.shine_knn_batch(None, None, None, 1, 10, 10, None, None, None) == L.ERR_ARG
+    assert lib.shine_knn_batch_ex(None, None, None, 1, 10, 10, None, None, None, None) == L.ERR_ARG
     assert lib.shine_set_search_mode(None, L.MODE_FAST) == L.ERR_ARG
     assert lib.shine_close(None) == L.OK
     assert lib.shine_last_error()  # a message is recorded

@@ -1,5 +1,6 @@
-"""Diagnostics: one 1,024-query fast-mode batch on the 1M SIFT-shaped index, for rocprofv3 --pmc passes
-(SQ instruction mix / wait counters of the search kernel).  Builds the phase-profile index if missing."""
+"""Diagnostics: one 1,024-query batch on the 1M SIFT-shaped index, for rocprofv3 --pmc passes (SQ instruction mix /
+wait counters of the search kernel).  MODE=fast (default) or exact; EF (default 128).  Builds the phase-profile index
+if missing."""
 import os
 import sys
 from pathlib import Path
@@ -19,7 +20,7 @@ if not path.exists():
         sys.exit(0)
 q = D.sift_like(int(os.environ.get("NQ", "1024")), seed=2)
 idx = shine_amd.Index.open([path], 128, 16, 0, gpus=[0])
-idx.set_search_mode(shine_amd.MODE_FAST)
+idx.set_search_mode(shine_amd.MODE_FAST if os.environ.get("MODE", "fast") == "fast" else shine_amd.MODE_EXACT)
 for _ in range(int(os.environ.get("REPS", "2"))):
-    r = idx.knn(q, 10, 128)
+    r = idx.knn(q, 10, int(os.environ.get("EF", "128")))
 print("kernel_ms", r.stats["kernel_ms"], "L0 lists", r.qstats[:, 4].mean())
