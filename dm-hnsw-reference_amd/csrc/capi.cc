@@ -128,6 +128,7 @@ struct ShardedArray {
 // stream a caller enqueues on gets its own, so batches on different streams run concurrently on one GPU.
 struct Scratch {
   DevBuf<uint32_t> visited, vlog, counter, ovf, qs;
+  DevBuf<uint32_t> spill_flags;  // fast kernel: which of the `visited` bitmaps a spilled query holds (all zero between calls)
   DevBuf<unsigned long long> heaps;  // global-heap pass
   // host memory the last pass of every call writes: [0..2] the queries each pass handed on, [3] = 1 once written,
   // [4] the most nodes a query of that call marked visited (sizes the next call's light pass and visited tables;
@@ -141,7 +142,7 @@ struct Scratch {
   uint32_t table_floor = 0;      // a learned table that overflowed is never learned again below twice its size
   uint32_t last_ef = 0;          // ef of the last call: what it visited says nothing about another ef
   void release() {
-    for (auto* b : {&visited, &vlog, &counter, &ovf, &qs}) b->release();
+    for (auto* b : {&visited, &vlog, &counter, &ovf, &qs, &spill_flags}) b->release();
     heaps.release();
     seen.release();
     seen_dev = nullptr;
@@ -667,6 +668,16 @@ struct LaunchShape {
   uint32_t vis16, vis_bits;  // fast kernel: u16 quotient visited entries over a vis_bits-bit id space
 };
 
+// spilled visited tables a fast pass may hold at once (SearchArgs::spill_flags)
+constexpr uint32_t kSpillSlots = 64;
+
+// the inverse of an odd multiplier mod 2^32 (Newton: each step doubles the correct low bits)
+uint32_t inverse_odd(uint32_t m) {
+  uint32_t x = m;  // correct to 3 bits: m * m == 1 (mod 8)
+  for (int i = 0; i < 4; ++i) x *= 2u - m * x;
+  return x;
+}
+
 uint32_t pow2_at_least(uint32_t x) {
   uint32_t p = 1;
   while (p < x) p <<= 1;
@@ -890,9 +901,20 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     a.g = dev_graph(h, R);
     if (!a.g.vec || !a.g.adj0 || !a.g.uid || !a.g.up_base)
       return set_error(SHINE_ERR_HIP, "search launch: an index array is missing on this GPU slot");
-    if (pass == PASS_LIGHT || pass == PASS_GLOBAL) {
-      const uint32_t need = std::max(pick_shape(h, R, nq, ef, PASS_LIGHT).grid, pick_shape(h, R, nq, ef, PASS_GLOBAL).grid);
+    if (pass == PASS_LIGHT || pass == PASS_GLOBAL || pass == PASS_FAST) {
+      // the fallback passes' bitmaps; the fast pass borrows them for its spilled tables (it runs first on the stream
+      // and hands every one back zeroed)
+      const uint32_t need = std::max<uint32_t>({pick_shape(h, R, nq, ef, PASS_LIGHT).grid,
+                                                pick_shape(h, R, nq, ef, PASS_GLOBAL).grid, kSpillSlots});
       if (int rc = ensure_bitmaps(h, S, s, need)) return rc;
+    }
+    if (pass == PASS_FAST && !env_int("SHINE_DEBUG_NO_SPILL", 0)) {
+      if (!S.spill_flags.p) {
+        if (int rc = S.spill_flags.grow(kSpillSlots)) return rc;
+        HIP_TRY(hipMemsetAsync(S.spill_flags.p, 0, kSpillSlots * sizeof(uint32_t), s));
+      }
+      a.spill_flags = S.spill_flags.p;
+      a.spill_slots = std::min<uint32_t>(kSpillSlots, S.slots);
     }
     if (pass == PASS_GLOBAL) {
       a.heap_stride = align16(8ull * ef) / 8 + sh.cap;
@@ -922,6 +944,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     a.vis16 = sh.vis16;
     a.vis_bits = sh.vis_bits;
     a.vis_mul = 0x9E3779B1u;  // odd: x -> x * mul mod 2^vis_bits permutes the id space
+    a.vis_mul_inv = inverse_odd(a.vis_mul);
     a.sort_out = fast_mode ? 1u : 0u;
     a.access = d_access;
     if (i > 0) {

@@ -64,6 +64,13 @@ struct SearchArgs {
   uint32_t vis16;           // LDS visited table of u16 quotient entries (kernels_impl.h VisitedLds<1>)
   uint32_t vis_bits;        // ... bits of the id space the multiply permutes (vis_bits - log2(vis_cap) <= 10: buckets of 8, >= 3 distance bits)
   uint32_t vis_mul;         // ... odd multiplier
+  uint32_t vis_mul_inv;     // ... its inverse mod 2^32 (decodes an entry back to its id when a table spills)
+  // Fast kernel: a query that outgrows its LDS visited table spills it in place into one of spill_slots HBM bitmaps
+  // (the `visited` bitmaps of the stream's fallback passes, words_per_slot words each, all zero between uses) and
+  // goes on with its visited set there; spill_flags[i] = 1 while bitmap i is held.  spill_slots = 0: no spilling
+  // (the query is handed on to the next pass instead).
+  uint32_t* spill_flags;
+  uint32_t spill_slots;
 };
 
 struct DistArgs {

@@ -189,59 +189,70 @@ __device__ __forceinline__ u64 heap_pop_any(u64* h, int n, int lane) {
   return j == 0 ? value : bcast64(ent);  // lane 0 holds the path's first node
 }
 
-// Fast form for NaN-free heaps.  Along any root-to-leaf path of a heap the keys are monotone, so the
-// comparisons std::__push_heap makes on its way back up are false on a prefix of the path and true below it:
-// every path node whose winning child the comparator does not rank past the value shifts up, the first one
-// that does marks the landing slot.  Each 6-level window costs one LDS round trip: lane i plays window node
-// i+1 (1-based), reads both children entries (adjacent slots: one ds_read2_b64) and votes for the right
-// child; the walk follows the ballot on SGPRs; the on-path lanes then shift their winner up in place.
+// Per-lane constants of the pop window: lane i plays window node j = i + 1 (1-based, depth lj, offset oj within its
+// depth); anc has bit (a - 1) set for every window ancestor a of j, dir holds at that bit the side (1 = right) the
+// path takes from a towards j.  Lane 63 is outside the 63-node window.
+struct PopLane {
+  u64 anc = 0, dir = 0;
+  int lj = 0, oj = 0;
+  bool in_window = false;
+  __device__ __forceinline__ explicit PopLane(int lane) {
+    const int j1 = lane + 1;
+    lj = 31 - __clz(j1);
+    oj = j1 - (1 << lj);
+    in_window = lane < 63;
+    for (int t = 0; t < lj; ++t) {
+      const int a = j1 >> (lj - t);
+      anc |= 1ull << (a - 1);
+      dir |= static_cast<u64>((j1 >> (lj - t - 1)) & 1) << (a - 1);
+    }
+  }
+};
+
+// Fast form for NaN-free heaps.  std::__adjust_heap's hole walks from the root towards the leaves, at every node
+// into the child the comparator prefers (the right one unless comp(right, left)), while the node has a child; along
+// any root-to-leaf path of a heap the keys are monotone, so the comparisons std::__push_heap makes on its way back
+// up are false on a prefix of the path and true below it: every path node whose winning child the comparator does
+// not rank past the value shifts that child up, the first one that does receives the value.  Each 6-level window
+// costs one LDS round trip: lane i plays window node i+1, reads both children entries (adjacent slots: one
+// ds_read2_b64) and votes for the right child; a lane knows it lies on the hole's path when the ballot agrees with
+// the side of every one of its window ancestors (one masked compare against its PopLane constants: no serial walk),
+// and the on-path lanes shift their winner up in place.
 template <bool MAXH>
-__device__ __forceinline__ u64 heap_pop(u64* h, int n, int lane) {
+__device__ __forceinline__ u64 heap_pop(u64* h, int n, int lane, const PopLane& pl) {
   if (n <= 1) return 0;
   const int len = n - 1;
   const u64 value = h[len];
   const float vk = key(value);
-  const int lim = (len - 1) / 2;  // the hole has two children while hole < lim
-  const int j1 = lane + 1;        // window node (1-based) of this lane
-  const int lj = 31 - __clz(j1);
-  const int oj = j1 - (1 << lj);
   int P1 = 1;  // window root, 1-based heap index
   u64 root = value;
   for (int round = 0;; ++round) {
-    const int a1 = (P1 << lj) + oj;  // this lane's node, 1-based
-    const int c1 = 2 * a1 - 1;       // its left child, 0-based
+    const int a1 = (P1 << pl.lj) + pl.oj;  // this lane's node, 1-based
+    const int c1 = 2 * a1 - 1;             // its left child, 0-based
+    const bool has_child = pl.in_window && c1 < len;
     u64 le = 0, re = 0;
-    if (lane < 63 && c1 < len) {
+    if (has_child) {
       le = h[c1];
       re = h[c1 + 1];
     }
-    const bool right = lane < 63 && c1 + 1 < len && !hcmp<MAXH>(key(re), key(le));
+    const bool right = has_child && c1 + 1 < len && !hcmp<MAXH>(key(re), key(le));
     const u64 we = right ? re : le;  // the child the hole would move into
     const u64 W = __ballot(right);
-    int P = P1, r1 = 1, steps = 0;
-    while (steps < 6 && P - 1 < lim) {
-      const int b = static_cast<int>((W >> (r1 - 1)) & 1ull);
-      r1 = 2 * r1 + b;
-      P = 2 * P + b;
-      ++steps;
-    }
-    const bool lone = (len & 1) == 0 && P - 1 == (len - 2) / 2;  // a last node with only a left child
-    bool more = steps == 6 && (P - 1 < lim || lone);
-    if (!more && lone) {
-      r1 = 2 * r1;
-      P = 2 * P;
-      ++steps;
-    }
-    const bool onp = lane < 63 && lj < steps && (r1 >> (steps - lj)) == j1;
-    const bool up = onp && !hcmp<MAXH>(key(we), vk);  // no move back down: the winner stays shifted up
-    const int k = __popcll(__ballot(up));
+    // on the path: every window ancestor sent the hole this lane's way; a hole there moves on iff the node has a child
+    const bool hole = has_child && ((W ^ pl.dir) & pl.anc) == 0ull;
+    const bool up = hole && !hcmp<MAXH>(key(we), vk);  // no move back down: the winner stays shifted up
+    const u64 H = __ballot(hole), UP = __ballot(up);
     if (up) h[a1 - 1] = we;
-    if (round == 0) root = k == 0 ? value : bcast64(we);  // lane 0 is the root
-    if (k < steps) {
-      if (lane == 0) h[(P >> (steps - k)) - 1] = value;
+    if (round == 0) root = UP & 1ull ? bcast64(we) : value;  // lane 0 is the root
+    const u64 stop = H & ~UP;
+    if (stop) {  // the first path node whose winner stays below the value receives it
+      if (lane == static_cast<int>(__builtin_ctzll(stop))) h[a1 - 1] = value;
       break;
     }
-    if (!more) {
+    // every hole moved: the walk ends in the deepest hole's winner child, or goes on from it in the next window
+    const int cw1 = 2 * a1 + (right ? 1 : 0);
+    const int P = H ? __builtin_amdgcn_readlane(cw1, 63 - static_cast<int>(__clzll(H))) : P1;
+    if (!(H >> 31)) {  // no hole at window depth 5: the path ended inside this window
       if (lane == 0) h[P - 1] = value;
       break;
     }
@@ -274,26 +285,62 @@ struct Lay {
   static_assert(DB >= 16, "dimension must be >= 16");
 };
 
-template <int D>
+template <typename E>
+constexpr bool kByte = std::is_same_v<E, uint8_t> || std::is_same_v<E, int8_t>;
+
+template <int D, typename E = float, bool BYTES = kByte<E>>
 struct QueryRegs {
   f32x2 q2[D / 16 * 2];  // {q[2c + 8t], q[2c + 1 + 8t]}, t < PER
   float qt[(D & 15) > 0 ? (D & 15) : 1];
 };
+// Byte rows also keep the query as bytes when every component is a byte value of the rows' kind (SIFT's u8 queries
+// against u8 records): qb[u] packs the four components the lane's row word u pairs with (kernels.h
+// permuted_index_bytes), qq is the lane's share of sum(q^2), qint says the whole query qualified (wave-uniform).
+template <int D, typename E>
+struct QueryRegs<D, E, true> {
+  f32x2 q2[D / 16 * 2];
+  float qt[(D & 15) > 0 ? (D & 15) : 1];
+  u32 qb[D / 16 > 0 ? D / 16 : 1];
+  int qq;
+  bool qint;
+};
 
-template <int D>
-__device__ __forceinline__ void load_query(const float* __restrict__ q, int lane, QueryRegs<D>& Q) {
+template <int D, typename E>
+__device__ __forceinline__ void load_query(const float* __restrict__ q, int lane, QueryRegs<D, E>& Q) {
   constexpr int DB = D >> 4 << 4, PER = DB / 8, TAIL = D - DB;
   const int c2 = 2 * (lane & 3);
 #pragma unroll
   for (int t = 0; t < PER; ++t) Q.q2[t] = f32x2{q[c2 + 8 * t], q[c2 + 1 + 8 * t]};
 #pragma unroll
   for (int t = 0; t < TAIL; ++t) Q.qt[t] = q[DB + t];
+  if constexpr (kByte<E>) {
+    constexpr bool U8 = std::is_same_v<E, uint8_t>;
+    const float lo = U8 ? 0.f : -128.f, hi = U8 ? 255.f : 127.f;
+    auto byte_ok = [&](float f) { return f == __builtin_rintf(f) && f >= lo && f <= hi; };
+    bool ok = true;
+    int qq = 0;
+#pragma unroll
+    for (int u = 0; u < PER / 2; ++u) {
+      const float f[4] = {Q.q2[2 * u].x, Q.q2[2 * u].y, Q.q2[2 * u + 1].x, Q.q2[2 * u + 1].y};
+      u32 w = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ok &= byte_ok(f[i]);
+        const int v = static_cast<int>(f[i]);
+        w |= (static_cast<u32>(v) & 0xFFu) << (8 * i);
+        qq += v * v;
+      }
+      Q.qb[u] = w;
+    }
+#pragma unroll
+    for (int t = 0; t < TAIL; ++t) ok &= byte_ok(Q.qt[t]);
+    Q.qq = qq;
+    Q.qint = __ballot(!ok) == 0ull;
+  }
 }
 
 // One chunk = elements (t, t+1) of accumulators (2c, 2c+1): f32 → 4 floats, f16 → 4 halves in 2 words, bytes →
 // one word.
-template <typename E>
-constexpr bool kByte = std::is_same_v<E, uint8_t> || std::is_same_v<E, int8_t>;
 // elements of one device row (byte rows are padded to 16 bytes, kernels.h row_bytes)
 template <int D, typename E>
 constexpr int kRowElems = kByte<E> ? (D + 15) / 16 * 16 : D;
@@ -417,8 +464,8 @@ __device__ __forceinline__ float fold8(f32x2 acc) {
   return s;
 }
 
-template <int D, int METRIC>
-__device__ __forceinline__ float add_tail(const QueryRegs<D>& Q, const float* xt, float s) {
+template <int D, int METRIC, typename E>
+__device__ __forceinline__ float add_tail(const QueryRegs<D, E>& Q, const float* xt, float s) {
   constexpr int TAIL = D & 15;
   if constexpr (METRIC == 0) {
 #pragma unroll
@@ -445,10 +492,53 @@ __device__ __forceinline__ f32x2 acc_step(f32x2 q, f32x2 x, f32x2 acc) {
   }
 }
 
+// Byte query against byte rows: every term of the reference's f32 sums is an integer and every partial sum stays
+// below 2^24 (d <= 256: 256 x 255^2 < 2^24), so the f32 FMA chains are exact and equal the integer sums.  The
+// integer sums are taken with v_dot4 (four byte products per instruction): L2 as sum(q^2) + sum(x^2) - 2 sum(q x),
+// IP as sum(q x); the group's four lanes are added in lane 3 (DPP), the tail there too; converted once, exactly.
+template <typename E>
+__device__ __forceinline__ int dot4(u32 a, u32 b, int c) {
+  if constexpr (std::is_same_v<E, uint8_t>) return static_cast<int>(__builtin_amdgcn_udot4(a, b, static_cast<u32>(c), false));
+  else return __builtin_amdgcn_sdot4(static_cast<int>(a), static_cast<int>(b), c, false);
+}
+
+template <int D, int METRIC, typename E, int P>
+__device__ __forceinline__ void pass_dists_int(const QueryRegs<D, E>& Q, const NbrBuf<D, E, P>& B, float (&out)[P]) {
+  using L = Lay<D, E>;
+  int v[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    int qx = 0, xx = 0;
+#pragma unroll
+    for (int u = 0; u < L::NCH; ++u) {
+      qx = dot4<E>(Q.qb[u], B.x[p][u], qx);
+      if constexpr (METRIC == 0) xx = dot4<E>(B.x[p][u], B.x[p][u], xx);
+    }
+    v[p] = METRIC == 0 ? Q.qq + xx - 2 * qx : qx;
+  }
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    int s = v[p] + __builtin_amdgcn_update_dpp(0, v[p], 0x111, 0xF, 0xF, false);  // row_shr:1
+    s += __builtin_amdgcn_update_dpp(0, s, 0x112, 0xF, 0xF, false);                 // row_shr:2: lane 3 = 0+1+2+3
+#pragma unroll
+    for (int t = 0; t < L::TAIL; ++t) {
+      const int q = static_cast<int>(Q.qt[t]), x = static_cast<int>(byte_f32<E>(B.xt[p][t >> 2], t & 3));
+      s += METRIC == 0 ? (q - x) * (q - x) : q * x;
+    }
+    out[p] = METRIC == 0 ? static_cast<float>(s) : 1.0f - static_cast<float>(s);
+  }
+}
+
 // out[p] = distance of the pass-p vector of this lane's group; valid in lanes c = 3.
 template <int D, int METRIC, typename E, int P>
-__device__ __forceinline__ void pass_dists(const QueryRegs<D>& Q, const NbrBuf<D, E, P>& B, float (&out)[P]) {
+__device__ __forceinline__ void pass_dists(const QueryRegs<D, E>& Q, const NbrBuf<D, E, P>& B, float (&out)[P]) {
   using L = Lay<D, E>;
+  if constexpr (kByte<E>) {
+    if (Q.qint) {  // byte query, byte rows: exact integer dot products (wave-uniform branch)
+      pass_dists_int<D, METRIC, E, P>(Q, B, out);
+      return;
+    }
+  }
   f32x2 acc[P];
 #pragma unroll
   for (int p = 0; p < P; ++p) acc[p] = f32x2{0.f, 0.f};
@@ -478,16 +568,16 @@ __device__ __forceinline__ void pass_dists(const QueryRegs<D>& Q, const NbrBuf<D
       float xt[L::TAILA];
 #pragma unroll
       for (int t = 0; t < L::TAILA; ++t) xt[t] = L::TAIL > 0 ? byte_f32<E>(B.xt[p][t >> 2], t & 3) : 0.f;
-      out[p] = add_tail<D, METRIC>(Q, xt, fold8(acc[p]));
+      out[p] = add_tail<D, METRIC, E>(Q, xt, fold8(acc[p]));
     } else {
-      out[p] = add_tail<D, METRIC>(Q, B.xt[p], fold8(acc[p]));
+      out[p] = add_tail<D, METRIC, E>(Q, B.xt[p], fold8(acc[p]));
     }
   }
 }
 
 // slots p0 .. p0 + 16P - 1 of the list (those below n)
 template <int D, int METRIC, typename E, int P>
-__device__ __forceinline__ void dist_chunk(const E* __restrict__ vec, const QueryRegs<D>& Q, const u32* sc_ids,
+__device__ __forceinline__ void dist_chunk(const E* __restrict__ vec, const QueryRegs<D, E>& Q, const u32* sc_ids,
                                            float* sc_d, int p0, int n, int lane) {
   const int g4 = lane >> 2, c4 = lane & 3;
   NbrBuf<D, E, P> B;
@@ -509,7 +599,7 @@ __device__ __forceinline__ void dist_chunk(const E* __restrict__ vec, const Quer
 // more than 16 remain, then one: a list of <= 16 fresh nodes (an upper-level
 // list, most level-0 expansions of the heap kernel) costs one pass of VALU instead of two.
 template <int D, int METRIC, typename E>
-__device__ __forceinline__ void dist_list(const E* __restrict__ vec, const QueryRegs<D>& Q, const u32* sc_ids,
+__device__ __forceinline__ void dist_list(const E* __restrict__ vec, const QueryRegs<D, E>& Q, const u32* sc_ids,
                                           float* sc_d, int n, int lane) {
   int p0 = 0;
   for (; n - p0 > 16; p0 += 32) dist_chunk<D, METRIC, E, 2>(vec, Q, sc_ids, sc_d, p0, n, lane);
@@ -602,7 +692,7 @@ __device__ __forceinline__ u32 sortable(float f) {  // order-preserving u32 imag
 
 template <int D, int METRIC, typename E, bool ACCT>
 __device__ __forceinline__ void entry_and_descent(const SearchArgs& A, const E* __restrict__ vec,
-                                                  const QueryRegs<D>& Q, u32* sc_ids, float* sc_d, int lane,
+                                                  const QueryRegs<D, E>& Q, u32* sc_ids, float* sc_d, int lane,
                                                   u32& nn, float& closest, u32& st_dist, u32& st_vup, u32& st_vl0,
                                                   u32& st_lup, u32& status, ReadCount& rc) {
   const u32 ep = A.g.ep;
@@ -728,6 +818,13 @@ struct VisitedLds<0> {
     for (u32 i = lane; i < A.vis_cap / 4; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
   }
   __device__ __forceinline__ void insert_first(u32 x) { t[vhash(x, shift)] = x; }  // the table is empty
+  // every id of the table into the HBM bitmap (the table's entries are the ids themselves)
+  __device__ __forceinline__ void spill(u32* __restrict__ bits, const SearchArgs& A, int lane) const {
+    for (u32 i = lane; i <= mask; i += 64) {
+      const u32 x = t[i];
+      if (x != INV) atomicOr(&bits[x >> 5], 1u << (x & 31));
+    }
+  }
   __device__ __forceinline__ bool at_home(u32 x) const { return t[vhash(x, shift)] == x; }
   // the word at x's home slot (one read); home_match: x sits at home in that word
   __device__ __forceinline__ u32 probe(u32 x) const { return t[vhash(x, shift)]; }
@@ -775,13 +872,43 @@ struct VisitedLds<1> {
     for (u32 i = lane; i < A.vis_cap / 8; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
   }
   __device__ __forceinline__ u32 image(u32 x) const { return (x * mul) & bmask; }
+  // every id of the table into the HBM bitmap: entry (bucket b, remainder, distance d) names the id whose image is
+  // ((b - d) << rbits) | remainder, and the inverse multiply maps the image back
+  __device__ __forceinline__ void spill(u32* __restrict__ bits, const SearchArgs& A, int lane) const {
+    const u32 nw = A.vis_cap >> 1;  // two entries per word
+    for (u32 i = lane; i < nw; i += 64) {
+      const u32 w = t[i], b = i >> 2;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const u32 v = half ? (w >> 16) : (w & 0xFFFFu);
+        if (v == 0xFFFFu) continue;
+        const u32 home = (b - (v & ((1u << dbits) - 1u))) & bmask_b;
+        const u32 x = (((home << rbits) | (v >> dbits)) * A.vis_mul_inv) & bmask;
+        atomicOr(&bits[x >> 5], 1u << (x & 31));
+      }
+    }
+  }
   __device__ __forceinline__ void insert_first(u32 x) {  // the table is empty: entry 0 of the home bucket
     const u32 h = image(x);
     t[(h >> rbits) * 4] = 0xFFFF0000u | ((h & rmask) << dbits);
   }
   __device__ __forceinline__ uint4 bucket(u32 b) const { return reinterpret_cast<const uint4*>(t)[b]; }
-  static __device__ __forceinline__ bool has(u32 w, u32 e) { return (w & 0xFFFFu) == e || (w >> 16) == e; }
-  static __device__ __forceinline__ bool has(const uint4& w, u32 e) { return (has(w.x, e) || has(w.y, e)) || (has(w.z, e) || has(w.w, e)); }
+  // Branch-free bucket tests on both 16-bit halves of a word at once (SWAR): zero16(x) is non-zero iff a half of x
+  // is zero (a borrow can flag the high half spuriously only when the low half is zero, so "any half" is exact).
+  // Written with `|`, not `||`: short-circuit tests compiled to a cascade of exec-mask branches per entry.
+  static __device__ __forceinline__ u32 zero16(u32 x) { return (x - 0x00010001u) & ~x & 0x80008000u; }
+  static __device__ __forceinline__ bool has(u32 w, u32 e) { return zero16(w ^ (e * 0x00010001u)) != 0u; }
+  static __device__ __forceinline__ bool has(const uint4& w, u32 e) {
+    const u32 ee = e * 0x00010001u;
+    return (zero16(w.x ^ ee) | zero16(w.y ^ ee) | zero16(w.z ^ ee) | zero16(w.w ^ ee)) != 0u;
+  }
+  // the bucket's first empty entry (0xFFFF) in bucket order: word j (-1: none) and half k (0 low, 1 high)
+  static __device__ __forceinline__ void first_empty(const uint4& w, int& j, u32& k, u32& word) {
+    const bool e0 = zero16(~w.x) != 0u, e1 = zero16(~w.y) != 0u, e2 = zero16(~w.z) != 0u, e3 = zero16(~w.w) != 0u;
+    j = e0 ? 0 : e1 ? 1 : e2 ? 2 : e3 ? 3 : -1;
+    word = e0 ? w.x : e1 ? w.y : e2 ? w.z : w.w;
+    k = (word & 0xFFFFu) == 0xFFFFu ? 0u : 1u;
+  }
   // the home bucket (one ds_read_b128); home_match: x sits in it
   __device__ __forceinline__ Hint probe(u32 x) const { return bucket(image(x) >> rbits); }
   __device__ __forceinline__ bool home_match(u32 x, const Hint& w) const {
@@ -796,19 +923,10 @@ struct VisitedLds<1> {
     const u32 h = image(x);
     const u32 e = (h & rmask) << dbits;
     if (has(cur, e)) return 0;
-    const u32 w[4] = {cur.x, cur.y, cur.z, cur.w};
-    int j = -1;
-    u32 k = 0;
-#pragma unroll
-    for (int i = 3; i >= 0; --i) {
-      const bool lo = (w[i] & 0xFFFFu) == 0xFFFFu, hi = (w[i] >> 16) == 0xFFFFu;
-      if (lo | hi) {
-        j = i;
-        k = lo ? 0u : 1u;
-      }
-    }
+    int j;
+    u32 k;
+    first_empty(cur, j, k, pexp);
     if (j < 0) return 2;
-    pexp = j == 0 ? cur.x : j == 1 ? cur.y : j == 2 ? cur.z : cur.w;
     pw = (h >> rbits) * 4 + static_cast<u32>(j);
     pold = atomicCAS(&t[pw], pexp, k ? ((pexp & 0xFFFFu) | (e << 16)) : ((pexp & 0xFFFF0000u) | e));
     return 1;
@@ -830,19 +948,10 @@ struct VisitedLds<1> {
       const u32 e = rem | disp;
       if (has(cur, e)) break;  // same bucket distance, same remainder: this id
       // first empty entry in bucket order: word j, high half k
-      const u32 w[4] = {cur.x, cur.y, cur.z, cur.w};
-      int j = -1;
-      u32 k = 0;
-#pragma unroll
-      for (int i = 3; i >= 0; --i) {
-        const bool lo = (w[i] & 0xFFFFu) == 0xFFFFu, hi = (w[i] >> 16) == 0xFFFFu;
-        if (lo | hi) {
-          j = i;
-          k = lo ? 0u : 1u;
-        }
-      }
+      int j;
+      u32 k, old_w;
+      first_empty(cur, j, k, old_w);
       if (j >= 0) {
-        const u32 old_w = j == 0 ? cur.x : j == 1 ? cur.y : j == 2 ? cur.z : cur.w;
         const u32 want = k ? ((old_w & 0xFFFFu) | (e << 16)) : ((old_w & 0xFFFF0000u) | e);
         if (atomicCAS(&t[b * 4 + static_cast<u32>(j)], old_w, want) == old_w) {
           fresh = true;
@@ -905,6 +1014,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
   };
 
   const int lane = threadIdx.x;
+  const PopLane pl(lane);
   const E* __restrict__ vec = static_cast<const E*>(A.g.vec);
   const u32 M0 = A.g.M0;
   u32* __restrict__ vis = A.visited + (VIS >= 1 ? static_cast<u64>(blockIdx.x) * A.words_per_slot : 0ull);
@@ -920,8 +1030,8 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
     const u32 qi = A.in_list ? A.in_list[item] : item;
 
     PHASE(0)
-    QueryRegs<D> Q;
-    load_query<D>(A.queries + static_cast<u64>(qi) * D, lane, Q);
+    QueryRegs<D, E> Q;
+    load_query<D, E>(A.queries + static_cast<u64>(qi) * D, lane, Q);
     if (VIS == 0) vt.clear(A, lane);  // visited_nodes.clear()  (:475) — done up front for this query
 
     u32 st_dist = 0, st_vup = 0, st_vl0 = 0, st_lup = 0, st_ll0 = 0, st_maxnext = 0, status = 0;
@@ -965,7 +1075,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         PHASE(2)
         const float ck = key(nroot), farthest0 = key(troot);  // next_candidates.top(); pop()  (:418-421)
         const u32 cid = eid(nroot);
-        nroot = nan_keys ? heap_pop_any<false>(nxt, nnext, lane) : heap_pop<false>(nxt, nnext, lane);
+        nroot = nan_keys ? heap_pop_any<false>(nxt, nnext, lane) : heap_pop<false>(nxt, nnext, lane, pl);
         hfence();
         --nnext;
         if (ck > farthest0) break;  // :421-426
@@ -1066,7 +1176,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
               ++ntop;
             } else {  // d < top().distance holds: it is the accept test with the top full
               PHASE(9)
-              troot = nan_keys ? heap_pop_any<true>(top, ntop, lane) : heap_pop<true>(top, ntop, lane);
+              troot = nan_keys ? heap_pop_any<true>(top, ntop, lane) : heap_pop<true>(top, ntop, lane, pl);
               hfence();
               PHASE(10)
               heap_push2(nxt, nnext, top, ntop - 1, en, nroot, troot, lane);
@@ -1086,7 +1196,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         PHASE(11)
         while (ntop > static_cast<int>(A.k)) {
           if (nan_keys) heap_pop_any<true>(top, ntop, lane);
-          else heap_pop<true>(top, ntop, lane);
+          else heap_pop<true>(top, ntop, lane, pl);
           hfence();
           --ntop;
         }
@@ -1232,8 +1342,8 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
     const u32 qi = A.in_list ? A.in_list[item] : item;
 
     PHASE(0)
-    QueryRegs<D> Q;
-    load_query<D>(A.queries + static_cast<u64>(qi) * D, lane, Q);
+    QueryRegs<D, E> Q;
+    load_query<D, E>(A.queries + static_cast<u64>(qi) * D, lane, Q);
     vis.clear(A, lane);
     u32 st_dist = 0, st_vup = 0, st_vl0 = 0, st_lup = 0, st_ll0 = 0, ties = 0, status = 0;
     ReadCount rc;
@@ -1276,6 +1386,32 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
     bool ehint_known = false;  // ehint is e's home bucket as it stands (not a guess)
     typename VisitedLds<VT>::Hint ehint = VisitedLds<VT>::unknown();  // e's home word / bucket as probed one
                                                                       // expansion earlier (VisitedLds::test_and_set)
+    // In-place spill (SearchArgs::spill_flags): once the table overflows, the query's visited set moves to an HBM
+    // bitmap and the search goes on there (a global atomicOr per fresh id) instead of being re-run from scratch.
+    int sslot = -1;  // the bitmap this query holds (wave-uniform), -1 = the LDS table
+    u32* __restrict__ sbits = nullptr;
+    // claim a bitmap and copy the table into it; then the ids of the lanes with `record` set go in too
+    auto spill = [&](bool record) -> bool {
+      if (A.spill_slots == 0) return false;
+      u32 got = INV;
+      if (lane == 0) {
+        const u32 n = A.spill_slots;
+        for (u32 i = 0, j = blockIdx.x % n; i < n; ++i, j = j + 1 == n ? 0u : j + 1)
+          if (atomicCAS(&A.spill_flags[j], 0u, 1u) == 0u) {
+            got = j;
+            break;
+          }
+      }
+      got = bcast(got);
+      if (got == INV) return false;
+      sslot = static_cast<int>(got);
+      sbits = A.visited + static_cast<u64>(got) * A.words_per_slot;
+      wave_sync();
+      vis.spill(sbits, A, lane);
+      if (record) atomicOr(&sbits[e >> 5], 1u << (e & 31));
+      EVENT(3)
+      return true;
+    };
 
     while (status == 0) {
       ++st_ll0;  // read_neighborlist (:436-438)
@@ -1295,17 +1431,34 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       // ef = 128, profiles/r02/lib_probe_deferred_insert.jsonl)
       bool fresh = false, vovf = false;
       u32 pw = INV, pexp = 0, pold = 0;
-      if constexpr (VT == 1) {
+      if (sslot >= 0) {  // spilled: the HBM bitmap
+        if (cand) {
+          const u32 bit = 1u << (e & 31);
+          fresh = (atomicOr(&sbits[e >> 5], bit) & bit) == 0u;
+        }
+      } else if constexpr (VT == 1) {
         if (cand) {
           const int r = ehint_known ? vis.begin(e, ehint, pw, pexp, pold) : 2;
           fresh = r == 2 ? vis.test_and_set(e, vovf, ehint) : r == 1;
         }
-        if (__ballot(vovf)) {
+      } else {
+        if (cand) fresh = vis.test_and_set(e, vovf, ehint);
+      }
+      // the table is too full (or an id landed too far from home): spill it and go on in HBM.  Lanes whose insert
+      // overflowed are tested against the bitmap; a deferred compare-and-swap that lost its word records its (fresh)
+      // id there instead of retrying in the table.
+      if (sslot < 0 && (__ballot(vovf) || nvis + __popcll(__ballot(fresh)) > A.vis_limit)) {
+        const bool lost = pw != INV && pold != pexp;
+        if (!spill(lost)) {
           status = ST_OVERFLOW;
           break;
         }
-      } else {
-        if (cand) fresh = vis.test_and_set(e, vovf, ehint);
+        pw = INV;
+        if (vovf) {
+          const u32 bit = 1u << (e & 31);
+          fresh = (atomicOr(&sbits[e >> 5], bit) & bit) == 0u;
+          vovf = false;
+        }
       }
       const u64 fm = __ballot(fresh);
       const int nf = __popcll(fm);
@@ -1313,10 +1466,6 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       nvis += nf;
       st_vl0 += nf;
       st_dist += nf;
-      if (nvis > A.vis_limit) {
-        status = ST_OVERFLOW;
-        break;
-      }
 
       PHASE(5)
       float my_d = INF;  // distance of this lane's list slot
@@ -1339,7 +1488,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
 
       if constexpr (VT == 1) {  // the deferred compare-and-swaps, before the table is probed again
         if (pw != INV) vis.finish(e, pexp, pold, vovf);
-        if (__ballot(vovf)) {
+        if (__ballot(vovf) && !spill(vovf)) {  // a retried insert overflowed: its id is fresh, record it in HBM
           status = ST_OVERFLOW;
           break;
         }
@@ -1368,8 +1517,9 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       const u32 prow = pid == r_id ? nrow : load_row(pid != INV ? pid : pad);  // a fresh f*: its list now
       // an entry already at its home slot of the visited table is not fresh: its row is not requested (one
       // read-only LDS probe; the visit proper still runs at the top of the next expansion)
-      const typename VisitedLds<VT>::Hint pword = in_row && prow != INV ? vis.probe(prow) : VisitedLds<VT>::unknown();
-      const bool seen = in_row && prow != INV && vis.home_match(prow, pword);
+      const bool probe = sslot < 0 && in_row && prow != INV;
+      const typename VisitedLds<VT>::Hint pword = probe ? vis.probe(prow) : VisitedLds<VT>::unknown();
+      const bool seen = probe && vis.home_match(prow, pword);
       issue_list<D, E, P>(X, vec, seen ? INV : prow, pad, c4);
 
       // ---- merge (:456-465 over the whole list at once) ----------------------------------------------------------
@@ -1477,7 +1627,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       nrow = load_row(nid);  // unconditional: always the youngest load
       e = erow;
       ehint = c != pid ? VisitedLds<VT>::unknown() : pword;  // the probe read prow's home bucket, no insert since
-      ehint_known = c == pid;
+      ehint_known = c == pid && sslot < 0;
       cur = c;
       r_id = c2;
       r_key = k2;
@@ -1519,6 +1669,12 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       qs[7] = status == 0 ? static_cast<u32>(cs < static_cast<int>(A.k) ? cs : A.k) : 0u;
       write_read_counts(qs, rc);
     }
+    if (sslot >= 0) {  // hand the bitmap back all zero: the stores land before the flag drops
+      for (u64 w = lane; w < A.words_per_slot; w += 64) sbits[w] = 0u;
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      __threadfence();
+      if (lane == 0) atomicExch(&A.spill_flags[sslot], 0u);
+    }
   }
   clk.flush(A.prof, lane);
   finish_call(A, lane);
@@ -1536,8 +1692,8 @@ __global__ __launch_bounds__(64) void distance_kernel(DistArgs A) {
   const u64 w = blockIdx.x;
   const u32 qi = static_cast<u32>(w / chunks), ch = static_cast<u32>(w % chunks);
   if (qi >= A.nq) return;
-  QueryRegs<D> Q;
-  load_query<D>(A.queries + static_cast<u64>(qi) * D, lane, Q);
+  QueryRegs<D, E> Q;
+  load_query<D, E>(A.queries + static_cast<u64>(qi) * D, lane, Q);
   const u32 j = ch * 64 + lane;
   u32 dense = INV;
   if (j < A.n_per) {
@@ -1566,6 +1722,7 @@ __global__ __launch_bounds__(64) void heap_replay_kernel(const int32_t* ops, con
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   u64* h = reinterpret_cast<u64*>(smem);
   const int lane = threadIdx.x;
+  const PopLane pl(lane);
   const bool any = (k & 0x80000000u) != 0;  // exercise the general pop instead of the fast one
   k &= 0x7FFFFFFFu;
   int n = 0;
@@ -1579,7 +1736,7 @@ __global__ __launch_bounds__(64) void heap_replay_kernel(const int32_t* ops, con
       ++n;
     } else if (op == 1) {
       if (n > 0) {
-        root = any ? heap_pop_any<MAXH>(h, n, lane) : heap_pop<MAXH>(h, n, lane);
+        root = any ? heap_pop_any<MAXH>(h, n, lane) : heap_pop<MAXH>(h, n, lane, pl);
         --n;
       }
     } else {
@@ -1587,7 +1744,7 @@ __global__ __launch_bounds__(64) void heap_replay_kernel(const int32_t* ops, con
         root = heap_push<MAXH>(h, n, e, root, lane);
         ++n;
       } else if (hcmp<MAXH>(vals[i], key(root))) {
-        root = any ? heap_pop_any<MAXH>(h, n, lane) : heap_pop<MAXH>(h, n, lane);
+        root = any ? heap_pop_any<MAXH>(h, n, lane) : heap_pop<MAXH>(h, n, lane, pl);
         root = heap_push<MAXH>(h, n - 1, e, root, lane);
       }
     }

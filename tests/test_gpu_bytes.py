@@ -115,3 +115,45 @@ def test_byte_rows_distance_kernel(gpu_available):
             for j in range(77):
                 ref = O.distance(metric, q[i], base[uids[i, j]])
                 assert np.float32(ref).view(np.uint32) == got[i, j].view(np.uint32), (dim, metric, i, j)
+
+
+def test_byte_rows_mixed_query_kinds_exact_mode_is_the_oracle(gpu_available):
+    """Byte queries take the integer dot-product path (v_dot4), other queries the f32 path, decided per query:
+    a batch mixing both (half-integers, out-of-range values, negative values against u8 rows) is the oracle
+    bitwise either way."""
+    for gen, dim, metric, elem in [(D.sift_like, 128, 0, L.ELEM_U8), (D.sift_like, 128, 1, L.ELEM_U8),
+                                   (i8_like, 100, 0, L.ELEM_I8), (i8_like, 100, 1, L.ELEM_I8)]:
+        base = gen(3000, seed=81, d=dim)
+        q = gen(120, seed=82, d=dim).copy()
+        q[1::4] += np.float32(0.5)      # not integers
+        q[2::4, 0] = np.float32(300.0)  # out of the byte range
+        q[3::8, 5] = np.float32(-1.0)   # negative: a byte value for i8 rows only
+        dumps, _, _ = O.build(base, 12, 64, metric, 1, seed=9)
+        ref_ids, ref_d, ref_qs = O.OracleIndex(dumps, dim, 12, metric).knn(q, 10, 64, threads=8)
+        with shine_amd.Index.from_buffers(dumps, dim, 12, metric, elem=elem, gpus=[0]) as idx:
+            r = idx.knn(q, 10, 64)
+        np.testing.assert_array_equal(r.ids, ref_ids)
+        np.testing.assert_array_equal(r.dists.view(np.uint32), ref_d.view(np.uint32))
+        np.testing.assert_array_equal(r.qstats[:, :8], ref_qs[:, :8])
+
+
+def test_byte_rows_distance_kernel_byte_queries(gpu_available):
+    import torch
+    for dim, metric, gen, elem in [(128, 0, D.sift_like, L.ELEM_U8), (128, 1, D.sift_like, L.ELEM_U8),
+                                   (100, 1, i8_like, L.ELEM_I8), (100, 0, i8_like, L.ELEM_I8)]:
+        base = gen(500, seed=43, d=dim)
+        q = gen(21, seed=44, d=dim)  # byte queries: the integer path
+        dumps, _, _ = O.build(base, 8, 32, metric, 1, seed=2)
+        uids = np.random.default_rng(dim + metric).integers(0, 500, (21, 70)).astype(np.uint32)
+        with shine_amd.Index.from_buffers(dumps, dim, 8, metric, elem=elem, gpus=[0]) as idx:
+            qt = torch.from_numpy(q).cuda()
+            ut = torch.from_numpy(uids.view(np.int32)).cuda()
+            out = torch.empty((21, 70), dtype=torch.float32, device="cuda")
+            idx.distance_device(qt.data_ptr(), 21, ut.data_ptr(), 70, out.data_ptr(),
+                                stream=torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            got = out.cpu().numpy()
+        for i in range(21):
+            for j in range(70):
+                ref = O.distance(metric, q[i], base[uids[i, j]])
+                assert np.float32(ref).view(np.uint32) == got[i, j].view(np.uint32), (dim, metric, i, j)

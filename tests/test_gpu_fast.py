@@ -103,6 +103,7 @@ def test_fast_mode_overflow_fixups_are_exact(gpu_available, monkeypatch):
     q = D.deep_like(64, seed=8, d=96)
     dumps, _, _ = O.build(base, 16, 100, 0, 1, seed=3)
     ref = O.OracleIndex(dumps, 96, 16, 0).knn(q, 10, 128)
+    monkeypatch.setenv("SHINE_DEBUG_NO_SPILL", "1")  # the hand-on path, not the in-place spill
     monkeypatch.setenv("SHINE_DEBUG_VISCAP", "1024")
     r = _fast_knn(dumps, 96, 16, 0, q, 10, 128)
     assert r.stats["overflow_retries"] > 0
@@ -117,6 +118,7 @@ def test_fast_mode_light_pass_at_ef512_is_exact(gpu_available, monkeypatch):
     q = D.deep_like(96, seed=92, d=96)
     dumps, _, _ = O.build(base, 16, 100, 1, 1, seed=4)
     ref = O.OracleIndex(dumps, 96, 16, 1).knn(q, 10, 512)
+    monkeypatch.setenv("SHINE_DEBUG_NO_SPILL", "1")  # the hand-on path, not the in-place spill
     monkeypatch.setenv("SHINE_DEBUG_VISCAP", "1024")
     r = _fast_knn(dumps, 96, 16, 1, q, 10, 512)
     assert r.stats["overflow_retries"] >= 48
@@ -131,6 +133,7 @@ def test_fast_mode_light_pass_overflow_goes_to_global_heaps(gpu_available, monke
     q = D.deep_like(48, seed=94, d=96)
     dumps, _, _ = O.build(base, 16, 100, 0, 1, seed=4)
     ref = O.OracleIndex(dumps, 96, 16, 0).knn(q, 10, 128)
+    monkeypatch.setenv("SHINE_DEBUG_NO_SPILL", "1")  # the hand-on path, not the in-place spill
     monkeypatch.setenv("SHINE_DEBUG_VISCAP", "1024")
     monkeypatch.setenv("SHINE_DEBUG_LIGHT_CAP", "8")
     r = _fast_knn(dumps, 96, 16, 0, q, 10, 128)
@@ -230,3 +233,31 @@ def test_learned_table_sizes_keep_results(mode, gpu_available):
         np.testing.assert_array_equal(runs[-1].ids, ref[0])
     else:
         _check_tie_free_exact(runs[-1], ref, 0.95)
+
+
+@pytest.mark.parametrize("vis16", ["0", "1"])
+@pytest.mark.parametrize("gen,dim,metric,ef", [(D.deep_like, 96, 0, 128), (D.sift_like, 128, 0, 128),
+                                                (D.deep_like, 96, 1, 256)])
+def test_fast_mode_spills_in_place_and_stays_exact(gpu_available, monkeypatch, vis16, gen, dim, metric, ef):
+    """A 256-entry visited table overflows in every query: each spills its table into an HBM bitmap mid-search and
+    goes on there (SearchArgs::spill_flags), so nothing is handed to the fallback passes while a bitmap is free, and
+    every tie-free query is still the oracle's search bit for bit.  Hundreds of queries spill at once, more than
+    the 64 bitmaps: the rest are handed on and re-run exactly, so the batch mixes both paths."""
+    base = gen(6000, seed=301, d=dim)
+    q = gen(600, seed=302, d=dim)
+    dumps, _, _ = O.build(base, 16, 100, metric, 1, seed=6)
+    ref = O.OracleIndex(dumps, dim, 16, metric).knn(q, 10, ef, threads=8)
+    monkeypatch.setenv("SHINE_DEBUG_VISCAP", "256")
+    monkeypatch.setenv("SHINE_DEBUG_VIS16", vis16)
+    r = _fast_knn(dumps, dim, 16, metric, q, 10, ef)
+    assert r.stats["overflow_retries"] < q.shape[0]  # some queries went on in place instead of being re-run
+    _check_tie_free_exact(r, ref, 0.25 if gen is D.sift_like else 0.95)
+    # one query at a time: every spill finds a free bitmap, none is handed on
+    with shine_amd.Index.from_buffers(dumps, dim, 16, metric, gpus=[0]) as idx:
+        idx.set_search_mode(L.MODE_FAST)
+        for i in range(0, 64, 8):
+            one = idx.knn(q[i:i + 8], 10, ef)
+            assert one.stats["overflow_retries"] == 0
+            clean = one.qstats[:, L.QS_TIES] == 0  # a handed-on query of the batch ran the exact heap kernel
+            np.testing.assert_array_equal(one.ids[clean], r.ids[i:i + 8][clean])
+            np.testing.assert_array_equal(one.dists[clean].view(np.uint32), r.dists[i:i + 8][clean].view(np.uint32))
