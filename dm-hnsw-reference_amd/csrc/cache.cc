@@ -1,0 +1,162 @@
+// Dynamic record cache engine: cache::Cache + CoolingTable (src/cache/cache.hh:24-311, cooling_table.hh:52-98) at
+// call granularity.  See cache.h.
+#include "cache.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace shine {
+
+namespace {
+
+constexpr uint32_t kInv = 0xFFFFFFFFu;
+constexpr uint32_t kCoolingBucketEntries = 6;  // constants.hh:14
+constexpr double kCoolingRatio = 0.1;          // constants.hh:15
+
+uint64_t murmur64(uint64_t h) {  // std::hash<RemotePtr> (remote_pointer.hh:31-51) over the key
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  h *= 0xc4ceb9fe1a85ec53ull;
+  h ^= h >> 33;
+  return h;
+}
+
+uint64_t splitmix(uint64_t z) {  // the cooling table's hash (cooling_table.hh:100-108)
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+}  // namespace
+
+uint64_t cache_entries(uint64_t n, uint32_t M, uint32_t dim, double ratio_percent) {
+  if (n == 0 || M < 2) return 0;
+  const uint32_t levels = static_cast<uint32_t>(std::round(std::log(static_cast<double>(n)) / std::log(M)));
+  uint64_t index_size = 0;  // hnsw.hh:309-321
+  for (uint32_t i = 0; i < levels; ++i) {
+    const uint64_t size = i == 0 ? (16ull + 4ull * dim) + (4ull + 8ull * 2 * M) : 4ull + 8ull * M;
+    index_size += static_cast<uint64_t>(std::llround(std::pow(1.0 / M, i) * static_cast<double>(n))) * size;
+  }
+  // static_cast<f32>(estimated_index_size) / 100. * ratio, in double after the f32 rounding (compute_node.cc:43)
+  const uint64_t cache_size =
+      static_cast<uint64_t>(static_cast<double>(static_cast<float>(index_size)) / 100. * ratio_percent);
+  return cache_size / (16ull + 4ull * dim);  // compute_node.cc:40-54
+}
+
+RecordCache::RecordCache(uint32_t entries, uint64_t seed)
+    : C_(entries),
+      B_(std::max<uint32_t>(1, entries)),
+      CT_(std::max<uint32_t>(1, static_cast<uint32_t>(std::ceil(entries / static_cast<double>(kCoolingBucketEntries) *
+                                                                kCoolingRatio)))),
+      state_(seed),
+      buckets_(B_),
+      ct_(CT_),
+      key_of_(entries, kInv),
+      dev_of_(entries, kInv),
+      cooling_(entries, 0) {}
+
+bool RecordCache::size_ok(uint32_t entries) {
+  const uint32_t ct = std::max<uint32_t>(
+      1, static_cast<uint32_t>(std::ceil(entries / static_cast<double>(kCoolingBucketEntries) * kCoolingRatio)));
+  return entries > kCoolingBucketEntries * ct;
+}
+
+uint64_t RecordCache::rand() {
+  state_ += 0x9E3779B97F4A7C15ull;
+  uint64_t z = state_;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+bool RecordCache::ct_remove(uint32_t key) {  // cooling_table.hh:52-75
+  auto& b = ct_[splitmix(key) % CT_];
+  auto it = std::find(b.begin(), b.end(), key);
+  if (it == b.end()) return false;
+  b.erase(it);
+  return true;
+}
+
+bool RecordCache::ct_insert(uint32_t key, uint32_t& victim) {  // cooling_table.hh:81-98
+  auto& b = ct_[splitmix(key) % CT_];
+  bool pushed = false;
+  if (b.size() == kCoolingBucketEntries) {
+    victim = b.back();
+    b.pop_back();
+    pushed = true;
+  }
+  b.insert(b.begin(), key);
+  return pushed;
+}
+
+uint32_t RecordCache::evict() {  // cache.hh:232-311
+  for (;;) {
+    auto& b = buckets_[rand() % B_];
+    if (b.empty()) continue;
+    const uint32_t key = b[rand() % b.size()];
+    const uint32_t slot = slot_of_.at(key);
+    uint32_t victim = kInv;
+    bool has_victim = false;
+    if (!cooling_[slot]) {  // hot -> cooling; the table may push its oldest key out
+      has_victim = ct_insert(key, victim);
+      cooling_[slot] = 1;
+      if (cool_on_) cool_on_->push_back(slot);
+    }
+    if (!has_victim) continue;
+    auto it = slot_of_.find(victim);
+    if (it == slot_of_.end() || !cooling_[it->second]) continue;  // rescued meanwhile: no eviction
+    const uint32_t vslot = it->second;
+    auto& vb = buckets_[murmur64(victim) % B_];
+    vb.erase(std::find(vb.begin(), vb.end(), victim));
+    slot_of_.erase(it);
+    cooling_[vslot] = 0;
+    ++evicted;
+    return vslot;
+  }
+}
+
+void RecordCache::insert(uint32_t key, uint32_t dev, std::vector<CacheUpdate>& updates) {  // cache.hh:147-203
+  const uint32_t slot = next_idx_ < C_ ? next_idx_++ : evict();
+  updates.push_back({slot, dev, dev_of_[slot]});
+  buckets_[murmur64(key) % B_].push_back(key);
+  slot_of_[key] = slot;
+  key_of_[slot] = key;
+  dev_of_[slot] = dev;
+  cooling_[slot] = 0;
+  ++admitted;
+}
+
+void RecordCache::apply_call(std::vector<uint32_t> rescued_keys, std::vector<CacheCandidate> candidates,
+                             std::vector<CacheUpdate>& updates, std::vector<uint32_t>& cool_on) {
+  if (C_ == 0) return;
+  cool_on_ = &cool_on;
+  std::sort(rescued_keys.begin(), rescued_keys.end());
+  rescued_keys.erase(std::unique(rescued_keys.begin(), rescued_keys.end()), rescued_keys.end());
+  for (uint32_t key : rescued_keys) {  // cache.hh:128-132
+    auto it = slot_of_.find(key);
+    if (it != slot_of_.end() && cooling_[it->second] && ct_remove(key)) {
+      cooling_[it->second] = 0;
+      ++rescued;
+    }
+  }
+  std::stable_sort(candidates.begin(), candidates.end(), [](const CacheCandidate& a, const CacheCandidate& b) {
+    return a.query != b.query ? a.query < b.query : a.key < b.key;
+  });
+  for (const CacheCandidate& c : candidates) {
+    if (contains(c.key)) continue;  // admitted by an earlier miss of this call (cache.hh:171-179)
+    if (c.always || !full() || c.coin) insert(c.key, c.dev_id, updates);
+  }
+  cool_on_ = nullptr;
+}
+
+std::vector<uint32_t> RecordCache::keys() const {
+  std::vector<uint32_t> out;
+  out.reserve(slot_of_.size());
+  for (const auto& kv : slot_of_) out.push_back(kv.first);
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+}  // namespace shine

@@ -14,11 +14,13 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
 #include "../../include/shine_gpu.h"
 #include "graph.h"
+#include "cache.h"
 #include "kernels.h"
 #include "placement.h"
 
@@ -168,6 +170,19 @@ struct Replica {
   HostBuf<float> hq, hd;
   HostBuf<uint32_t> hids, hqs;
   DevBuf<unsigned long long> prof;  // SHINE_PHASE_PROFILE diagnostics
+  // dynamic record cache (SHINE_CACHE_DYNAMIC): this GPU's arena, lookup table, logs and the host policy engine
+  DevBuf<uint32_t> cslot, cool, rlog, logn, upd;
+  DevBuf<uint8_t> cvec;
+  DevBuf<unsigned long long> clog;
+  uint32_t clog_cap = 0, rlog_cap = 0, dyn_call = 0;
+  RecordCache cache;
+  void release_dynamic() {
+    for (auto* b : {&cslot, &cool, &rlog, &logn, &upd}) b->release();
+    cvec.release();
+    clog.release();
+    clog_cap = rlog_cap = dyn_call = 0;
+    cache = RecordCache();
+  }
 };
 
 }  // namespace
@@ -199,6 +214,11 @@ struct IndexState {
   HostGraph host;
   std::vector<uint32_t> dev_of;  // dev_of[g] = device id of graph node g
   std::vector<int> devs;
+  // sharded placements: uid of every device id and device id of every uid (host copies, for the dynamic cache)
+  std::vector<uint32_t> uid_of_dev, dev_of_uid;
+  int cache_policy = SHINE_CACHE_STATIC;
+  uint64_t cache_seed = 0;
+  uint64_t cache_entries_per_gpu = 0;
 };
 
 struct shine_index : IndexState {
@@ -231,6 +251,19 @@ DevGraph dev_graph(const shine_index* h, const Replica& r) {
   g.cached_list_rows = static_cast<uint32_t>(h->cached_list_rows);
   g.div_magic = h->div_magic;
   g.div_shift = h->div_shift;
+  if (h->cache_policy == SHINE_CACHE_DYNAMIC && g.sharded && r.cslot.p) {
+    g.cslot = r.cslot.p;
+    g.cvec = r.cvec.p;
+    g.cool = r.cool.p;
+    g.clog = r.clog.p;
+    g.clog_n = r.logn.p;
+    g.rlog = r.rlog.p;
+    g.clog_cap = r.clog_cap;
+    g.rlog_cap = r.rlog_cap;
+    g.dyn_full = r.cache.full() ? 1u : 0u;
+    g.dyn_call = r.dyn_call;
+    g.dyn_seed = h->cache_seed + r.slot;
+  }
   return g;
 }
 
@@ -270,6 +303,7 @@ void release_state(IndexState* h) {
     for (auto& e : R.by_stream) e.second->release();
     R.by_stream.clear();
     R.main.release();
+    R.release_dynamic();
     R.prof.release();
     R.vec.release();
     R.hq.release();
@@ -643,6 +677,8 @@ int make_index(HostGraph G, int elem, const int* gpu_ids, uint32_t n_gpus, int p
   }
   if (sharded) {
     h->devs = devs;
+    h->uid_of_dev = std::move(uid_s);
+    h->dev_of_uid = std::move(inv);
     if (h->cached_rows || h->cached_list_rows) {  // a warmup may re-rank the stripes: keep what it relays out
       h->dev_of = std::move(newid);
       h->host = std::move(G);
@@ -965,6 +1001,13 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     }
     hipError_t e = launch_search(h->dim, h->metric, h->elem, sh.grid, a, s);
     if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("search launch: ") + hipGetErrorString(e));
+    if (env_int("SHINE_DEBUG_SYNC", 0)) {  // diagnostics: wait for every pass and name the one that failed
+      e = hipStreamSynchronize(s);
+      if (e != hipSuccess)
+        return set_error(SHINE_ERR_HIP, "pass " + std::to_string(i) + " (kind " + std::to_string(pass) + ", grid " +
+                                            std::to_string(sh.grid) + ", table " + std::to_string(sh.vis_cap) +
+                                            ", vis16 " + std::to_string(sh.vis16) + "): " + hipGetErrorString(e));
+    }
   }
   if (timed) HIP_TRY(hipEventRecord(R.ev1, s));
   S.counters_zero = true;
@@ -1168,6 +1211,89 @@ int shine_knn_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_qu
 
 namespace {
 
+// The dynamic cache between calls (SHINE_CACHE_DYNAMIC): read slot R's logs of the last call(s), replay the
+// reference's policy on the host engine (cache.cc), and enqueue the arena updates on R's stream, ahead of its next call.
+int apply_dynamic(shine_index* h, Replica& R, shine_stats* agg) {
+  if (!R.logn.p) return 0;
+  HIP_TRY(hipSetDevice(R.device));
+  uint32_t cnt[2] = {0, 0};
+  HIP_TRY(hipMemcpy(cnt, R.logn.p, sizeof(cnt), hipMemcpyDeviceToHost));
+  const uint32_t n0 = std::min(cnt[0], R.clog_cap), n1 = std::min(cnt[1], R.rlog_cap);
+  std::vector<unsigned long long> cl(n0);
+  std::vector<uint32_t> rl(n1);
+  if (n0) HIP_TRY(hipMemcpy(cl.data(), R.clog.p, n0 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  if (n1) HIP_TRY(hipMemcpy(rl.data(), R.rlog.p, n1 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  std::vector<uint32_t> rescued_keys;
+  rescued_keys.reserve(n1);
+  for (uint32_t slot : rl) rescued_keys.push_back(R.cache.slot_key(slot));
+  std::vector<CacheCandidate> cand(n0);
+  for (uint32_t i = 0; i < n0; ++i) {
+    const unsigned long long e = cl[i];
+    CacheCandidate& c = cand[i];
+    c.query = static_cast<uint32_t>(e >> 32) & 0x7FFFFFFFu;
+    c.dev_id = static_cast<uint32_t>(e) & 0x7FFFFFFFu;
+    c.always = ((e >> 31) & 1ull) != 0;
+    c.coin = (e >> 63) != 0;
+    c.key = c.dev_id < h->uid_of_dev.size() ? h->uid_of_dev[c.dev_id] : kInvalid;
+  }
+  const uint64_t a0 = R.cache.admitted, e0 = R.cache.evicted, r0 = R.cache.rescued;
+  std::vector<CacheUpdate> ups;
+  std::vector<uint32_t> cool_on;
+  R.cache.apply_call(std::move(rescued_keys), std::move(cand), ups, cool_on);
+  // one change per slot: the occupant at the call's start leaves cslot, the last one admitted is copied in
+  std::vector<uint32_t> order, first_old, last_new;
+  std::unordered_map<uint32_t, uint32_t> at;
+  for (const CacheUpdate& u : ups) {
+    auto it = at.find(u.slot);
+    if (it == at.end()) {
+      at.emplace(u.slot, static_cast<uint32_t>(order.size()));
+      order.push_back(u.slot);
+      first_old.push_back(u.old_dev);
+      last_new.push_back(u.new_dev);
+    } else {
+      last_new[it->second] = u.new_dev;
+    }
+  }
+  std::vector<uint32_t> upd;
+  for (uint32_t i = 0; i < order.size(); ++i)
+    if (first_old[i] != kInvalid) upd.push_back(first_old[i]);
+  const uint32_t n_drop = static_cast<uint32_t>(upd.size());
+  for (uint32_t i = 0; i < order.size(); ++i) {
+    upd.push_back(order[i]);
+    upd.push_back(last_new[i]);
+  }
+  const uint32_t n_fill = static_cast<uint32_t>(order.size());
+  std::vector<uint32_t> touched(rl);
+  touched.insert(touched.end(), cool_on.begin(), cool_on.end());
+  touched.insert(touched.end(), order.begin(), order.end());
+  std::sort(touched.begin(), touched.end());
+  touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
+  for (uint32_t slot : touched) {  // the engine's final cooling state of every slot this call changed
+    upd.push_back(slot);
+    upd.push_back(R.cache.cooling(slot) ? 1u : 0u);
+  }
+  const uint32_t n_cool = static_cast<uint32_t>(touched.size());
+  if (!upd.empty()) {
+    if (R.upd.n < upd.size()) HIP_TRY(hipStreamSynchronize(R.stream));
+    if (int rc = R.upd.grow(upd.size())) return rc;
+    HIP_TRY(hipMemcpyAsync(R.upd.p, upd.data(), upd.size() * sizeof(uint32_t), hipMemcpyHostToDevice, R.stream));
+    hipError_t e = launch_cache_apply(R.upd.p, n_drop, n_fill, n_cool, R.cslot.p, R.cvec.p, R.cool.p,
+                                      reinterpret_cast<const uint8_t*>(h->svec.view[R.slot].va),
+                                      row_bytes(h->dim, h->elem), R.stream);
+    if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("cache update: ") + hipGetErrorString(e));
+  }
+  HIP_TRY(hipMemsetAsync(R.logn.p, 0, 2 * sizeof(uint32_t), R.stream));
+  HIP_TRY(hipStreamSynchronize(R.stream));  // the upload reads a host vector that goes out of scope here
+  ++R.dyn_call;
+  if (agg) {
+    agg->cache_admitted += R.cache.admitted - a0;
+    agg->cache_evicted += R.cache.evicted - e0;
+    agg->cache_rescued += R.cache.rescued - r0;
+    agg->cache_log_dropped += (cnt[0] - n0) + (cnt[1] - n1);
+  }
+  return 0;
+}
+
 // shine_knn_batch with the handle locked.  access (nullable): per-slot device counters of record reads (warmup).
 int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k, uint32_t ef,
              uint32_t* out_ids, float* out_dists, uint32_t* qstats, shine_stats* stats,
@@ -1267,10 +1393,16 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
       agg.remote_reads_in_bytes += qs[SHINE_QS_REMOTE_VEC] * h->dim * e + qs[SHINE_QS_REMOTE_LIST] * 4ull * h->M0;
       agg.cache_hits += qs[SHINE_QS_CACHED_VEC] + qs[SHINE_QS_CACHED_LIST];
       agg.cache_misses += qs[SHINE_QS_REMOTE_VEC] + qs[SHINE_QS_REMOTE_LIST];
+      // every node read is a cache lookup in the reference (hnsw.hh:524-548): distcomps less the top push (:285)
+      agg.node_reads += qs[SHINE_QS_DISTCOMPS] > 0 ? qs[SHINE_QS_DISTCOMPS] - 1 : 0;
+      agg.node_cache_hits += qs[SHINE_QS_CACHED_VEC];
     }
   }
   agg.overflow_retries = retries;
   agg.kernel_ms = kernel_ms;
+  if (h->cache_policy == SHINE_CACHE_DYNAMIC && !access)  // admission / eviction between calls
+    for (uint32_t r = 0; r < G; ++r)
+      if (int e = apply_dynamic(h, h->reps[r], &agg)) return e;
   if (stats) *stats = agg;
   return rc;
 }
@@ -1514,6 +1646,109 @@ int shine_selftest_heap(int is_max, const int32_t* ops, const float* vals, const
   if (e == hipSuccess && *out_n) e = hipMemcpy(out_ids, di.p, 4ull * *out_n, hipMemcpyDeviceToHost);
   cleanup();
   if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("heap replay: ") + hipGetErrorString(e));
+  return SHINE_OK;
+}
+
+int shine_set_cache_policy(shine_index_t h, int policy, double ratio_percent, uint64_t seed) {
+  if (!h) return set_error(SHINE_ERR_ARG, "index handle is NULL");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (policy == SHINE_CACHE_STATIC) {
+    for (auto& R : h->reps) {
+      HIP_TRY(hipSetDevice(R.device));
+      HIP_TRY(hipDeviceSynchronize());
+      R.release_dynamic();
+    }
+    h->cache_policy = SHINE_CACHE_STATIC;
+    return SHINE_OK;
+  }
+  if (policy != SHINE_CACHE_DYNAMIC) return set_error(SHINE_ERR_ARG, "unknown cache policy");
+  if (h->placement == SHINE_PLACE_REPLICA || h->reps.size() < 2)
+    return set_error(SHINE_ERR_ARG, "the dynamic cache needs a sharded placement over >= 2 GPU slots");
+  if (h->cached_rows || h->cached_list_rows)
+    return set_error(SHINE_ERR_ARG, "the handle holds a static cache (cache_fraction > 0): open it with 0");
+  if (!(ratio_percent > 0.0 && ratio_percent <= 100.0)) return set_error(SHINE_ERR_ARG, "ratio must be in (0, 100]");
+  const uint64_t entries = std::min<uint64_t>(cache_entries(h->N, h->M, h->dim, ratio_percent), 0x7FFFFFFFull);
+  if (!RecordCache::size_ok(static_cast<uint32_t>(entries)))
+    return set_error(SHINE_ERR_ARG, "the cache ratio gives " + std::to_string(entries) +
+                                        " entries, no more than its cooling table holds (the reference's eviction "
+                                        "would never end)");
+  const uint64_t vrow = row_bytes(h->dim, h->elem);
+  for (auto& R : h->reps) {
+    HIP_TRY(hipSetDevice(R.device));
+    HIP_TRY(hipDeviceSynchronize());
+    R.release_dynamic();
+    R.clog_cap = 1u << 22;
+    R.rlog_cap = static_cast<uint32_t>(entries);
+    int rc = 0;
+    if ((rc = R.cslot.grow(h->id_space)) || (rc = R.cvec.grow(entries * vrow)) || (rc = R.cool.grow(entries)) ||
+        (rc = R.clog.grow(R.clog_cap)) || (rc = R.rlog.grow(entries)) || (rc = R.logn.grow(2))) {
+      R.release_dynamic();
+      return rc;
+    }
+    HIP_TRY(hipMemsetAsync(R.cslot.p, 0xFF, h->id_space * sizeof(uint32_t), R.stream));
+    HIP_TRY(hipMemsetAsync(R.cool.p, 0, entries * sizeof(uint32_t), R.stream));
+    HIP_TRY(hipMemsetAsync(R.logn.p, 0, 2 * sizeof(uint32_t), R.stream));
+    HIP_TRY(hipStreamSynchronize(R.stream));
+    R.cache = RecordCache(static_cast<uint32_t>(entries), seed + R.slot);
+  }
+  h->cache_policy = SHINE_CACHE_DYNAMIC;
+  h->cache_seed = seed;
+  h->cache_entries_per_gpu = entries;
+  return SHINE_OK;
+}
+
+int shine_cache_update(shine_index_t h) {
+  if (!h) return set_error(SHINE_ERR_ARG, "index handle is NULL");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (h->cache_policy != SHINE_CACHE_DYNAMIC) return SHINE_OK;
+  for (auto& R : h->reps) {  // every stream of the slot may have searched: wait for the device
+    HIP_TRY(hipSetDevice(R.device));
+    HIP_TRY(hipDeviceSynchronize());
+    if (int rc = apply_dynamic(h, R, nullptr)) return rc;
+  }
+  return SHINE_OK;
+}
+
+int shine_cache_keys(shine_index_t h, uint32_t slot, uint32_t* uids, uint64_t cap, uint64_t* n) {
+  if (!h || !n) return set_error(SHINE_ERR_ARG, "NULL argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (slot >= h->reps.size()) return set_error(SHINE_ERR_ARG, "gpu_slot out of range");
+  const std::vector<uint32_t> keys = h->reps[slot].cache.keys();
+  *n = keys.size();
+  if (uids) std::copy(keys.begin(), keys.begin() + std::min<uint64_t>(cap, keys.size()), uids);
+  return SHINE_OK;
+}
+
+int shine_device_ids(shine_index_t h, const uint32_t* uids, uint32_t n, uint32_t* out) {
+  if (!h || (n && (!uids || !out))) return set_error(SHINE_ERR_ARG, "NULL argument");
+  if (h->dev_of_uid.empty()) return set_error(SHINE_ERR_ARG, "device ids are kept for sharded placements only");
+  for (uint32_t i = 0; i < n; ++i) out[i] = uids[i] < h->dev_of_uid.size() ? h->dev_of_uid[uids[i]] : kInvalid;
+  return SHINE_OK;
+}
+
+int shine_selftest_cache(uint32_t entries, uint64_t seed, uint32_t n_calls, const uint32_t* cand_off,
+                         const uint32_t* cand, const uint32_t* resc_off, const uint32_t* resc, uint32_t* keys,
+                         uint64_t cap, uint64_t* n, uint64_t* counts) {
+  if (!cand_off || !resc_off || !n || !counts) return set_error(SHINE_ERR_ARG, "NULL argument");
+  if (!RecordCache::size_ok(entries)) return set_error(SHINE_ERR_ARG, "cache no larger than its cooling table");
+  RecordCache c(entries, seed);
+  for (uint32_t call = 0; call < n_calls; ++call) {
+    std::vector<uint32_t> rk(resc + resc_off[call], resc + resc_off[call + 1]);
+    std::vector<CacheCandidate> cv;
+    for (uint32_t i = cand_off[call]; i < cand_off[call + 1]; ++i) {
+      const uint32_t* t = cand + 3ull * i;
+      cv.push_back({t[0], t[1], t[1], (t[2] & 1u) != 0, (t[2] & 2u) != 0});
+    }
+    std::vector<CacheUpdate> ups;
+    std::vector<uint32_t> cool_on;
+    c.apply_call(std::move(rk), std::move(cv), ups, cool_on);
+  }
+  const std::vector<uint32_t> k = c.keys();
+  *n = k.size();
+  if (keys) std::copy(k.begin(), k.begin() + std::min<uint64_t>(cap, k.size()), keys);
+  counts[0] = c.admitted;
+  counts[1] = c.evicted;
+  counts[2] = c.rescued;
   return SHINE_OK;
 }
 

@@ -24,6 +24,23 @@ struct DevGraph {
   uint32_t sharded, slot, stripe_ids, cached_rows, div_magic, div_shift;
   uint32_t cached_list_rows;  // lists of rows x % stripe_ids < cached_list_rows are cached (the arrays' cached
                               // prefixes are whole VM pages of each array, so the two row counts differ)
+  // Dynamic record cache (SHINE_CACHE_DYNAMIC, the reference's cache::Cache, cache.hh:102-311): this GPU's arena of
+  // record vectors, fixed during a call and updated between calls by the host's admission / eviction engine.
+  // Kernels built with ACCT = 2 look every off-stripe vector read up in cslot: a hit reads the local arena row and
+  // rescues a cooling entry (cache.hh:128-132: its slot goes to rlog), a miss reads over xGMI and is offered for
+  // admission through clog (entry point and upper levels always, level-0 reads while the cache is not full or when
+  // their coin passes, hnsw.hh:447-448).
+  const uint32_t* cslot;      // [id space]: arena slot of device id x, or 0xFFFFFFFF
+  const void* cvec;           // [arena slots][row]: cached vectors, device row layout
+  uint32_t* cool;             // [arena slots]: 1 while the entry is cooling
+  unsigned long long* clog;   // admission candidates: (query << 32) | x | always << 31 | coin << 63
+  uint32_t* clog_n;           // [0] candidates logged (may exceed clog_cap: the overflow is counted, not stored);
+                              // [1] rescued slots logged
+  uint32_t* rlog;             // rescued arena slots
+  uint32_t clog_cap, rlog_cap;
+  uint32_t dyn_full;          // the cache was full when the call started: level-0 misses draw the coin
+  uint32_t dyn_call;          // call counter (coin input)
+  unsigned long long dyn_seed;
 };
 
 // Per-query counter words (u32) written by the search kernels; include/shine_gpu.h SHINE_QS_*.
@@ -152,6 +169,13 @@ SHINE_BYTE_DIMS(SHINE_DECLARE_BDIM)
 // Returns hipSuccess or the launch error.  grid = number of persistent search slots (one wavefront each).
 hipError_t launch_search(uint32_t dim, int metric, int elem, uint32_t grid, const SearchArgs& a, hipStream_t s);
 hipError_t launch_distance(uint32_t dim, int metric, int elem, const DistArgs& a, hipStream_t s);
+
+// Dynamic record cache updates between calls (capi.cc apply_dynamic), in order on one stream: drop the departing
+// device ids from cslot; copy the admitted records' rows (row_bytes each, from the GPU's view of the vectors) into
+// their arena slots and point cslot at them; set the cooling flags.  upd = [drop ids (n_drop) | (slot, id) pairs
+// (n_fill) | (slot, flag) pairs (n_cool)].
+hipError_t launch_cache_apply(const uint32_t* upd, uint32_t n_drop, uint32_t n_fill, uint32_t n_cool, uint32_t* cslot,
+                              uint8_t* cvec, uint32_t* cool, const uint8_t* vec, uint64_t row_bytes, hipStream_t s);
 
 // Diagnostics: replay push / pop / push_k sequences through the device heap routines (one wavefront).
 hipError_t launch_heap_replay(int is_max, const int32_t* ops, const float* vals, const uint32_t* ids, uint32_t n_ops,

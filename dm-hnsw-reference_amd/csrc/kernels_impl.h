@@ -428,10 +428,8 @@ __device__ __forceinline__ void issue_pass(NbrBuf<D, E, P>& B, int p, const E* _
 // Unconditional form: always the same number of load instructions (an INV slot reads the local node `pad` and is
 // ignored), so that the compiler's vmcnt bookkeeping stays exact across the software pipeline of search_fast_kernel.
 template <int D, typename E, int P>
-__device__ __forceinline__ void issue_pass_u(NbrBuf<D, E, P>& B, int p, const E* __restrict__ vec, u32 id, u32 pad,
-                                             int c4) {
+__device__ __forceinline__ void issue_row(NbrBuf<D, E, P>& B, int p, const E* __restrict__ row, int c4) {
   using L = Lay<D, E>;
-  const E* row = vec + static_cast<u64>(id == INV ? pad : id) * kRowElems<D, E>;
   if constexpr (kByte<E>) {
     load_byte_row<D, E, P>(B, p, row, c4);
   } else {
@@ -441,6 +439,12 @@ __device__ __forceinline__ void issue_pass_u(NbrBuf<D, E, P>& B, int p, const E*
 #pragma unroll
     for (int t = 0; t < L::TAIL; ++t) B.xt[p][t] = to_f32(row[L::DB + t]);
   }
+}
+
+template <int D, typename E, int P>
+__device__ __forceinline__ void issue_pass_u(NbrBuf<D, E, P>& B, int p, const E* __restrict__ vec, u32 id, u32 pad,
+                                             int c4) {
+  issue_row<D, E, P>(B, p, vec + static_cast<u64>(id == INV ? pad : id) * kRowElems<D, E>, c4);
 }
 
 // byte i of word w widened to f32 (exact): v_cvt_f32_ubyte{i} for u8, a sign-extending extract + convert for i8
@@ -629,13 +633,47 @@ __device__ __forceinline__ u32 read_class(const DevGraph& g, u32 x, u32 cached) 
   return s == g.slot ? 0u : (r < cached ? 1u : 2u);
 }
 
-// vector reads of the lanes with `active` set (each reads record x).  ACCT = false (replica, no warmup) compiles
-// the accounting out of the search loop.
-template <bool ACCT>
-__device__ __forceinline__ void count_vec_reads(const SearchArgs& A, ReadCount& rc, bool active, u32 x) {
+// The coin of a level-0 miss once the cache is full (hnsw.hh:447-448, ADMISSION_RATIO = 0.01, constants.hh:16): a
+// SplitMix64 hash of (seed, call, query, device id) below 0.01 * 2^24 in its top 24 bits (oracle/cache_ref.py).
+__device__ __forceinline__ bool admission_coin(unsigned long long seed, u32 call, u32 q, u32 x) {
+  unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (call + 1ull) + 0xC2B2AE3D27D4EB4Full * (q + 1ull) +
+                         0x165667B19E3779F9ull * (x + 1ull);
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (z >> 40) < static_cast<unsigned long long>(0.01 * (1 << 24));
+}
+
+// vector reads of the lanes with `active` set (each reads record x; `always`: an entry-point or upper-level read,
+// admitted without the coin).  ACCT = 0 (replica, no warmup) compiles the accounting out of the search loop; ACCT = 2
+// adds the dynamic cache's lookups and logs (DevGraph::cslot).
+template <int ACCT>
+__device__ __forceinline__ void count_vec_reads(const SearchArgs& A, ReadCount& rc, bool active, u32 x, u32 qi = 0,
+                                                bool always = false) {
   if constexpr (!ACCT) return;
   if (A.g.sharded) {
-    const u32 c = active ? read_class(A.g, x, A.g.cached_rows) : 0u;
+    u32 c = active ? read_class(A.g, x, A.g.cached_rows) : 0u;
+    if constexpr (ACCT == 2) {
+      if (c == 2u) {
+        const u32 slot = A.g.cslot[x];
+        if (slot != INV) {
+          c = 1u;
+          if (A.g.cool[slot] && atomicExch(&A.g.cool[slot], 0u)) {  // a hit on a cooling entry: second chance
+            const u32 i = atomicAdd(&A.g.clog_n[1], 1u);
+            if (i < A.g.rlog_cap) A.g.rlog[i] = slot;
+          }
+        } else {
+          const bool coin = admission_coin(A.g.dyn_seed, A.g.dyn_call, qi, x);
+          if (always || !A.g.dyn_full || coin) {
+            const u32 i = atomicAdd(&A.g.clog_n[0], 1u);
+            if (i < A.g.clog_cap)
+              A.g.clog[i] = (static_cast<unsigned long long>(qi) << 32) | x | (always ? 0x80000000ull : 0ull) |
+                            (coin ? 0x8000000000000000ull : 0ull);
+          }
+        }
+      }
+    }
     rc.vec_remote += __popcll(__ballot(c == 2u));
     rc.vec_cached += __popcll(__ballot(c == 1u));
   }
@@ -643,7 +681,7 @@ __device__ __forceinline__ void count_vec_reads(const SearchArgs& A, ReadCount& 
 }
 
 // one neighbour-list read of record x (x uniform over the wave)
-template <bool ACCT>
+template <int ACCT>
 __device__ __forceinline__ void count_list_read(const SearchArgs& A, ReadCount& rc, u32 x, int lane) {
   if constexpr (!ACCT) return;
   if (A.g.sharded) {
@@ -690,14 +728,14 @@ __device__ __forceinline__ u32 sortable(float f) {  // order-preserving u32 imag
   return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
 }
 
-template <int D, int METRIC, typename E, bool ACCT>
+template <int D, int METRIC, typename E, int ACCT>
 __device__ __forceinline__ void entry_and_descent(const SearchArgs& A, const E* __restrict__ vec,
                                                   const QueryRegs<D, E>& Q, u32* sc_ids, float* sc_d, int lane,
                                                   u32& nn, float& closest, u32& st_dist, u32& st_vup, u32& st_vl0,
-                                                  u32& st_lup, u32& status, ReadCount& rc) {
+                                                  u32& st_lup, u32& status, ReadCount& rc, u32 qi) {
   const u32 ep = A.g.ep;
   if (lane == 0) sc_ids[0] = ep;
-  count_vec_reads<ACCT>(A, rc, lane == 0, ep);
+  count_vec_reads<ACCT>(A, rc, lane == 0, ep, qi, true);
   wave_sync();
   dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, 1, lane);
   wave_sync();
@@ -721,7 +759,7 @@ __device__ __forceinline__ void entry_and_descent(const SearchArgs& A, const E* 
       st_vup += cnt;
       st_dist += cnt;
       if (valid) sc_ids[lane] = e;
-      count_vec_reads<ACCT>(A, rc, valid, e);  // upper-level lists are replicated: only the vectors can be remote
+      count_vec_reads<ACCT>(A, rc, valid, e, qi, true);  // upper-level lists are replicated: only vectors can be remote
       wave_sync();
       dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, cnt, lane);
       wave_sync();
@@ -822,7 +860,7 @@ struct VisitedLds<0> {
   __device__ __forceinline__ void spill(u32* __restrict__ bits, const SearchArgs& A, int lane) const {
     for (u32 i = lane; i <= mask; i += 64) {
       const u32 x = t[i];
-      if (x != INV) atomicOr(&bits[x >> 5], 1u << (x & 31));
+      if (x < A.g.N) atomicOr(&bits[x >> 5], 1u << (x & 31));
     }
   }
   __device__ __forceinline__ bool at_home(u32 x) const { return t[vhash(x, shift)] == x; }
@@ -884,7 +922,7 @@ struct VisitedLds<1> {
         if (v == 0xFFFFu) continue;
         const u32 home = (b - (v & ((1u << dbits) - 1u))) & bmask_b;
         const u32 x = (((home << rbits) | (v >> dbits)) * A.vis_mul_inv) & bmask;
-        atomicOr(&bits[x >> 5], 1u << (x & 31));
+        if (x < A.g.N) atomicOr(&bits[x >> 5], 1u << (x & 31));
       }
     }
   }
@@ -994,7 +1032,7 @@ __device__ __forceinline__ void finish_call(const SearchArgs& A, int lane) {
   for (int i = 0; i < 8; ++i) __atomic_store_n(&c[i], 0u, __ATOMIC_RELAXED);
 }
 
-template <int D, int METRIC, typename E, int VIS, bool ACCT, int VT = 0, bool PROF = false>
+template <int D, int METRIC, typename E, int VIS, int ACCT, int VT = 0, bool PROF = false>
 __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
   PhaseClock<PROF> clk;
   clk.start();
@@ -1042,7 +1080,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
     u32 nn;
     float closest;
     entry_and_descent<D, METRIC, E, ACCT>(A, vec, Q, sc_ids, sc_d, lane, nn, closest, st_dist, st_vup, st_vl0, st_lup, status,
-                                    rc);
+                                    rc, qi);
 
     // ---- top_candidates.push({nn, dist(q, nn)}) (hnsw.hh:285-286) ---------------------------------------
     ++st_dist;
@@ -1079,6 +1117,10 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         hfence();
         --nnext;
         if (ck > farthest0) break;  // :421-426
+        if (cid >= A.g.N) {  // a heap entry that is not a record: report it, never dereference it
+          status = ST_FORMAT;
+          break;
+        }
 
         // neighbour list of the candidate at level 0 (:436-438)
         PHASE(3)
@@ -1108,7 +1150,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         }
         const u64 fm = __ballot(fresh);
         const int nf = __popcll(fm);
-        count_vec_reads<ACCT>(A, rc, fresh, e);
+        count_vec_reads<ACCT>(A, rc, fresh, e, qi);
         if (fresh) {
           const int r = __popcll(fm & below);
           sc_ids[r] = e;
@@ -1150,8 +1192,8 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
             const u64 hit = __ballot(pd_l == pd);
             pid = __builtin_amdgcn_readlane(static_cast<int>(my_id), static_cast<int>(__builtin_ctzll(hit)));
           }
-          pre_id = pid;
-          if (pid != INV && static_cast<u32>(lane) < M0) pre_e = A.g.adj0[static_cast<u64>(pid) * M0 + lane];
+          pre_id = pid < A.g.N ? pid : INV;
+          if (pre_id != INV && static_cast<u32>(lane) < M0) pre_e = A.g.adj0[static_cast<u64>(pre_id) * M0 + lane];
         }
 
         // accept / push / push_k in list order (:456-465)
@@ -1301,16 +1343,47 @@ __device__ __forceinline__ u32 quad_bcast(u32 x, int p) {  // lane 4g + p's valu
   }
 }
 
-template <int D, typename E, int P>
-__device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restrict__ vec, u32 e, u32 pad, int c4) {
-  u32 sid[P];
+template <int D, typename E, int P, int ACCT>
+__device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restrict__ vec, u32 e, u32 pad, int c4,
+                                           const DevGraph& g) {
+  if constexpr (ACCT == 2) {  // dynamic cache: each lane resolves its own list slot to a row, the groups share it
+    const E* row = vec + static_cast<u64>(e == INV ? pad : e) * kRowElems<D, E>;
+    if (e != INV && read_class(g, e, 0u) == 2u) {
+      const u32 c = g.cslot[e];
+      if (c != INV) row = static_cast<const E*>(g.cvec) + static_cast<u64>(c) * kRowElems<D, E>;
+    }
+    const u64 rp = reinterpret_cast<u64>(row);
 #pragma unroll
-  for (int p = 0; p < P; ++p) sid[p] = quad_bcast(e, p);
+    for (int p = 0; p < P; ++p) {
+      const u64 lo = quad_bcast(static_cast<u32>(rp), p), hi = quad_bcast(static_cast<u32>(rp >> 32), p);
+      issue_row<D, E, P>(B, p, reinterpret_cast<const E*>((hi << 32) | lo), c4);
+    }
+  } else {
+    u32 sid[P];
 #pragma unroll
-  for (int p = 0; p < P; ++p) issue_pass_u<D, E, P>(B, p, vec, sid[p], pad, c4);
+    for (int p = 0; p < P; ++p) sid[p] = quad_bcast(e, p);
+#pragma unroll
+    for (int p = 0; p < P; ++p) issue_pass_u<D, E, P>(B, p, vec, sid[p], pad, c4);
+  }
 }
 
-template <int D, int METRIC, typename E, int R, int P, bool ACCT, int VT, bool PROF = false>
+// One of the stream's spill bitmaps for this wavefront (SearchArgs::spill_flags), or -1 when all are held.
+__device__ __forceinline__ int claim_spill_bitmap(const SearchArgs& A, int lane) {
+  if (A.spill_slots == 0) return -1;
+  u32 got = INV;
+  if (lane == 0) {
+    const u32 n = A.spill_slots;
+    for (u32 i = 0, j = blockIdx.x % n; i < n; ++i, j = j + 1 == n ? 0u : j + 1)
+      if (atomicCAS(&A.spill_flags[j], 0u, 1u) == 0u) {
+        got = j;
+        break;
+      }
+  }
+  got = bcast(got);
+  return got == INV ? -1 : static_cast<int>(got);
+}
+
+template <int D, int METRIC, typename E, int R, int P, int ACCT, int VT, bool PROF = false>
 __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
   PhaseClock<PROF> clk;
   clk.start();
@@ -1330,7 +1403,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
   const u32 row_lane = in_row ? my_slot : 0u;
   // Unconditional, and never masked right after the load (that would wait for it): lanes without a slot hold a copy
   // of entry 0 and are excluded where the list is used (the visited test; they are never fresh).
-  auto load_row = [&](u32 node) -> u32 { return adj0[static_cast<u64>(node) * M0 + row_lane]; };
+  auto load_row = [&](u32 node) -> u32 { return adj0[static_cast<u64>(node < A.g.N ? node : pad) * M0 + row_lane]; };
   auto slot_of = [](int l) { return 16 * (l & 3) + (l >> 2); };
 
   const u32 n_items = A.in_count ? *A.in_count : A.nq;
@@ -1351,7 +1424,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
     u32 nn;
     float closest;
     entry_and_descent<D, METRIC, E, ACCT>(A, vec, Q, sc_ids, sc_d, lane, nn, closest, st_dist, st_vup, st_vl0, st_lup, status,
-                                    rc);
+                                    rc, qi);
     ++st_dist;  // top_candidates.push({nn, dist(q, nn)}) (hnsw.hh:285-286)
 
     float ck[R];  // candidate keys, ascending; +inf beyond the size
@@ -1377,7 +1450,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
     // prefetched list.  X is refilled for the next candidate as soon as the current distances have consumed it.
     NbrBuf<D, E, P> X;
     u32 e = load_row(status == 0 ? nn : pad);
-    issue_list<D, E, P>(X, vec, e, pad, c4);
+    issue_list<D, E, P, ACCT>(X, vec, e, pad, c4, A.g);
     u32 r_id = INV;
     float r_key = INF;
     u32 nid = nn;
@@ -1388,30 +1461,9 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
                                                                       // expansion earlier (VisitedLds::test_and_set)
     // In-place spill (SearchArgs::spill_flags): once the table overflows, the query's visited set moves to an HBM
     // bitmap and the search goes on there (a global atomicOr per fresh id) instead of being re-run from scratch.
+    // (Plain code, no lambda: a bitmap pointer assigned through a lambda's reference capture compiled to a constant
+    // null base on this toolchain.)
     int sslot = -1;  // the bitmap this query holds (wave-uniform), -1 = the LDS table
-    u32* __restrict__ sbits = nullptr;
-    // claim a bitmap and copy the table into it; then the ids of the lanes with `record` set go in too
-    auto spill = [&](bool record) -> bool {
-      if (A.spill_slots == 0) return false;
-      u32 got = INV;
-      if (lane == 0) {
-        const u32 n = A.spill_slots;
-        for (u32 i = 0, j = blockIdx.x % n; i < n; ++i, j = j + 1 == n ? 0u : j + 1)
-          if (atomicCAS(&A.spill_flags[j], 0u, 1u) == 0u) {
-            got = j;
-            break;
-          }
-      }
-      got = bcast(got);
-      if (got == INV) return false;
-      sslot = static_cast<int>(got);
-      sbits = A.visited + static_cast<u64>(got) * A.words_per_slot;
-      wave_sync();
-      vis.spill(sbits, A, lane);
-      if (record) atomicOr(&sbits[e >> 5], 1u << (e & 31));
-      EVENT(3)
-      return true;
-    };
 
     while (status == 0) {
       ++st_ll0;  // read_neighborlist (:436-438)
@@ -1433,8 +1485,9 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       u32 pw = INV, pexp = 0, pold = 0;
       if (sslot >= 0) {  // spilled: the HBM bitmap
         if (cand) {
+          u32* sb = A.visited + static_cast<u64>(sslot) * A.words_per_slot;
           const u32 bit = 1u << (e & 31);
-          fresh = (atomicOr(&sbits[e >> 5], bit) & bit) == 0u;
+          fresh = (atomicOr(&sb[e >> 5], bit) & bit) == 0u;
         }
       } else if constexpr (VT == 1) {
         if (cand) {
@@ -1449,20 +1502,26 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       // id there instead of retrying in the table.
       if (sslot < 0 && (__ballot(vovf) || nvis + __popcll(__ballot(fresh)) > A.vis_limit)) {
         const bool lost = pw != INV && pold != pexp;
-        if (!spill(lost)) {
+        sslot = claim_spill_bitmap(A, lane);
+        if (sslot < 0) {
           status = ST_OVERFLOW;
           break;
         }
+        u32* sb = A.visited + static_cast<u64>(sslot) * A.words_per_slot;
+        wave_sync();
+        vis.spill(sb, A, lane);
+        EVENT(3)
+        if (lost) atomicOr(&sb[e >> 5], 1u << (e & 31));
         pw = INV;
         if (vovf) {
           const u32 bit = 1u << (e & 31);
-          fresh = (atomicOr(&sbits[e >> 5], bit) & bit) == 0u;
+          fresh = (atomicOr(&sb[e >> 5], bit) & bit) == 0u;
           vovf = false;
         }
       }
       const u64 fm = __ballot(fresh);
       const int nf = __popcll(fm);
-      count_vec_reads<ACCT>(A, rc, fresh, e);
+      count_vec_reads<ACCT>(A, rc, fresh, e, qi);
       nvis += nf;
       st_vl0 += nf;
       st_dist += nf;
@@ -1488,9 +1547,17 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
 
       if constexpr (VT == 1) {  // the deferred compare-and-swaps, before the table is probed again
         if (pw != INV) vis.finish(e, pexp, pold, vovf);
-        if (__ballot(vovf) && !spill(vovf)) {  // a retried insert overflowed: its id is fresh, record it in HBM
-          status = ST_OVERFLOW;
-          break;
+        if (__ballot(vovf)) {  // a retried insert overflowed: its id is fresh, record it in HBM
+          sslot = claim_spill_bitmap(A, lane);
+          if (sslot < 0) {
+            status = ST_OVERFLOW;
+            break;
+          }
+          u32* sb = A.visited + static_cast<u64>(sslot) * A.words_per_slot;
+          wave_sync();
+          vis.spill(sb, A, lane);
+          EVENT(3)
+          if (vovf) atomicOr(&sb[e >> 5], 1u << (e & 31));
         }
       }
 
@@ -1520,7 +1587,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       const bool probe = sslot < 0 && in_row && prow != INV;
       const typename VisitedLds<VT>::Hint pword = probe ? vis.probe(prow) : VisitedLds<VT>::unknown();
       const bool seen = probe && vis.home_match(prow, pword);
-      issue_list<D, E, P>(X, vec, seen ? INV : prow, pad, c4);
+      issue_list<D, E, P, ACCT>(X, vec, seen ? INV : prow, pad, c4, A.g);
 
       // ---- merge (:456-465 over the whole list at once) ----------------------------------------------------------
       PHASE(6)
@@ -1620,7 +1687,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       if (c != pid) {  // mispredicted (ties / NaN keys): fetch the picked candidate's list and vectors
         EVENT(11)
         erow = c == nid ? nrow : load_row(c);
-        issue_list<D, E, P>(X, vec, erow, pad, c4);
+        issue_list<D, E, P, ACCT>(X, vec, erow, pad, c4, A.g);
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this rare path leaves nothing in flight behind the prefetch
       }
       nid = c2 != INV ? c2 : c;
@@ -1650,7 +1717,7 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
     for (int r = 0; r < R; ++r) {
       const u32 i = static_cast<u32>(64 * r + lane);
       if (i < A.k) {
-        const bool ok = status == 0 && static_cast<int>(i) < cs;
+        const bool ok = status == 0 && static_cast<int>(i) < cs && (ci[r] & ~EXPANDED) < A.g.N;
         A.out_ids[obase + i] = ok ? A.g.uid[ci[r] & ~EXPANDED] : INV;
         if (A.out_dists) A.out_dists[obase + i] = ok ? ck[r] : 0.f;
       }
@@ -1670,10 +1737,14 @@ __global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
       write_read_counts(qs, rc);
     }
     if (sslot >= 0) {  // hand the bitmap back all zero: the stores land before the flag drops
-      for (u64 w = lane; w < A.words_per_slot; w += 64) sbits[w] = 0u;
+      u32* sb = A.visited + static_cast<u64>(sslot) * A.words_per_slot;
+      for (u64 w = lane; w < A.words_per_slot; w += 64) sb[w] = 0u;
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
       __threadfence();
-      if (lane == 0) atomicExch(&A.spill_flags[sslot], 0u);
+      // Every lane stores the same zero (one dword).  A lane-0 branch here, the last statement of the item loop,
+      // was jump-threaded into the next item's lane-0 fetch: the wave split, lanes 1-63 ran an item without lane 0
+      // and faulted (tests/test_gpu_fast.py::test_fast_mode_spills_in_place_and_stays_exact).
+      __hip_atomic_store(&A.spill_flags[sslot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   clk.flush(A.prof, lane);
@@ -1757,7 +1828,7 @@ __global__ __launch_bounds__(64) void heap_replay_kernel(const int32_t* ops, con
   if (lane == 0) *out_n = root_ok ? static_cast<u32>(n) : 0xFFFFFFFFu;
 }
 
-template <int D, int METRIC, typename E, bool AC>
+template <int D, int METRIC, typename E, int AC>
 hipError_t launch_search_acct(uint32_t grid, const SearchArgs& a, hipStream_t s) {
   const size_t lds = search_lds_bytes(a.ef, a.cap, a.vis_cap, a.vis16 && a.vis_cap > 0 ? 2 : 4);
   auto run = [&](auto kern) -> hipError_t {
@@ -1814,8 +1885,9 @@ hipError_t launch_search_acct(uint32_t grid, const SearchArgs& a, hipStream_t s)
 // Read accounting (qstats words 8-11, cache-warmup counters) is compiled in only where it can count something.
 template <int D, int METRIC, typename E>
 hipError_t launch_search_t(uint32_t grid, const SearchArgs& a, hipStream_t s) {
-  if (a.g.sharded || a.access) return launch_search_acct<D, METRIC, E, true>(grid, a, s);
-  return launch_search_acct<D, METRIC, E, false>(grid, a, s);
+  if (a.g.sharded && a.g.cslot) return launch_search_acct<D, METRIC, E, 2>(grid, a, s);  // dynamic cache
+  if (a.g.sharded || a.access) return launch_search_acct<D, METRIC, E, 1>(grid, a, s);
+  return launch_search_acct<D, METRIC, E, 0>(grid, a, s);
 }
 
 template <int D, int METRIC, typename E>

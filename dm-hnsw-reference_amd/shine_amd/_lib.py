@@ -22,6 +22,7 @@ QS_REMOTE_VEC, QS_REMOTE_LIST, QS_CACHED_VEC, QS_CACHED_LIST = range(8, 12)
 QS_WORDS = 12
 QS_TIES = 5  # fast mode's meaning of word 5
 MODE_EXACT, MODE_FAST = 0, 1
+CACHE_STATIC, CACHE_DYNAMIC = 0, 1
 PLACE_REPLICA, PLACE_SHARDED, PLACE_SHARDED_REGIONS = 0, 1, 2
 
 
@@ -46,6 +47,12 @@ class Stats(C.Structure):
         ("cache_hits", C.c_uint64),
         ("cache_misses", C.c_uint64),
         ("kernel_ms", C.c_double),
+        ("node_reads", C.c_uint64),
+        ("node_cache_hits", C.c_uint64),
+        ("cache_admitted", C.c_uint64),
+        ("cache_evicted", C.c_uint64),
+        ("cache_rescued", C.c_uint64),
+        ("cache_log_dropped", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -109,6 +116,11 @@ PROTOTYPES = {
     "shine_knn_batch": (I32, [P, P, P, U32, U32, U32, P, P, C.POINTER(Stats)]),  # SURVEY.md §8b's 9 arguments
     "shine_knn_batch_ex": (I32, [P, P, P, U32, U32, U32, P, P, P, C.POINTER(Stats)]),
     "shine_release_stream": (I32, [P, P]),
+    "shine_set_cache_policy": (I32, [P, I32, C.c_double, U64]),
+    "shine_cache_update": (I32, [P]),
+    "shine_cache_keys": (I32, [P, U32, P, U64, C.POINTER(U64)]),
+    "shine_device_ids": (I32, [P, P, U32, P]),
+    "shine_selftest_cache": (I32, [U32, U64, U32, P, P, P, P, P, U64, C.POINTER(U64), P]),
     "shine_cache_warmup": (I32, [P, P, P, U32, U32, U32]),
     "shine_knn_batch_device": (I32, [P, U32, P, U32, U32, U32, P, P, P, P]),
     "shine_distance_batch_device": (I32, [P, U32, P, U32, P, U32, P, P]),

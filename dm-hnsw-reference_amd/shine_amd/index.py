@@ -114,6 +114,28 @@ class Index:
         self.mode = mode
 
     # ---- queries -----------------------------------------------------------------------------------------
+    def set_cache_policy(self, policy: int, ratio_percent: float = 5.0, seed: int = 0) -> None:
+        """SHINE_CACHE_STATIC / SHINE_CACHE_DYNAMIC (include/shine_gpu.h): the reference's runtime admission and
+        cooling-table eviction, applied between calls, ratio_percent % of the estimated index size per GPU."""
+        L.check(L.lib().shine_set_cache_policy(self._h, int(policy), float(ratio_percent), int(seed)))
+
+    def cache_update(self) -> None:
+        L.check(L.lib().shine_cache_update(self._h))
+
+    def cache_keys(self, slot: int) -> np.ndarray:
+        """uids the dynamic cache of GPU slot `slot` holds, ascending."""
+        n = C.c_uint64()
+        L.check(L.lib().shine_cache_keys(self._h, slot, None, 0, C.byref(n)))
+        out = np.empty(n.value, dtype=np.uint32)
+        L.check(L.lib().shine_cache_keys(self._h, slot, _ptr(out), out.size, C.byref(n)))
+        return out
+
+    def device_ids(self, uids: np.ndarray) -> np.ndarray:
+        u = np.ascontiguousarray(uids, dtype=np.uint32)
+        out = np.empty_like(u)
+        L.check(L.lib().shine_device_ids(self._h, _ptr(u), u.size, _ptr(out)))
+        return out
+
     def knn(self, queries: np.ndarray, k: int, ef: int, query_ids: np.ndarray | None = None) -> KnnResult:
         """shine_knn_batch_ex (shine_knn_batch plus per-query counters): query i is answered on GPU slot query_ids[i] % n_gpus (position when None)."""
         q = np.ascontiguousarray(queries, dtype=np.float32)

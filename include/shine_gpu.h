@@ -80,6 +80,14 @@ typedef struct shine_stats {
   uint64_t cache_hits;            /* cache.hits_total: off-stripe record reads served by local copies */
   uint64_t cache_misses;          /* cache.misses_total: off-stripe record reads that crossed xGMI */
   double kernel_ms;               /* device time of the search launch(es), HIP events */
+  /* The reference's cache counters (statistics.hh:159-173), where every node (vector) read is a cache lookup:
+   * cache.hit_rate = node_cache_hits / node_reads. */
+  uint64_t node_reads;            /* node reads: the entry point, upper-level neighbours, fresh level-0 neighbours */
+  uint64_t node_cache_hits;       /* ... served by this GPU's cache (static copies or the dynamic cache) */
+  uint64_t cache_admitted;        /* SHINE_CACHE_DYNAMIC, after this call: records admitted ... */
+  uint64_t cache_evicted;         /* ... evicted through the cooling table ... */
+  uint64_t cache_rescued;         /* ... cooling entries given a second chance by a hit */
+  uint64_t cache_log_dropped;     /* admission candidates past the log's capacity (not offered) */
 } shine_stats;
 
 typedef struct shine_index_info {
@@ -185,6 +193,36 @@ int shine_release_stream(shine_index_t h, void* stream);
  * zero cache fraction.  On failure the handle keeps its previous layout but can no longer be re-ranked. */
 int shine_cache_warmup(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
                        uint32_t ef);
+
+/* Cache policy of a sharded handle (the compute node's record cache, cache::Cache, cache.hh:24-311).
+ * STATIC (default): the cache_fraction of shine_open_ex — each stripe's hottest records (static rank, or the warmup
+ *   re-rank of shine_cache_warmup) copied once to every other GPU.
+ * DYNAMIC: the reference's runtime policy.  Every GPU keeps an arena of ratio_percent % of estimate_index_size(N)
+ *   over 16 + 4d bytes entries (compute_node.cc:40-56, hnsw.hh:309-321).  A search reads a cached record from the
+ *   arena, any other off-stripe record over xGMI; after every shine_knn_batch the misses are admitted (entry point and
+ *   upper levels always, level-0 records while the cache is not full, then with probability 0.01 — hnsw.hh:447-448,
+ *   constants.hh:16), evicting through random cooling and the cooling table, and a hit on a cooling entry rescues it
+ *   (cache.hh:128-132, 232-311, cooling_table.hh:52-98).  The cache is fixed during a call and updated between calls
+ *   (stream-ordered before the next call on the slot's stream); random draws come from SplitMix64 seeded with
+ *   `seed` + slot, so runs are reproducible (oracle/cache_ref.py restates the policy).  Results never depend on it.
+ *   Needs a sharded handle of >= 2 slots opened with cache_fraction 0.  Device-API calls (shine_knn_batch_device)
+ *   read the cache but their misses are applied only by shine_cache_update. */
+#define SHINE_CACHE_STATIC 0
+#define SHINE_CACHE_DYNAMIC 1
+int shine_set_cache_policy(shine_index_t h, int policy, double ratio_percent, uint64_t seed);
+/* Apply the misses and rescues logged since the last update (shine_knn_batch does this itself after every call). */
+int shine_cache_update(shine_index_t h);
+/* Diagnostics: the uids GPU slot `slot`'s dynamic cache holds, ascending (*n = count; up to cap written), and the
+ * device ids of uids (0xFFFFFFFF where a uid is not a record). */
+int shine_cache_keys(shine_index_t h, uint32_t slot, uint32_t* uids, uint64_t cap, uint64_t* n);
+int shine_device_ids(shine_index_t h, const uint32_t* uids, uint32_t n, uint32_t* out);
+/* Diagnostics (host only): the dynamic cache's policy engine driven by explicit logs, for tests against its
+ * restatement.  entries / seed as a GPU slot's cache; call c offers cand[cand_off[c] .. cand_off[c+1]) (triples
+ * query, key, flags: bit 0 always, bit 1 coin) after rescuing resc[resc_off[c] .. resc_off[c+1]) (keys).  Writes the
+ * final keys ascending (up to cap; *n = count) and counts[0..2] = admitted, evicted, rescued. */
+int shine_selftest_cache(uint32_t entries, uint64_t seed, uint32_t n_calls, const uint32_t* cand_off,
+                         const uint32_t* cand, const uint32_t* resc_off, const uint32_t* resc, uint32_t* keys,
+                         uint64_t cap, uint64_t* n, uint64_t* counts);
 
 /* The GPU slot each query of a batch is answered on: id % n_gpus, or for SHINE_PLACE_SHARDED_REGIONS the slot the
  * handle's query router picks (QueryRouter::run_routing, query_router.hh:280-387): the closest region whose count in

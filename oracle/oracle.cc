@@ -300,6 +300,11 @@ struct SearchState {
   MinHeap next_candidates;
   u32 qs[QS_WORDS] = {0};
   u64 distcomps = 0;
+  // record reads in order (nullable): every cache_lookup of a node (hnsw.hh:263, 368, 449), as (node, admit-always)
+  std::vector<std::pair<u64, bool>>* reads = nullptr;
+  void read(u64 r, bool always) {
+    if (reads) reads->emplace_back(r, always);
+  }
 };
 
 // hnsw.hh:331-393 — greedy 1-NN descent from begin_level down to target_level+1
@@ -315,6 +320,7 @@ static void search_for_one(const Index& I, const f32* q, u64& nearest_neighbor, 
       const u32 cnt = Index::list_count(nl);
       for (u32 i = 0; i < cnt; ++i) {  // :364
         const u64 r_ptr = Index::list_at(nl, i);
+        st.read(r_ptr, true);       // cache_lookup, inner nodes always admitted (:368)
         ++st.qs[QS_VISITED_UPPER];  // inc_visited_nodes(level), level > 0
         const f32 d = I.dist(q, I.comps(r_ptr));  // :375
         ++st.distcomps;
@@ -352,6 +358,7 @@ static void search_level(const Index& I, const f32* q, u32 ef, u32 level, Search
       if (!visited.contains(nb)) {  // :441
         if (level > 0) ++st.qs[QS_VISITED_UPPER]; else ++st.qs[QS_VISITED_L0];  // :442
         visited.insert(nb);                                                     // :443
+        st.read(nb, level > 0);                                                 // cache_lookup (:447-449)
         farthest_dist = top.top().distance;                                     // :456
         const f32 nd = I.dist(q, I.comps(nb));                                   // :458
         ++st.distcomps;
@@ -374,6 +381,7 @@ static void knn(const Index& I, const f32* q, u32 k, u32 ef, SearchState& st, u3
   st.distcomps = 0;
   const u64 ep_ptr = I.ep_ptr();  // :256-259
   const u64 entry_point = ep_ptr; // cache_lookup → read_node (:261-268)
+  st.read(entry_point, true);
   if (I.level(entry_point) > 0) ++st.qs[QS_VISITED_UPPER]; else ++st.qs[QS_VISITED_L0];  // :270
   const f32 ep_distance = I.dist(q, I.comps(entry_point));  // :271
   ++st.distcomps;
@@ -661,6 +669,37 @@ int oracle_knn_pinned(void* h, const float* queries, uint32_t nq, uint32_t k, ui
 int oracle_knn(void* h, const float* queries, uint32_t nq, uint32_t k, uint32_t ef, uint32_t* out_ids,
                float* out_dists, uint32_t* stats, uint32_t n_threads) {
   return oracle_knn_pinned(h, queries, nq, k, ef, out_ids, out_dists, stats, n_threads, nullptr);
+}
+
+// knn with the record reads of every query (single thread): reads[offsets[i] .. offsets[i+1]) are query i's node
+// reads in order, each (uid << 1) | always, where always = 1 for the entry point and upper-level nodes (admitted
+// without the coin, hnsw.hh:263, 368) and 0 for level-0 neighbours (hnsw.hh:447-448); nodes[] the memory node of
+// each read.  Returns 3 when cap is too small.  The reads are what a compute-node cache sees (cache_lookup).
+int oracle_knn_trace(void* h, const float* queries, uint32_t nq, uint32_t k, uint32_t ef, uint32_t* out_ids,
+                     float* out_dists, uint32_t* stats, uint32_t* reads, uint16_t* nodes, uint64_t cap,
+                     uint64_t* offsets) {
+  const Index& I = *static_cast<Index*>(h);
+  if (ef < k) return 1;
+  if (I.ep_ptr() == 0) return 2;
+  SearchState st;
+  std::vector<std::pair<u64, bool>> rd;
+  st.reads = &rd;
+  uint64_t n = 0;
+  offsets[0] = 0;
+  for (u32 qi = 0; qi < nq; ++qi) {
+    rd.clear();
+    knn(I, queries + static_cast<size_t>(qi) * I.L.dim, k, ef, st, out_ids + static_cast<size_t>(qi) * k,
+        out_dists ? out_dists + static_cast<size_t>(qi) * k : nullptr);
+    if (stats) std::memcpy(stats + static_cast<size_t>(qi) * QS_WORDS, st.qs, sizeof(st.qs));
+    if (n + rd.size() > cap) return 3;
+    for (const auto& [r, always] : rd) {
+      reads[n] = (I.uid(r) << 1) | (always ? 1u : 0u);
+      nodes[n] = static_cast<uint16_t>(rp_node(r));
+      ++n;
+    }
+    offsets[qi + 1] = n;
+  }
+  return 0;
 }
 
 // Distances of explicit (query, node-uid) pairs, for distance-kernel parity.  node_uids index the dense

@@ -42,6 +42,8 @@ def lib(path: Path = LIB_PATH):
         L.oracle_free.argtypes = [P]
         L.oracle_knn.restype = I32
         L.oracle_knn.argtypes = [P, P, U32, U32, U32, P, P, P, U32]
+        L.oracle_knn_trace.restype = I32
+        L.oracle_knn_trace.argtypes = [P, P, U32, U32, U32, P, P, P, P, P, C.c_uint64, P]
         L.oracle_knn_pinned.restype = I32
         L.oracle_knn_pinned.argtypes = [P, P, U32, U32, U32, P, P, P, U32, P]
         L.oracle_distance.restype = C.c_float
@@ -104,6 +106,25 @@ class OracleIndex:
         if rc != 0:
             raise RuntimeError(f"oracle_knn failed: {rc}")
         return ids, dd, qs
+
+    def knn_trace(self, queries, k, ef, cap_per_query=None):
+        """knn (one thread) plus every query's record reads in order: (uids, always, memory_nodes, offsets); reads
+        offsets[i]:offsets[i+1] belong to query i, always = entry point / upper-level node (admitted without the coin)."""
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        nq = q.shape[0]
+        cap = nq * (cap_per_query or 64 * ef + 1024)
+        ids = np.empty((nq, k), np.uint32)
+        dd = np.empty((nq, k), np.float32)
+        qs = np.empty((nq, QS_WORDS), np.uint32)
+        reads = np.empty(cap, np.uint32)
+        nodes = np.empty(cap, np.uint16)
+        off = np.zeros(nq + 1, np.uint64)
+        rc = self._lib.oracle_knn_trace(self._h, _p(q), nq, k, ef, _p(ids), _p(dd), _p(qs), _p(reads), _p(nodes), cap,
+                                        _p(off))
+        if rc != 0:
+            raise RuntimeError(f"oracle_knn_trace failed: {rc}")
+        n = int(off[-1])
+        return (ids, dd, qs), (reads[:n] >> 1, (reads[:n] & 1).astype(bool), nodes[:n].copy(), off.astype(np.int64))
 
     def close(self):
         if self._h:
