@@ -756,10 +756,12 @@ LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds
                             uint32_t learned = 0, bool grow = false) {
   LaunchShape sh{};
   const uint32_t want = std::max<uint32_t>(1, std::min<uint32_t>(16, (nq + cus - 1) / cus));
-  const uint32_t target = std::min<uint32_t>(16, 2 * want);
+  // tuning hooks (measurement): waves per CU the tables are sized for, in batches of `want`; table floor per ef
+  const uint32_t target = std::min<uint32_t>(16, static_cast<uint32_t>(env_int("SHINE_FAST_TARGET_BATCHES", 2)) * want);
   // a table below pow2(40·ef) entries sends a measurable share of queries to the light pass (ef = 128 on the bench's
   // index: 4,096 entries gave 1.1 M QPS against 4.2 M for 8,192), whatever residency it buys
-  uint32_t lo = std::min<uint32_t>(16384, std::max<uint32_t>(2048, pow2_at_least(40 * ef)));
+  const uint32_t per_ef = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_FAST_TABLE_PER_EF", 40)));
+  uint32_t lo = std::min<uint32_t>(16384, std::max<uint32_t>(2048, pow2_at_least(per_ef * ef)));
   // what the previous call's queries needed: a smaller table, or a larger one once the fixed size overflowed
   if (learned && (learned < lo || grow)) lo = learned;
   const uint32_t hi = std::min<uint32_t>(16384, std::max<uint32_t>(lo, pow2_at_least(48 * ef)));

@@ -1383,8 +1383,14 @@ __device__ __forceinline__ int claim_spill_bitmap(const SearchArgs& A, int lane)
   return got == INV ? -1 : static_cast<int>(got);
 }
 
+// Waves per SIMD the register allocation must allow (build-time tuning: 4 caps a wave at 128 VGPRs, so 16 wavefronts
+// fit a CU when their LDS tables do).
+#ifndef SHINE_FAST_MIN_WAVES
+#define SHINE_FAST_MIN_WAVES 1
+#endif
 template <int D, int METRIC, typename E, int R, int P, int ACCT, int VT, bool PROF = false>
-__global__ __launch_bounds__(64) void search_fast_kernel(SearchArgs A) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHINE_FAST_MIN_WAVES))) void search_fast_kernel(
+    SearchArgs A) {
   PhaseClock<PROF> clk;
   clk.start();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

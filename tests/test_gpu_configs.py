@@ -186,3 +186,55 @@ def test_cfg5_fp16_zipf_mix_recall(gpu_available):
                 np.testing.assert_array_equal(r.ids[i], r.ids[first[s]])
             else:
                 first[s] = i
+
+
+@pytest.mark.parametrize("policy", ["warmup", "dynamic"])
+def test_cfg5_fp16_eight_slots_cached_skewed_stream(policy, gpu_available):
+    """cfg 5 as one workload: fp16 records, eight memory-node dumps over eight GPU slots, a 5 % cache of the other
+    stripes (ranked by a warmup split, shine_cache_warmup, or run by the reference's admission / cooling policy
+    between calls, SHINE_CACHE_DYNAMIC), a Zipf alpha=1 stream (skew.py).  Recall within 1e-3 of the f32 oracle on
+    the same dumps; the cache changes where records are read from, never the answers."""
+    base = D.tti_like(12000, seed=511)
+    pool = D.tti_like(800, seed=512)
+    q, warm, _ = D.zipf_query_mix(pool, 2048 + 512, 1.0, split=512, seed=7)
+    dumps, _, _ = O.build(base, 16, 100, 1, 8, seed=52)
+    ref_ids, _, _ = O.OracleIndex(dumps, 200, 16, 1).knn(q, 10, 250, threads=8)
+    gt, _ = D.brute_force_knn(base, q, 10, metric=1)
+    ro = D.recall_at_k(ref_ids, gt, 10)
+    qid = np.arange(q.shape[0], dtype=np.uint32)
+    with shine_amd.Index.from_buffers(dumps, 200, 16, 1, elem=L.ELEM_F16, gpus=[0] * 8, placement="sharded") as plain:
+        plain.set_search_mode(L.MODE_FAST)
+        want = plain.knn(q, 10, 250, query_ids=qid)
+    cache = 0.05 if policy == "warmup" else 0.0
+    with shine_amd.Index.from_buffers(dumps, 200, 16, 1, elem=L.ELEM_F16, gpus=[0] * 8, placement="sharded",
+                                      cache=cache) as idx:
+        idx.set_search_mode(L.MODE_FAST)
+        if policy == "warmup":
+            idx.cache_warmup(warm, 10, 250, query_ids=np.arange(warm.shape[0], dtype=np.uint32))
+            r = idx.knn(q, 10, 250, query_ids=qid)
+            hit = r.stats["node_cache_hits"] / r.stats["node_reads"]
+        else:
+            idx.set_cache_policy(L.CACHE_DYNAMIC, ratio_percent=5.0, seed=3)
+            idx.knn(warm, 10, 250, query_ids=np.arange(warm.shape[0], dtype=np.uint32))  # fills the cache
+            parts = [idx.knn(q[b:b + 512], 10, 250, query_ids=qid[b:b + 512]) for b in range(0, q.shape[0], 512)]
+            r = shine_amd.KnnResult(np.concatenate([p.ids for p in parts]), np.concatenate([p.dists for p in parts]),
+                                    np.concatenate([p.qstats for p in parts]), parts[-1].stats)
+            hit = parts[-1].stats["node_cache_hits"] / parts[-1].stats["node_reads"]
+    assert (r.qstats[:, L.QS_STATUS] == 0).all()
+    np.testing.assert_array_equal(r.ids, want.ids)
+    np.testing.assert_array_equal(r.dists.view(np.uint32), want.dists.view(np.uint32))
+    assert abs(D.recall_at_k(r.ids, gt, 10) - ro) <= 1e-3
+    assert hit > 0.0
+
+
+def test_cfg4_eight_slots_dynamic_cache_exact(cfg4, gpu_available):
+    """cfg 4 under the reference's runtime cache (5 %): exact mode stays the oracle's search call after call while
+    the cache fills and evicts."""
+    with shine_amd.Index.from_buffers(cfg4["dumps"], 96, 16, 0, gpus=[0] * 8, placement="sharded") as idx:
+        idx.set_cache_policy(L.CACHE_DYNAMIC, ratio_percent=5.0, seed=11)
+        parts = [idx.knn(cfg4["q"][b:b + 256], 10, 128, query_ids=np.arange(b, b + 256, dtype=np.uint32))
+                 for b in range(0, 1024, 256)]
+    r = shine_amd.KnnResult(np.concatenate([p.ids for p in parts]), np.concatenate([p.dists for p in parts]),
+                            np.concatenate([p.qstats for p in parts]), {})
+    _check_exact(r, cfg4["ref"])
+    assert parts[-1].stats["node_cache_hits"] > 0

@@ -35,6 +35,9 @@ WORKLOADS = {
     # name: generator, dim, metric, elem, M, efc, ef, batch, shards, placement, gpus
     "cfg3": ("deep_like", 96, 1, 0, 16, 200, 256, 4096, 1, "replica", [0]),
     "cfg5": ("tti_like", 200, 1, 1, 16, 200, 250, 1024, 1, "replica", [0]),
+    # cfg4-shaped (configs[3]: DEEP L2 sharded over 8 GPUs, ef=128): 8 memory-node dumps over 8 GPU slots; on a
+    # one-GPU box the slots repeat device 0 (every stripe its own allocation: the read classes are exact, all local)
+    "cfg4": ("deep_like", 96, 0, 0, 16, 200, 128, 1024, 8, "sharded", [0] * 8),
     "sharded": ("sift_like", 128, 0, 0, 16, 200, 128, 1024, 4, "sharded", [0, 0]),
     "sharded1": ("sift_like", 128, 0, 0, 16, 200, 128, 1024, 4, "sharded", [0]),   # one slot: the VM layout alone
     "replica4": ("sift_like", 128, 0, 0, 16, 200, 128, 1024, 4, "replica", [0]),   # same 4 dumps, plain HBM
@@ -83,13 +86,11 @@ def ground_truth(torch, base_t, q_t, k, metric):
     return np.concatenate(out)
 
 
-def run(name, a):
-    import torch
+def build_dumps(name, gen, n, dim, M, efc, metric, shards, a):
+    """The workload's memory-node dumps under --cache (built once per box, shared by layouts and cache variants)."""
     import shine_amd
     from shine_amd import datasets as D
-    gen, dim, metric, elem, M, efc, ef, batch, shards, placement, gpus = WORKLOADS[name]
-    n = a.n
-    key = hashlib.sha1(f"{n}-{dim}-{M}-{efc}-{shards}-{gen}-v1".encode()).hexdigest()[:12]  # shared by layouts
+    key = hashlib.sha1(f"{n}-{dim}-{M}-{efc}-{shards}-{gen}-v1".encode()).hexdigest()[:12]
     cache = Path(a.cache) / key
     base = getattr(D, gen)(n, seed=1, d=dim)
     paths = [cache / shine_amd.dump_name(M, efc, i, shards) for i in range(shards)]
@@ -102,11 +103,31 @@ def run(name, a):
         for p, d in zip(paths, dumps):
             d.tofile(p)
         del dumps
-    with Heartbeat(f"{name}: opening"):
-        idx = shine_amd.Index.open(paths, dim, M, metric, elem=elem, gpus=gpus, placement=placement)
-    info = idx.info()
-    slots = len(gpus)
+    return base, paths
 
+
+def read_classes(qs_h):
+    """Record reads of a set of queries by class (qstats words, include/shine_gpu.h).  cache_hit_rate has the
+    reference's denominator, every node read (statistics.hh:171-173: on a compute node every read is remote);
+    off_stripe_hit_rate counts only the reads of records another GPU holds."""
+    import shine_amd
+    L = shine_amd._lib
+    reads = np.maximum(qs_h[:, L.QS_DISTCOMPS].astype(np.int64) - 1, 0).sum()
+    hits = qs_h[:, L.QS_CACHED_VEC].astype(np.int64).sum()
+    remote = qs_h[:, L.QS_REMOTE_VEC].astype(np.int64).sum()
+    return {"node_reads": int(reads), "cache_hit_rate": float(hits / max(1, reads)),
+            "off_stripe_share": float((hits + remote) / max(1, reads)),
+            "off_stripe_hit_rate": float(hits / max(1, hits + remote))}
+
+
+def run(name, a):
+    import torch
+    import shine_amd
+    from shine_amd import datasets as D
+    gen, dim, metric, elem, M, efc, ef, batch, shards, placement, gpus = WORKLOADS[name]
+    n = a.n
+    base, paths = build_dumps(name, gen, n, dim, M, efc, metric, shards, a)
+    slots = len(gpus)
     nb = a.nbatches
     if name == "cfg5":  # Zipf-skewed replay of a query pool (skew.py), alpha 1.0
         pool = getattr(D, gen)(50_000, seed=2, d=dim)
@@ -117,7 +138,68 @@ def run(name, a):
     qd = torch.from_numpy(q).cuda()
     with Heartbeat(f"{name}: ground truth"):
         gt = ground_truth(torch, torch.from_numpy(base).cuda(), qd, a.k, metric)
+    del base
     torch.cuda.empty_cache()
+    fracs = [float(x) for x in a.cache_fracs.split(",")] if placement == "sharded" else [0.0]
+    lines = []
+    for frac in fracs:
+        with Heartbeat(f"{name}: opening (cache {frac})"):
+            idx = shine_amd.Index.open(paths, dim, M, metric, elem=elem, gpus=gpus, placement=placement, cache=frac)
+        if frac > 0 and a.cache_warmup:  # compute_node.cc:116-131: a warmup run fills the cache before measuring
+            warm = getattr(D, gen)(a.cache_warmup, seed=5, d=dim)
+            with Heartbeat(f"{name}: cache warmup"):
+                idx.cache_warmup(warm, a.k, ef, query_ids=np.arange(warm.shape[0], dtype=np.uint32))
+        for line in measure(torch, idx, name, a, qd, gt, batch, slots, ef):
+            line["config"].update({"generator": gen, "n": n, "dim": dim, "metric": "IP" if metric else "L2", "M": M,
+                                   "efc": efc, "shards": shards, "placement": placement, "gpu_slots": gpus,
+                                   "cache_fraction": frac, "cache_warmup_queries": a.cache_warmup if frac else 0})
+            line["dtype"] = "f16 records, f32 accumulate" if elem else "f32"
+            log(json.dumps(line))
+            lines.append(line)
+        idx.close()
+    if placement == "sharded" and a.dynamic:
+        lines.append(run_dynamic(name, a, paths, dim, M, metric, elem, gpus, q, gt, batch, ef))
+    return lines
+
+
+def run_dynamic(name, a, paths, dim, M, metric, elem, gpus, q, gt, batch, ef):
+    """The reference's runtime cache (SHINE_CACHE_DYNAMIC: admission, cooling eviction, second chance, applied
+    between calls) over a stream of batches through the host API: hit rate per call from an empty cache."""
+    import shine_amd
+    from shine_amd import datasets as D
+    L = shine_amd._lib
+    idx = shine_amd.Index.open(paths, dim, M, metric, elem=elem, gpus=gpus, placement="sharded")
+    idx.set_search_mode(L.MODE_FAST)
+    idx.set_cache_policy(L.CACHE_DYNAMIC, ratio_percent=a.dynamic, seed=1)
+    rates, res, t_total = [], [], 0.0
+    calls = a.dynamic_calls
+    nb = q.shape[0] // batch
+    for c in range(calls):
+        b = c % nb
+        t0 = time.perf_counter()
+        r = idx.knn(q[b * batch:(b + 1) * batch], a.k, ef,
+                    query_ids=np.arange(c * batch, (c + 1) * batch, dtype=np.uint32))
+        t_total += time.perf_counter() - t0
+        rates.append(r.stats["node_cache_hits"] / max(1, r.stats["node_reads"]))
+        if c < nb:
+            res.append(r.ids)
+    idx.close()
+    line = {"workload": name, "search_mode": "fast", "cache_policy": "dynamic", "cache_ratio_percent": a.dynamic,
+            "calls": calls, "batch": batch, "hit_rate_per_call": rates, "cache_hit_rate_last": rates[-1],
+            "recall_at_10": D.recall_at_k(np.concatenate(res), gt[:len(res) * batch], a.k),
+            "host_api_qps_including_cache_updates": calls * batch / t_total,
+            "note": "hit rate = cached record reads / all record reads (statistics.hh:171-173); the cache is updated "
+                    "between calls on the host (cache.h RecordCache) and the arena on the GPU"}
+    log(json.dumps(line))
+    return line
+
+
+def measure(torch, idx, name, a, qd, gt, batch, slots, ef, nb=None):
+    """Validation pass, then timed batches on the device (slot s answers rows [s*per, (s+1)*per) of each batch)."""
+    import shine_amd
+    from shine_amd import datasets as D
+    info = idx.info()
+    nb = nb or a.nbatches
     ids = torch.empty((nb, batch, a.k), dtype=torch.int32, device="cuda")
     dists = torch.empty((nb, batch, a.k), dtype=torch.float32, device="cuda")
     qs = torch.zeros((nb, batch, shine_amd.QS_WORDS), dtype=torch.int32, device="cuda")
@@ -174,73 +256,87 @@ def run(name, a):
             "visited_p99": float(np.percentile(qs_h[:, 1].astype(np.int64) + qs_h[:, 2], 99)),
             "visited_max": int((qs_h[:, 1].astype(np.int64) + qs_h[:, 2]).max()),
             "queries_with_ties": float((qs_h[:, 5] > 0).mean()) if mode_name == "fast" else None,
-            "dtype": "f16 records, f32 accumulate" if elem else "f32",
-            "config": {"generator": gen, "n": n, "dim": dim, "metric": "IP" if metric else "L2", "M": M, "efc": efc,
-                       "ef": ef, "k": a.k, "batch": batch, "shards": shards, "placement": placement, "gpu_slots": gpus,
-                       "device_bytes_per_gpu": info["device_bytes"], "id_space": info["id_space"]},
+            "reads": read_classes(qs_h),
+            "config": {"ef": ef, "k": a.k, "batch": batch, "device_bytes_per_gpu": info["device_bytes"],
+                       "id_space": info["id_space"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "algorithmic_bytes_per_batch": float(np.mean(byts))},
             "data": "synthetic, random-seeded; index built in-run",
         }
-        log(json.dumps(line))
         lines.append(line)
-    idx.close()
     return lines
 
 
 def run_skew(a):
     """cfg5's skew experiment (scripts/exp_cache_size_and_skew.py: Zipf alpha 0-1.5, cache 5 % of the index) on the
     sharded layout: the TTI-shaped fp16 index as 8 memory-node dumps over 8 GPU slots (repeated device ids on a
-    one-GPU box: every stripe is a separate allocation, so the read classes are exact, but all reads are local HBM),
-    a 5 % cache fraction, and per alpha: a fresh open, the static (in-degree) ranking's hit rate, a cache warmup
-    on the warmup split (shine_cache_warmup), then the measured split's hit rate and remote-read share.  Results
-    must not change with the layout: recall is reported for both."""
+    one-GPU box: every stripe is a separate allocation, so the read classes are exact, but all reads are local HBM).
+    Per alpha: a fresh open with a 5 % cache fraction, the static (in-degree) ranking's hit rate, a cache warmup on
+    the warmup split (shine_cache_warmup, compute_node.cc:116-131), then the measured split's hit rate, read classes,
+    recall, and its device-timed QPS and roofline fraction; then the same stream under the reference's runtime
+    policy (SHINE_CACHE_DYNAMIC) from an empty cache.  Results must not change with the cache: same_ids."""
     import torch
     import shine_amd
     from shine_amd import datasets as D
+    L = shine_amd._lib
     gen, dim, metric, elem, M, efc, ef, shards = "tti_like", 200, 1, 1, 16, 200, 250, 8
     n = a.n
-    key = hashlib.sha1(f"{n}-{dim}-{M}-{efc}-{shards}-{gen}-v1".encode()).hexdigest()[:12]
-    cache = Path(a.cache) / key
-    base = getattr(D, gen)(n, seed=1, d=dim)
-    paths = [cache / shine_amd.dump_name(M, efc, i, shards) for i in range(shards)]
-    if not all(p.exists() for p in paths):
-        with Heartbeat(f"skew: building {n} x {dim}"):
-            dumps, _ = shine_amd.build(base, M, efc, metric, shards, seed=1234, threads=host_threads())
-        cache.mkdir(parents=True, exist_ok=True)
-        for p, d in zip(paths, dumps):
-            d.tofile(p)
-        del dumps
+    base, paths = build_dumps("skew", gen, n, dim, M, efc, metric, shards, a)
     pool = getattr(D, gen)(20_000, seed=2, d=dim)
     base_t = torch.from_numpy(base).cuda()
+    del base
     lines = []
+    batch = 1024
     for alpha in [float(x) for x in a.alphas.split(",")]:
-        q, warm, _ = D.zipf_query_mix(pool, 3 * 1024, alpha, split=1024, seed=9)
+        q, warm, _ = D.zipf_query_mix(pool, 3 * batch, alpha, split=batch, seed=9)
         q, warm = np.ascontiguousarray(q), np.ascontiguousarray(warm)
+        qd = torch.from_numpy(q).cuda()
         with Heartbeat("skew: ground truth"):
-            gt = ground_truth(torch, base_t, torch.from_numpy(q).cuda(), a.k, metric)
+            gt = ground_truth(torch, base_t, qd, a.k, metric)
         qid = np.arange(q.shape[0], dtype=np.uint32)
         with Heartbeat("skew: opening"):
             idx = shine_amd.Index.open(paths, dim, M, metric, elem=elem, gpus=[0] * shards, placement="sharded",
                                        cache=0.05)
-        idx.set_search_mode(shine_amd.MODE_FAST)
+        idx.set_search_mode(L.MODE_FAST)
         r0 = idx.knn(q, a.k, ef, query_ids=qid)
         with Heartbeat("skew: warmup"):
             idx.cache_warmup(warm, a.k, ef, query_ids=np.arange(warm.shape[0], dtype=np.uint32))
         r1 = idx.knn(q, a.k, ef, query_ids=qid)
+        timed = measure(torch, idx, "cfg5", argparse.Namespace(**{**vars(a), "modes": "fast", "ef": ""}), qd, gt,
+                        batch, shards, ef, nb=q.shape[0] // batch)[0]
         idx.close()
 
-        def rate(r):
+        def rate(r):  # off-stripe reads only
             h, m = r.stats["cache_hits"], r.stats["cache_misses"]
             return h / max(1, h + m)
 
+        dyn = {}
+        if a.dynamic:
+            with shine_amd.Index.open(paths, dim, M, metric, elem=elem, gpus=[0] * shards,
+                                      placement="sharded") as di:
+                di.set_search_mode(L.MODE_FAST)
+                di.set_cache_policy(L.CACHE_DYNAMIC, ratio_percent=a.dynamic, seed=1)
+                rates = []
+                stream = [warm] + [q[b * batch:(b + 1) * batch] for b in range(q.shape[0] // batch)]
+                for c in range(a.dynamic_calls):
+                    qq = stream[c % len(stream)]
+                    r = di.knn(qq, a.k, ef, query_ids=np.arange(c * batch, c * batch + qq.shape[0], dtype=np.uint32))
+                    rates.append(r.stats["node_cache_hits"] / max(1, r.stats["node_reads"]))
+            dyn = {"cache_ratio_percent": a.dynamic, "calls": a.dynamic_calls, "hit_rate_per_call": rates}
+
         line = {"workload": "cfg5-skew", "alpha": alpha, "cache_fraction": 0.05, "gpu_slots": shards,
-                "hit_rate_static": rate(r0), "hit_rate_warmed": rate(r1),
+                "off_stripe_hit_rate_static": rate(r0), "off_stripe_hit_rate_warmed": rate(r1),
+                "cache_hit_rate_static": r0.stats["node_cache_hits"] / max(1, r0.stats["node_reads"]),
+                "cache_hit_rate_warmed": r1.stats["node_cache_hits"] / max(1, r1.stats["node_reads"]),
                 "remote_share_static": r0.stats["remote_reads_in_bytes"] / max(1, r0.stats["algorithmic_bytes"]),
                 "remote_share_warmed": r1.stats["remote_reads_in_bytes"] / max(1, r1.stats["algorithmic_bytes"]),
                 "recall_at_10": D.recall_at_k(r1.ids, gt, a.k), "same_ids": bool((r0.ids == r1.ids).all()),
+                "value": timed["value"], "unit": "queries/s", "ms_per_batch": timed["ms_per_batch"],
+                "recall_at_10_device": timed["recall_at_10"], "reads_device": timed["reads"],
+                "roofline": timed["roofline"], "dynamic_cache": dyn,
                 "config": {"generator": gen, "n": n, "dim": dim, "metric": "IP", "elem": "f16", "M": M, "efc": efc,
-                           "ef": ef, "queries": int(q.shape[0]), "warmup_queries": int(warm.shape[0])},
+                           "ef": ef, "k": a.k, "batch": batch, "queries": int(q.shape[0]),
+                           "warmup_queries": int(warm.shape[0]), "batches_in_flight": a.inflight},
                 "note": "one physical GPU: the read classes (local / cached / remote) are exact, the xGMI rate is not "
                         "measured"}
         log(json.dumps(line))
@@ -262,6 +358,12 @@ def main():
     p.add_argument("--cache", default=os.environ.get("SHINE_CFG_CACHE", "/tmp/shine_cfg"))
     p.add_argument("--out", default=str(ROOT / "gpurun_out" / "config_lines.jsonl"))
     p.add_argument("--alphas", default="0,0.5,1.0,1.5", help="cfg5skew: Zipf exponents")
+    p.add_argument("--cache-fracs", default="0,0.05", help="sharded workloads: cache fractions measured")
+    p.add_argument("--cache-warmup", type=int, default=1024,
+                   help="queries of the warmup run that ranks a non-empty cache (0: static in-degree ranking)")
+    p.add_argument("--dynamic", type=float, default=5.0,
+                   help="sharded workloads: also stream batches under SHINE_CACHE_DYNAMIC at this ratio % (0: off)")
+    p.add_argument("--dynamic-calls", type=int, default=12)
     a = p.parse_args()
     import torch
     torch.cuda.set_device(0)

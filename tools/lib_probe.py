@@ -5,7 +5,7 @@ two builds in one process (tools/ab_lib.py) share the process's hardware queues,
 second side's streams collide on them (it measured up to 28 % slower whichever build it was, profiles/r02/
 ab_order_bias.txt).
 
-Usage: SHINE_GPU_LIB=_abl/libX.so python tools/lib_probe.py --runs fast:48,fast:128,exact:128 --tag X
+Usage: SHINE_GPU_LIB=_abl/libX.so python tools/lib_probe.py --runs fast:48,fast:128,exact:128,fast:128:u8 --tag X
 """
 from __future__ import annotations
 
@@ -45,21 +45,31 @@ def main():
                                threads=host_threads())[0]
 
     prepare_dumps(paths, 0, None, build)
-    idx = shine_amd.Index.open(paths, 128, 16, shine_amd.METRIC_L2, gpus=[0])
+    opened = {}
+
+    def index(rows):  # f32 rows (the bench's `value`) or u8 rows (lossless for SIFT-shaped records)
+        if rows not in opened:
+            elem = shine_amd.ELEM_U8 if rows == "u8" else shine_amd.ELEM_F32
+            opened[rows] = shine_amd.Index.open(paths, 128, 16, shine_amd.METRIC_L2, elem=elem, gpus=[0])
+        return opened[rows]
     q = torch.from_numpy(D.sift_like(B * nb, seed=2, d=128)).cuda()
     ids = torch.empty((nb, B, 10), dtype=torch.int32, device="cuda")
     qs = torch.empty((nb, B, shine_amd.QS_WORDS), dtype=torch.int32, device="cuda")
     streams = [torch.cuda.Stream() for _ in range(S)]
 
     def run(steps, ef):
+        idx = cur[0]
         for i in range(steps):
             b = i % nb
             idx.knn_device(q[b * B:(b + 1) * B].data_ptr(), B, 10, ef, ids[b].data_ptr(), None, qs[b].data_ptr(),
                            stream=streams[i % S].cuda_stream)
 
+    cur = [None]
     for spec in a.runs.split(","):
-        mode, ef = spec.split(":")
+        mode, ef, *rows = spec.split(":")
         ef = int(ef)
+        rows = rows[0] if rows else "f32"
+        idx = cur[0] = index(rows)
         idx.set_search_mode(shine_amd.MODE_FAST if mode == "fast" else shine_amd.MODE_EXACT)
         run(2 * nb, ef)
         torch.cuda.synchronize()
@@ -69,8 +79,9 @@ def main():
         run(a.steps, ef)
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
-        print(json.dumps({"tag": a.tag, "mode": mode, "ef": ef, "qps": a.steps * B / el}), flush=True)
-    idx.close()
+        print(json.dumps({"tag": a.tag, "mode": mode, "ef": ef, "rows": rows, "qps": a.steps * B / el}), flush=True)
+    for idx in opened.values():
+        idx.close()
 
 
 if __name__ == "__main__":

@@ -27,7 +27,8 @@ if not path.exists():
     path.parent.mkdir(parents=True, exist_ok=True)
     dumps[0].tofile(path)
 q = D.sift_like(1024, seed=2)
-idx = shine_amd.Index.open([path], 128, 16, 0, gpus=[0])
+elem = shine_amd.ELEM_U8 if os.environ.get("ROWS") == "u8" else shine_amd.ELEM_F32  # ROWS=u8: byte rows
+idx = shine_amd.Index.open([path], 128, 16, 0, elem=elem, gpus=[0])
 if os.environ.get("MODE", "exact") == "fast":
     idx.set_search_mode(shine_amd.MODE_FAST)
 r = idx.knn(q, 10, ef)

@@ -19,7 +19,8 @@ if not path.exists():
     if os.environ.get("BUILD_ONLY"):
         sys.exit(0)
 q = D.sift_like(int(os.environ.get("NQ", "1024")), seed=2)
-idx = shine_amd.Index.open([path], 128, 16, 0, gpus=[0])
+elem = shine_amd.ELEM_U8 if os.environ.get("ROWS") == "u8" else shine_amd.ELEM_F32  # ROWS=u8: byte rows
+idx = shine_amd.Index.open([path], 128, 16, 0, elem=elem, gpus=[0])
 idx.set_search_mode(shine_amd.MODE_FAST if os.environ.get("MODE", "fast") == "fast" else shine_amd.MODE_EXACT)
 for _ in range(int(os.environ.get("REPS", "2"))):
     r = idx.knn(q, 10, int(os.environ.get("EF", "128")))
