@@ -704,8 +704,9 @@ struct LaunchShape {
   uint32_t vis16, vis_bits;  // fast kernel: u16 quotient visited entries over a vis_bits-bit id space
 };
 
-// spilled visited tables a fast pass may hold at once (SearchArgs::spill_flags)
+// spilled visited tables a main pass (fast or exact) may hold at once (SearchArgs::spill_flags)
 constexpr uint32_t kSpillSlots = 64;
+bool spill_enabled();
 
 // the inverse of an odd multiplier mod 2^32 (Newton: each step doubles the correct low bits)
 uint32_t inverse_odd(uint32_t m) {
@@ -731,6 +732,10 @@ int64_t env_int(const char* name, int64_t dflt) {
   return e ? std::atoll(e) : dflt;
 }
 
+// the main passes continue a query whose visited table overflows in an HBM bitmap (SHINE_DEBUG_NO_SPILL=1: hand it
+// to the light pass instead, the round-2 behaviour)
+bool spill_enabled() { return env_int("SHINE_DEBUG_NO_SPILL", 0) == 0; }
+
 // Fast mode: the sorted list lives in VGPRs, LDS holds only the visited table.  The table holds between pow2(40·ef)
 // and pow2(48·ef) entries (a query visits ~5-20·ef nodes; one that fills 7/8 of it goes to the light pass).  The
 // shape aims at the wavefronts of two batches being resident together (the next batch in flight runs beside this
@@ -753,14 +758,19 @@ uint32_t learned_table(const Scratch& S) {
 }
 
 LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds_per_cu, uint64_t id_space,
-                            uint32_t learned = 0, bool grow = false) {
+                            uint32_t learned = 0, bool grow = false, bool byte_rows = false) {
   LaunchShape sh{};
   const uint32_t want = std::max<uint32_t>(1, std::min<uint32_t>(16, (nq + cus - 1) / cus));
-  // tuning hooks (measurement): waves per CU the tables are sized for, in batches of `want`; table floor per ef
-  const uint32_t target = std::min<uint32_t>(16, static_cast<uint32_t>(env_int("SHINE_FAST_TARGET_BATCHES", 2)) * want);
-  // a table below pow2(40·ef) entries sends a measurable share of queries to the light pass (ef = 128 on the bench's
-  // index: 4,096 entries gave 1.1 M QPS against 4.2 M for 8,192), whatever residency it buys
-  const uint32_t per_ef = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_FAST_TABLE_PER_EF", 40)));
+  // Waves per CU the tables are sized for, in batches of `want`, and the table floor per ef.  f32 rows: two batches,
+  // pow2(40·ef) entries.  Byte rows move a quarter of the bytes per distance, so the kernel is latency-bound there and
+  // residency pays: four batches (16 wavefronts per CU at batch 1,024) and pow2(24·ef) entries, the few queries that
+  // outgrow them spilling in place (SearchArgs::spill_flags) — u8 rows at ef = 128: 8.18 M against 7.74 M QPS, f32
+  // rows 6.34 M against 6.69 M (profiles/r03/lib_probe_v16_tables.jsonl).  The environment overrides both (tuning).
+  const uint32_t target = std::min<uint32_t>(
+      16, static_cast<uint32_t>(env_int("SHINE_FAST_TARGET_BATCHES", byte_rows ? 4 : 2)) * want);
+  // with f32 rows a table below pow2(40·ef) entries costs more than its residency buys
+  const uint32_t per_ef =
+      static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_FAST_TABLE_PER_EF", byte_rows ? 24 : 40)));
   uint32_t lo = std::min<uint32_t>(16384, std::max<uint32_t>(2048, pow2_at_least(per_ef * ef)));
   // what the previous call's queries needed: a smaller table, or a larger one once the fixed size overflowed
   if (learned && (learned < lo || grow)) lo = learned;
@@ -825,12 +835,17 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
   uint64_t budget = lds;
   if (pass == PASS_LDS) {
     // u16 quotient entries (VisitedLds<1>) when the id space fits them and they let more wavefronts share a CU with
-    // next_candidates still >= 5·ef entries (u32: 4·ef)
-    sh.vis_cap = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(48 * ef)));
+    // next_candidates still >= 5·ef entries (u32: 4·ef).  With the in-place spill (a query that outgrows its table
+    // goes on in an HBM bitmap) tables of pow2(24·ef) entries, sized for the wavefronts of four batches in flight
+    // (4,096 entries and up to 11 wavefronts per CU at ef = 128 instead of 8,192 and 7); without it pow2(48·ef) and
+    // two batches, as a query that overflows is re-run from scratch by the light pass.  Tuning hooks: the two env knobs.
+    const bool spill = spill_enabled();
+    const uint32_t per_ef = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_EXACT_TABLE_PER_EF", spill ? 24 : 48)));
+    const uint32_t batches = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_EXACT_TARGET_BATCHES", spill ? 4 : 2)));
+    sh.vis_cap = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(per_ef * ef)));
     if (learned && (learned < sh.vis_cap || (handed != 0xFFFFFFFFu && handed > 0))) sh.vis_cap = learned;  // as fast
     sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
-    // aim at the wavefronts of two batches in flight being resident together, as pick_fast_shape does
-    const uint32_t want = std::min<uint32_t>(2 * ((nq + cus - 1) / cus), 16u);
+    const uint32_t want = std::min<uint32_t>(batches * ((nq + cus - 1) / cus), 16u);
     auto waves = [&](uint64_t need) {
       return std::max<uint32_t>(1, std::min<uint32_t>(want, static_cast<uint32_t>(lds / need)));
     };
@@ -925,7 +940,8 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   for (int i = 0; i < n_pass; ++i) {
     const int pass = chain[i];
     const LaunchShape sh =
-        pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu, h->id_space, learned, handed > 0)
+        pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu, h->id_space, learned, handed > 0,
+                                          elem_is_byte(h->elem))
                           : pick_shape(h, R, nq, ef, pass, handed, learned);
     if (i == 0) {
       S.last_table = sh.vis_cap;
@@ -939,14 +955,14 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     a.g = dev_graph(h, R);
     if (!a.g.vec || !a.g.adj0 || !a.g.uid || !a.g.up_base)
       return set_error(SHINE_ERR_HIP, "search launch: an index array is missing on this GPU slot");
-    if (pass == PASS_LIGHT || pass == PASS_GLOBAL || pass == PASS_FAST) {
-      // the fallback passes' bitmaps; the fast pass borrows them for its spilled tables (it runs first on the stream
+    if (pass == PASS_LIGHT || pass == PASS_GLOBAL || pass == PASS_FAST || pass == PASS_LDS) {
+      // the fallback passes' bitmaps; the main pass borrows them for its spilled tables (it runs first on the stream
       // and hands every one back zeroed)
       const uint32_t need = std::max<uint32_t>({pick_shape(h, R, nq, ef, PASS_LIGHT).grid,
                                                 pick_shape(h, R, nq, ef, PASS_GLOBAL).grid, kSpillSlots});
       if (int rc = ensure_bitmaps(h, S, s, need)) return rc;
     }
-    if (pass == PASS_FAST && !env_int("SHINE_DEBUG_NO_SPILL", 0)) {
+    if ((pass == PASS_FAST || pass == PASS_LDS) && spill_enabled()) {
       if (!S.spill_flags.p) {
         if (int rc = S.spill_flags.grow(kSpillSlots)) return rc;
         HIP_TRY(hipMemsetAsync(S.spill_flags.p, 0, kSpillSlots * sizeof(uint32_t), s));

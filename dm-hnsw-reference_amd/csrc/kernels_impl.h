@@ -38,6 +38,9 @@
 
 #include <type_traits>
 
+// v_writelane_b32 (this clang exposes readlane as a builtin but not writelane): `val` into lane `lane` of `old`
+extern "C" __device__ int shine_writelane_i32(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
 namespace shine {
 namespace {
 
@@ -1032,6 +1035,22 @@ __device__ __forceinline__ void finish_call(const SearchArgs& A, int lane) {
   for (int i = 0; i < 8; ++i) __atomic_store_n(&c[i], 0u, __ATOMIC_RELAXED);
 }
 
+// One of the stream's spill bitmaps for this wavefront (SearchArgs::spill_flags), or -1 when all are held.
+__device__ __forceinline__ int claim_spill_bitmap(const SearchArgs& A, int lane) {
+  if (A.spill_slots == 0) return -1;
+  u32 got = INV;
+  if (lane == 0) {
+    const u32 n = A.spill_slots;
+    for (u32 i = 0, j = blockIdx.x % n; i < n; ++i, j = j + 1 == n ? 0u : j + 1)
+      if (atomicCAS(&A.spill_flags[j], 0u, 1u) == 0u) {
+        got = j;
+        break;
+      }
+  }
+  got = bcast(got);
+  return got == INV ? -1 : static_cast<int>(got);
+}
+
 template <int D, int METRIC, typename E, int VIS, int ACCT, int VT = 0, bool PROF = false>
 __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
   PhaseClock<PROF> clk;
@@ -1074,6 +1093,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
 
     u32 st_dist = 0, st_vup = 0, st_vl0 = 0, st_lup = 0, st_ll0 = 0, st_maxnext = 0, status = 0;
     ReadCount rc;
+    int sslot = -1;  // VIS == 0: the spill bitmap this query holds (wave-uniform), -1 = the LDS table
 
     // ---- entry point + greedy descent (hnsw.hh:256-287) ---------------------------------------------------
     PHASE(1)
@@ -1141,11 +1161,32 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         }
         bool fresh = false, vovf = false;
         if (cand) {  // visited.contains / insert (:441-443)
-          if (VIS == 0) {
+          if (VIS == 0 && sslot < 0) {
             fresh = vt.test_and_set(e, vovf);
-          } else {
+          } else {  // the HBM bitmap: the fallback passes', or this query's spilled table
+            u32* __restrict__ bm = VIS == 0 ? A.visited + static_cast<u64>(sslot) * A.words_per_slot : vis;
             const u32 bit = 1u << (e & 31);
-            fresh = (atomicOr(&vis[e >> 5], bit) & bit) == 0;
+            fresh = (atomicOr(&bm[e >> 5], bit) & bit) == 0;
+          }
+        }
+        if constexpr (VIS == 0) {
+          // In-place spill (as the fast kernel): the table is too full, or an id landed too far from its home
+          // bucket — the table moves to an HBM bitmap and the query goes on there instead of being handed to the
+          // light pass and re-run from scratch.  An insert that overflowed is tested against the bitmap.
+          if (sslot < 0 && (__ballot(vovf) || nvis + __popcll(__ballot(fresh)) > A.vis_limit)) {
+            sslot = claim_spill_bitmap(A, lane);
+            if (sslot < 0) {
+              status = ST_OVERFLOW;
+              break;
+            }
+            u32* sb = A.visited + static_cast<u64>(sslot) * A.words_per_slot;
+            wave_sync();
+            vt.spill(sb, A, lane);
+            EVENT(3)
+            if (vovf) {
+              const u32 bit = 1u << (e & 31);
+              fresh = (atomicOr(&sb[e >> 5], bit) & bit) == 0u;
+            }
           }
         }
         const u64 fm = __ballot(fresh);
@@ -1164,10 +1205,6 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         if (VIS >= 1 && logpos > A.log_cap) log_overflow = true;
         st_vl0 += nf;
         st_dist += nf;
-        if (VIS == 0 && nvis > A.vis_limit) { status = ST_OVERFLOW; break; }
-        if constexpr (VIS == 0 && VT == 1) {
-          if (__ballot(vovf)) { status = ST_OVERFLOW; break; }  // an id too far from its home slot
-        }
         if (nf == 0) continue;
         PHASE(4)
         wave_sync();
@@ -1281,6 +1318,14 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
       write_read_counts(qs, rc);
     }
 
+    if (VIS == 0 && sslot >= 0) {  // hand the spill bitmap back all zero (as the fast kernel, which explains why
+                                   // every lane stores the flag)
+      u32* sb = A.visited + static_cast<u64>(sslot) * A.words_per_slot;
+      for (u64 w = lane; w < A.words_per_slot; w += 64) sb[w] = 0u;
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      __threadfence();
+      __hip_atomic_store(&A.spill_flags[sslot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (VIS >= 1) {  // visited_nodes.clear() (:475): clear exactly the words this query touched
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (!log_overflow) {
@@ -1367,21 +1412,6 @@ __device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restri
   }
 }
 
-// One of the stream's spill bitmaps for this wavefront (SearchArgs::spill_flags), or -1 when all are held.
-__device__ __forceinline__ int claim_spill_bitmap(const SearchArgs& A, int lane) {
-  if (A.spill_slots == 0) return -1;
-  u32 got = INV;
-  if (lane == 0) {
-    const u32 n = A.spill_slots;
-    for (u32 i = 0, j = blockIdx.x % n; i < n; ++i, j = j + 1 == n ? 0u : j + 1)
-      if (atomicCAS(&A.spill_flags[j], 0u, 1u) == 0u) {
-        got = j;
-        break;
-      }
-  }
-  got = bcast(got);
-  return got == INV ? -1 : static_cast<int>(got);
-}
 
 // Waves per SIMD the register allocation must allow (build-time tuning: 4 caps a wave at 128 VGPRs, so 16 wavefronts
 // fit a CU when their LDS tables do).
@@ -1603,21 +1633,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHINE_FAST_M
         for (int r = 0; r < R; ++r) shift[r] = 0;
         int frank = 0;  // fresh lane: accepted keys ordered before it
         int fbase = 0;  // fresh lane: list entries below it
+        // The merged order of the fresh keys as one 64-bit key per lane: the distance's order-preserving image (-0
+        // made +0 first, so equal distances compare equal), then later list slots first.  One 64-bit compare per
+        // accepted key instead of three float / slot compares and two mask operations.
+        const u32 ohi = sortable(my_d + 0.0f), olo = 63u - my_slot;
+        const u64 okey = (static_cast<u64>(ohi) << 32) | olo;
         u64 todo = acc;
         while (todo) {
           const int i = static_cast<int>(__builtin_ctzll(todo));
-          todo &= todo - 1;
+          todo ^= 1ull << i;
           const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_d), i));
-          int below = 0;
+          const u64 oi = (static_cast<u64>(static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(ohi), i))) << 32) |
+                         static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(olo), i));
+          // one compare per register serves both counts: the entries at or above d (shifted by this key) and, by
+          // complement, the entries below it (neither d nor the list holds NaN)
+          int at_or_above = 0;
 #pragma unroll
           for (int r = 0; r < R; ++r) {
-            shift[r] += d <= ck[r] ? 1 : 0;
-            below += __popcll(__ballot(ck[r] < d));
+            const bool le = d <= ck[r];
+            shift[r] += le ? 1 : 0;
+            at_or_above += __popcll(__ballot(le));
           }
-          // non-short-circuit: three compares and two mask ops, no exec-mask branches inside the key loop
-          const bool before = (d < my_d) | ((d == my_d) & (slot_of(i) > static_cast<int>(my_slot)));
-          frank += before ? 1 : 0;
-          fbase = lane == i ? below : fbase;
+          frank += oi < okey ? 1 : 0;
+          fbase = shine_writelane_i32(64 * R - at_or_above, i, fbase);
         }
         const int total = cs + __popcll(acc);
         const int hi = total < ef + 1 ? total : ef + 1;  // merged positions written: 0 .. hi-1

@@ -238,9 +238,10 @@ def test_device_heaps_match_libstdcxx(is_max, ties, general, gpu_available):
         np.testing.assert_array_equal(od[:n], ref_d)
 
 
-@pytest.mark.parametrize("env", [{"SHINE_DEBUG_VISCAP": "1024"}, {"SHINE_DEBUG_START_MODE": "1"},
+@pytest.mark.parametrize("env", [{"SHINE_DEBUG_VISCAP": "1024", "SHINE_DEBUG_NO_SPILL": "1"},
+                                 {"SHINE_DEBUG_START_MODE": "1"},
                                  {"SHINE_DEBUG_START_MODE": "2"}, {"SHINE_DEBUG_START_MODE": "3"},
-                                 {"SHINE_DEBUG_VISCAP": "1024", "SHINE_DEBUG_LIGHT_CAP": "16"}])
+                                 {"SHINE_DEBUG_VISCAP": "1024", "SHINE_DEBUG_LIGHT_CAP": "16", "SHINE_DEBUG_NO_SPILL": "1"}])
 def test_visited_modes(env, gpu_available, monkeypatch):
     """Every pass of the chain alone or handed overflowing queries: the whole-CU LDS pass (start mode 1), the
     light pass (HBM visited bitmap, 16 KiB LDS heaps; start mode 2), the global-heap pass (bitmap and both heaps in
@@ -257,6 +258,30 @@ def test_visited_modes(env, gpu_available, monkeypatch):
             assert r.stats["overflow_retries"] > 0
         _check_same(r, *ref)
         _check_same(idx.knn(q, 10, 200), *ref)
+
+
+@pytest.mark.parametrize("vis16", ["0", "1"])
+@pytest.mark.parametrize("gen,dim,metric,ef", [(D.sift_like, 128, 0, 128), (D.deep_like, 96, 1, 256)])
+def test_exact_mode_spills_in_place(gen, dim, metric, ef, vis16, gpu_available, monkeypatch):
+    """Exact mode with a 256-entry visited table: every query outgrows it, spills it into an HBM bitmap mid-search
+    and goes on there (the in-place spill the fast kernel has); more queries than the 64 bitmaps spill at once, so
+    the rest are handed to the light pass.  Both paths: ids, distances and every counter identical to the oracle."""
+    base = gen(6000, seed=311, d=dim)
+    q = gen(300, seed=312, d=dim)
+    dumps, _, _ = O.build(base, 16, 100, metric, 1, seed=6)
+    ref = O.OracleIndex(dumps, dim, 16, metric).knn(q, 10, ef, threads=8)
+    monkeypatch.setenv("SHINE_DEBUG_VISCAP", "256")
+    monkeypatch.setenv("SHINE_DEBUG_VIS16", vis16)
+    with shine_amd.Index.from_buffers(dumps, dim, 16, metric, gpus=[0]) as idx:
+        r = idx.knn(q, 10, ef)
+        assert r.stats["overflow_retries"] < q.shape[0]  # some queries went on in place instead of being re-run
+        _check_same(r, *ref)
+        for i in range(0, 32, 8):  # a few queries at a time: every spill finds a free bitmap, none is handed on
+            one = idx.knn(q[i:i + 8], 10, ef)
+            assert one.stats["overflow_retries"] == 0
+            np.testing.assert_array_equal(one.ids, ref[0][i:i + 8])
+            np.testing.assert_array_equal(one.dists.view(np.uint32), ref[1][i:i + 8].view(np.uint32))
+            np.testing.assert_array_equal(one.qstats[:, :5], ref[2][i:i + 8, :5])
 
 
 def test_global_heap_capacity_overflow_is_reported(gpu_available, monkeypatch):
