@@ -143,6 +143,7 @@ struct Scratch {
   bool last_learned = false;
   uint32_t table_floor = 0;      // a learned table that overflowed is never learned again below twice its size
   uint32_t last_ef = 0;          // ef of the last call: what it visited says nothing about another ef
+  uint32_t last_nq = 0;          // queries of the last call (seen[5] / last_nq: the mean a query marked visited)
   void release() {
     for (auto* b : {&visited, &vlog, &counter, &ovf, &qs, &spill_flags}) b->release();
     heaps.release();
@@ -634,7 +635,7 @@ int make_index(HostGraph G, int elem, const int* gpu_ids, uint32_t n_gpus, int p
     if (int rc = upload(R.up_base, upb_d->data(), upb_d->size(), R.stream)) return rc;
     if (int rc = upload(R.adjU, adjU_d->data(), adjU_d->size(), R.stream)) return rc;
     if (int rc = upload(R.inv_uid, inv.data(), inv.size(), R.stream)) return rc;
-    if (int rc = R.main.counter.grow(8)) return rc;
+    if (int rc = R.main.counter.grow(kCallWords)) return rc;
     HIP_TRY(hipStreamSynchronize(R.stream));
   }
   const uint64_t replicated = 4 * (uid_d->size() + upb_d->size() + adjU_d->size() + inv.size());
@@ -755,6 +756,18 @@ uint32_t learned_table(const Scratch& S) {
   const uint32_t vmax = S.seen.p[4];
   if (vmax == 0) return 0;
   return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, pow2_at_least(vmax + vmax / 2 + vmax / 8)}));
+}
+
+// With the in-place spill a table need only hold the typical query of the stream: pow2(1.25 x the previous call's
+// mean visited count + 64) — a query beyond it spills and goes on in an HBM bitmap.  The mean, not the maximum: on the
+// DEEP-shaped 10M index at ef = 256 a query visits 2.9K nodes on average but up to 7K (profiles/r02/
+// config_lines_cfg3_10m_final.jsonl), and a table sized for the maximum holds half the wavefronts per CU.  Never below
+// the floor a call that exhausted the spill bitmaps set.
+uint32_t learned_mean_table(const Scratch& S) {
+  if (!S.seen.p || !S.seen.p[3] || !S.last_nq || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
+  const uint32_t mean = S.seen.p[5] / S.last_nq;
+  if (mean == 0) return 0;
+  return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, pow2_at_least(mean + mean / 4 + 64)}));
 }
 
 LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds_per_cu, uint64_t id_space,
@@ -911,7 +924,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
                    uint32_t* d_ids, float* d_dists, uint32_t* d_qs, hipStream_t s, bool timed,
                    uint32_t* d_access = nullptr) {
   Scratch& S = scratch_for(R, s);
-  if (int rc = S.counter.grow(8)) return rc;
+  if (int rc = S.counter.grow(kCallWords)) return rc;
   if (S.ovf.n < 3ull * nq) HIP_TRY(hipStreamSynchronize(s));  // a reallocation must not pull the list from under
   if (int rc = S.ovf.grow(3ull * nq)) return rc;                // an earlier call on this stream
   if (!S.seen_dev) {
@@ -921,7 +934,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     S.seen_dev = static_cast<uint32_t*>(dp);
   }
   // the counter words start at zero: left so by the last call's last pass, else (first call, a failed call) set here
-  if (!S.counters_zero) HIP_TRY(hipMemsetAsync(S.counter.p, 0, 8 * sizeof(uint32_t), s));
+  if (!S.counters_zero) HIP_TRY(hipMemsetAsync(S.counter.p, 0, kCallWords * sizeof(uint32_t), s));
   S.counters_zero = false;
   if (timed) HIP_TRY(hipEventRecord(R.ev0, s));
   const int start = static_cast<int>(env_int("SHINE_DEBUG_START_MODE", 0));  // test hook: the fallback passes alone
@@ -930,8 +943,9 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   const uint32_t handed = S.seen.p[3] ? S.seen.p[0] : 0;  // [3] = 1 once a call has written the counts
   if (handed && S.last_learned) S.table_floor = std::max(S.table_floor, 2 * S.last_table);  // it was too small
   if (ef != S.last_ef) S.table_floor = 0;
-  const uint32_t learned = ef == S.last_ef ? learned_table(S) : 0;
+  const uint32_t learned = ef != S.last_ef ? 0 : spill_enabled() ? learned_mean_table(S) : learned_table(S);
   S.last_ef = ef;
+  S.last_nq = nq;
   int chain[3], n_pass = 0;
   if (start <= 0) chain[n_pass++] = fast_kernel ? PASS_FAST : PASS_LDS;
   else if (start == 1) chain[n_pass++] = PASS_WHOLE_CU;
@@ -994,6 +1008,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     a.log_cap = kLogCap;
     a.counter = S.counter.p + i;
     a.vis_max = S.counter.p + 3;
+    a.vis_sum = S.counter.p + 8;
     a.fast = pass == PASS_FAST ? 1u : 0u;
     a.vis16 = sh.vis16;
     a.vis_bits = sh.vis_bits;

@@ -43,6 +43,9 @@ struct DevGraph {
   unsigned long long dyn_seed;
 };
 
+// Counter words of one call on a stream (SearchArgs::call_counters).
+constexpr uint32_t kCallWords = 9;
+
 // Per-query counter words (u32) written by the search kernels; include/shine_gpu.h SHINE_QS_*.
 constexpr uint32_t kQsWords = 12;
 
@@ -68,12 +71,14 @@ struct SearchArgs {
   unsigned long long* heaps; // global-heap pass: per-slot top / next heaps in HBM, heap_stride entries each
   uint64_t heap_stride;
   uint32_t* access;          // cache warmup (nullable): per device id, reads of the record (vector or list)
-  uint32_t* call_counters;   // last pass of a call (nullable): the call's 8 counter words; the last workgroup to
-  uint32_t* host_counts;     // finish copies words 4..6 to host_counts[0..2] (host memory), sets host_counts[3] = 1,
-                             // copies word 3 to host_counts[4] and zeroes the 8 words for the next call on the stream
-                             // (word 7 counts finished groups)
+  uint32_t* call_counters;   // last pass of a call (nullable): the call's kCallWords counter words; the last workgroup
+  uint32_t* host_counts;     // to finish copies words 4..6 to host_counts[0..2] (host memory), sets host_counts[3] = 1,
+                             // copies words 3 and 8 to host_counts[4] and [5] and zeroes the words for the next call
+                             // on the stream (word 7 counts finished groups)
   uint32_t* vis_max;         // every pass (nullable): the call's counter word 3, the most nodes any query marked
                              // visited (atomicMax per query) — sizes the next call's visited tables
+  uint32_t* vis_sum;         // every pass (nullable): the call's counter word 8, the nodes its queries marked visited
+                             // (atomicAdd per query; copied to host_counts[5]) — the mean sizes spilling tables
   unsigned long long* prof; // diagnostics (nullable): per-phase shader-clock totals, PROF kernel variant only
   uint32_t fast;            // 1: sorted-list kernel (SHINE_MODE_FAST; ef <= kFastMaxEf, vis_cap > 0)
   uint32_t sort_out;        // heap kernel writes ascending order (fast-mode fixup passes)

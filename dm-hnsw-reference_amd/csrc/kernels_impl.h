@@ -1030,9 +1030,10 @@ __device__ __forceinline__ void finish_call(const SearchArgs& A, int lane) {
   host[1] = h1;
   host[2] = h2;
   host[4] = __atomic_load_n(&c[3], __ATOMIC_RELAXED);
+  host[5] = __atomic_load_n(&c[8], __ATOMIC_RELAXED);
   host[3] = 1u;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) __atomic_store_n(&c[i], 0u, __ATOMIC_RELAXED);
+  for (int i = 0; i < static_cast<int>(kCallWords); ++i) __atomic_store_n(&c[i], 0u, __ATOMIC_RELAXED);
 }
 
 // One of the stream's spill bitmaps for this wavefront (SearchArgs::spill_flags), or -1 when all are held.
@@ -1304,7 +1305,8 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
       if (A.out_dists) A.out_dists[obase + slot] = d;
     }
     if (status == ST_OVERFLOW && A.out_list && lane == 0) A.out_list[atomicAdd(A.out_count, 1u)] = qi;
-    if (A.vis_max && lane == 0) atomicMax(A.vis_max, nvis);  // visited-table occupancy, for the next call's shape
+    if (A.vis_max && lane == 0) atomicMax(A.vis_max, nvis);
+    if (A.vis_sum && lane == 0) atomicAdd(A.vis_sum, nvis);  // visited-table occupancy, for the next call's shape
     if (A.qstats && lane == 0) {
       u32* qs = A.qstats + static_cast<u64>(qi) * kQsWords;
       qs[0] = st_dist;
@@ -1767,7 +1769,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHINE_FAST_M
       }
     }
     if (status == ST_OVERFLOW && A.out_list && lane == 0) A.out_list[atomicAdd(A.out_count, 1u)] = qi;
-    if (A.vis_max && lane == 0) atomicMax(A.vis_max, nvis);  // visited-table occupancy, for the next call's shape
+    if (A.vis_max && lane == 0) atomicMax(A.vis_max, nvis);
+    if (A.vis_sum && lane == 0) atomicAdd(A.vis_sum, nvis);  // visited-table occupancy, for the next call's shape
     if (A.qstats && lane == 0) {
       u32* qs = A.qstats + static_cast<u64>(qi) * kQsWords;
       qs[0] = st_dist;
