@@ -241,7 +241,7 @@ def sharded_leg(a, world: int):
                                                            "SHINE_BENCH_ARGV")}
     env["OMP_NUM_THREADS"] = str(max(1, min(host_threads(), 16 * world)))
     t0 = time.time()
-    r = child_json(cmd, env=env)
+    r = child_json(cmd, env=env, timeout=float(os.environ.get("SHINE_SHARDED_LEG_TIMEOUT", "900")))
     keys = ("value", "ms_per_step", "n_gpus", "gpu_slots", "recall_at_10", "search_mode", "scaling", "one_gpu_value",
             "speedup_vs_one_gpu", "reads", "bounds", "config", "data", "stub")
     out = {k: r[k] for k in keys if k in r}
@@ -571,7 +571,13 @@ def main():
         if a.sharded_leg == "on" or (a.sharded_leg == "auto" and world > 1):
             del qd, ids, dists, qs
             torch.cuda.empty_cache()
-            out["sharded"] = sharded_leg(a, world)
+            # the replica measurement above is this line's `value`: a failing sharded child (it has never run on
+            # more than one physical GPU of this pool) is reported in the line instead of losing the line
+            try:
+                out["sharded"] = sharded_leg(a, world)
+            except (SystemExit, Exception) as e:
+                log(f"sharded leg failed: {e}")
+                out["sharded"] = {"error": str(e)}
         print(json.dumps(out), flush=True)
 
 
