@@ -292,6 +292,16 @@ def main():
     rows = ROW_NAMES[info["elem"]]
     log(f"rank {rank}: index on GPU {local}: {info['num_nodes']} nodes, max level {info['max_level']}, "
         f"{info['device_bytes'] / 2**20:.0f} MiB ({rows} rows); device {info['cus']} CUs, {info['lds_per_cu']} B LDS per CU")
+    if dist:
+        # the entry-point all-gather (RCCL; once, outside the timed region): every compute node reads the entry point
+        # from memory node 1 (rdma_reads.hh:74-99) — here every rank gathers every other's (uid, level, records) and
+        # checks that all serve the same index before any query runs
+        mine = torch.tensor([info["entry_uid"], info["max_level"], info["num_nodes"]], dtype=torch.int64,
+                            device=f"cuda:{local}")
+        every = torch.empty((world, 3), dtype=torch.int64, device=f"cuda:{local}")
+        dist.all_gather_into_tensor(every, mine)
+        if not (every == mine).all():
+            raise SystemExit(f"rank {rank}: ranks disagree on the entry point / index: {every.tolist()}")
 
     # queries: rank r takes ids ≡ r (mod G) of a common pool (read_data.hh:57-58)
     nq_rank = a.batch * a.nbatches
