@@ -775,15 +775,18 @@ LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds
   LaunchShape sh{};
   const uint32_t want = std::max<uint32_t>(1, std::min<uint32_t>(16, (nq + cus - 1) / cus));
   // Waves per CU the tables are sized for, in batches of `want`, and the table floor per ef.  f32 rows: two batches,
-  // pow2(40·ef) entries.  Byte rows move a quarter of the bytes per distance, so the kernel is latency-bound there and
-  // residency pays: four batches (16 wavefronts per CU at batch 1,024) and pow2(24·ef) entries, the few queries that
-  // outgrow them spilling in place (SearchArgs::spill_flags) — u8 rows at ef = 128: 8.18 M against 7.74 M QPS, f32
-  // rows 6.34 M against 6.69 M (profiles/r03/lib_probe_v16_tables.jsonl).  The environment overrides both (tuning).
+  // pow2(40·ef) entries.  Byte rows at ef > 64 move a quarter of the bytes per distance over long searches, so the
+  // kernel is latency-bound there and residency pays: four batches (12-16 wavefronts per CU at batch 1,024) and
+  // pow2(24·ef) entries, the few queries that outgrow them spilling in place (SearchArgs::spill_flags) — u8 rows at
+  // ef = 128: 8.26-8.28 M against 7.78-7.79 M QPS; at ef = 48 the same policy lost 17 % (17.3 M against 20.8 M), f32
+  // rows lose at ef = 128 (6.34 M against 6.69 M) (profiles/r03/ab1_merge_spill_tables.jsonl,
+  // lib_probe_v16_tables.jsonl).  The environment overrides both (tuning).
+  const bool wide_residency = byte_rows && ef > 64;
   const uint32_t target = std::min<uint32_t>(
-      16, static_cast<uint32_t>(env_int("SHINE_FAST_TARGET_BATCHES", byte_rows ? 4 : 2)) * want);
+      16, static_cast<uint32_t>(env_int("SHINE_FAST_TARGET_BATCHES", wide_residency ? 4 : 2)) * want);
   // with f32 rows a table below pow2(40·ef) entries costs more than its residency buys
   const uint32_t per_ef =
-      static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_FAST_TABLE_PER_EF", byte_rows ? 24 : 40)));
+      static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_FAST_TABLE_PER_EF", wide_residency ? 24 : 40)));
   uint32_t lo = std::min<uint32_t>(16384, std::max<uint32_t>(2048, pow2_at_least(per_ef * ef)));
   // what the previous call's queries needed: a smaller table, or a larger one once the fixed size overflowed
   if (learned && (learned < lo || grow)) lo = learned;
@@ -848,13 +851,13 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
   uint64_t budget = lds;
   if (pass == PASS_LDS) {
     // u16 quotient entries (VisitedLds<1>) when the id space fits them and they let more wavefronts share a CU with
-    // next_candidates still >= 5·ef entries (u32: 4·ef).  With the in-place spill (a query that outgrows its table
-    // goes on in an HBM bitmap) tables of pow2(24·ef) entries, sized for the wavefronts of four batches in flight
-    // (4,096 entries and up to 11 wavefronts per CU at ef = 128 instead of 8,192 and 7); without it pow2(48·ef) and
-    // two batches, as a query that overflows is re-run from scratch by the light pass.  Tuning hooks: the two env knobs.
-    const bool spill = spill_enabled();
-    const uint32_t per_ef = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_EXACT_TABLE_PER_EF", spill ? 24 : 48)));
-    const uint32_t batches = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_EXACT_TARGET_BATCHES", spill ? 4 : 2)));
+    // next_candidates still >= 5·ef entries (u32: 4·ef).  Tables of pow2(48·ef) entries, sized for the wavefronts of
+    // two batches in flight.  Smaller tables for four batches (pow2(24·ef): 4,096 entries and up to 11 wavefronts per
+    // CU at ef = 128 instead of 8,192 and 7), with the in-place spill catching the queries that outgrow them, were
+    // slower: 1.76-1.84 M against 1.94 M QPS (profiles/r03/ab1_merge_spill_tables.jsonl) — the exact kernel is bound
+    // by instruction issue, not by resident wavefronts.  Tuning hooks: the two env knobs.
+    const uint32_t per_ef = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_EXACT_TABLE_PER_EF", 48)));
+    const uint32_t batches = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_EXACT_TARGET_BATCHES", 2)));
     sh.vis_cap = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(per_ef * ef)));
     if (learned && (learned < sh.vis_cap || (handed != 0xFFFFFFFFu && handed > 0))) sh.vis_cap = learned;  // as fast
     sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
@@ -943,7 +946,10 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   const uint32_t handed = S.seen.p[3] ? S.seen.p[0] : 0;  // [3] = 1 once a call has written the counts
   if (handed && S.last_learned) S.table_floor = std::max(S.table_floor, 2 * S.last_table);  // it was too small
   if (ef != S.last_ef) S.table_floor = 0;
-  const uint32_t learned = ef != S.last_ef ? 0 : spill_enabled() ? learned_mean_table(S) : learned_table(S);
+  // the fast pass sizes its table for the mean query when it can spill in place; the exact pass keeps the maximum
+  // (its tables sized from the mean ran slower, profiles/r03/ab1_merge_spill_tables.jsonl)
+  const uint32_t learned = ef != S.last_ef ? 0 : learned_table(S);
+  const uint32_t learned_fast = ef != S.last_ef ? 0 : spill_enabled() ? learned_mean_table(S) : learned;
   S.last_ef = ef;
   S.last_nq = nq;
   int chain[3], n_pass = 0;
@@ -954,12 +960,13 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   for (int i = 0; i < n_pass; ++i) {
     const int pass = chain[i];
     const LaunchShape sh =
-        pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu, h->id_space, learned, handed > 0,
+        pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu, h->id_space, learned_fast, handed > 0,
                                           elem_is_byte(h->elem))
                           : pick_shape(h, R, nq, ef, pass, handed, learned);
     if (i == 0) {
       S.last_table = sh.vis_cap;
-      S.last_learned = learned != 0 && sh.vis_cap == learned;  // the table came from learning, not the fixed rule
+      const uint32_t lw = pass == PASS_FAST ? learned_fast : learned;
+      S.last_learned = lw != 0 && sh.vis_cap == lw;  // the table came from learning, not the fixed rule
       if (env_int("SHINE_DEBUG_SHAPE", 0))  // diagnostics: the main pass's shape and what it was learned from
         std::fprintf(stderr, "shape: pass %d nq %u ef %u table %u vis16 %u grid %u learned %u vmax %u handed %u floor %u\n",
                      pass, nq, ef, sh.vis_cap, sh.vis16, sh.grid, learned, S.seen.p[3] ? S.seen.p[4] : 0u, handed,
