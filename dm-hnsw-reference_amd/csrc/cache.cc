@@ -55,7 +55,9 @@ RecordCache::RecordCache(uint32_t entries, uint64_t seed)
       ct_(CT_),
       key_of_(entries, kInv),
       dev_of_(entries, kInv),
-      cooling_(entries, 0) {}
+      cooling_(entries, 0) {
+  slot_of_.reserve(entries);  // no rehash while the cache fills
+}
 
 bool RecordCache::size_ok(uint32_t entries) {
   const uint32_t ct = std::max<uint32_t>(

@@ -136,8 +136,14 @@ def run(name, a):
     else:
         q = getattr(D, gen)(batch * nb, seed=2, d=dim)
     qd = torch.from_numpy(q).cuda()
+    dyn = None
     with Heartbeat(f"{name}: ground truth"):
-        gt = ground_truth(torch, torch.from_numpy(base).cuda(), qd, a.k, metric)
+        base_t = torch.from_numpy(base).cuda()
+        gt = ground_truth(torch, base_t, qd, a.k, metric)
+        if placement == "sharded" and a.dynamic:  # the dynamic-cache stream: a fresh batch every call
+            dq = np.ascontiguousarray(getattr(D, gen)(a.dynamic_calls * batch, seed=11, d=dim))
+            dyn = (dq, ground_truth(torch, base_t, torch.from_numpy(dq).cuda(), a.k, metric))
+        del base_t
     del base
     torch.cuda.empty_cache()
     fracs = [float(x) for x in a.cache_fracs.split(",")] if placement == "sharded" else [0.0]
@@ -157,14 +163,15 @@ def run(name, a):
             log(json.dumps(line))
             lines.append(line)
         idx.close()
-    if placement == "sharded" and a.dynamic:
-        lines.append(run_dynamic(name, a, paths, dim, M, metric, elem, gpus, q, gt, batch, ef))
+    if dyn is not None:
+        lines.append(run_dynamic(name, a, paths, dim, M, metric, elem, gpus, dyn[0], dyn[1], batch, ef))
     return lines
 
 
 def run_dynamic(name, a, paths, dim, M, metric, elem, gpus, q, gt, batch, ef):
     """The reference's runtime cache (SHINE_CACHE_DYNAMIC: admission, cooling eviction, second chance, applied
-    between calls) over a stream of batches through the host API: hit rate per call from an empty cache."""
+    between calls) over a stream of distinct batches through the host API: hit rate per call from an empty cache,
+    recall over the whole stream, and the host call rate including the cache updates."""
     import shine_amd
     from shine_amd import datasets as D
     L = shine_amd._lib
@@ -181,12 +188,13 @@ def run_dynamic(name, a, paths, dim, M, metric, elem, gpus, q, gt, batch, ef):
                     query_ids=np.arange(c * batch, (c + 1) * batch, dtype=np.uint32))
         t_total += time.perf_counter() - t0
         rates.append(r.stats["node_cache_hits"] / max(1, r.stats["node_reads"]))
-        if c < nb:
-            res.append(r.ids)
+        res.append(r.ids)
     idx.close()
     line = {"workload": name, "search_mode": "fast", "cache_policy": "dynamic", "cache_ratio_percent": a.dynamic,
-            "calls": calls, "batch": batch, "hit_rate_per_call": rates, "cache_hit_rate_last": rates[-1],
-            "recall_at_10": D.recall_at_k(np.concatenate(res), gt[:len(res) * batch], a.k),
+            "calls": calls, "batch": batch, "distinct_batches": nb, "hit_rate_per_call": rates,
+            "cache_hit_rate_last": rates[-1],
+            "recall_at_10": D.recall_at_k(np.concatenate(res), np.concatenate([gt[(c % nb) * batch:(c % nb + 1) * batch]
+                                                                                for c in range(calls)]), a.k),
             "host_api_qps_including_cache_updates": calls * batch / t_total,
             "note": "hit rate = cached record reads / all record reads (statistics.hh:171-173); the cache is updated "
                     "between calls on the host (cache.h RecordCache) and the arena on the GPU"}
