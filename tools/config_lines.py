@@ -325,9 +325,11 @@ def run_skew(a):
                 di.set_search_mode(L.MODE_FAST)
                 di.set_cache_policy(L.CACHE_DYNAMIC, ratio_percent=a.dynamic, seed=1)
                 rates = []
-                stream = [warm] + [q[b * batch:(b + 1) * batch] for b in range(q.shape[0] // batch)]
+                # a fresh Zipf-drawn batch every call (repeats come from the skew itself, not from replaying batches)
+                sq, _, _ = D.zipf_query_mix(pool, a.dynamic_calls * batch, alpha, seed=13)
+                stream = [np.ascontiguousarray(sq[c * batch:(c + 1) * batch]) for c in range(a.dynamic_calls)]
                 for c in range(a.dynamic_calls):
-                    qq = stream[c % len(stream)]
+                    qq = stream[c]
                     r = di.knn(qq, a.k, ef, query_ids=np.arange(c * batch, c * batch + qq.shape[0], dtype=np.uint32))
                     rates.append(r.stats["node_cache_hits"] / max(1, r.stats["node_reads"]))
             dyn = {"cache_ratio_percent": a.dynamic, "calls": a.dynamic_calls, "hit_rate_per_call": rates}
