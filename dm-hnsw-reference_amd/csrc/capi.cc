@@ -838,7 +838,7 @@ uint32_t bitmap_slot_cap(const shine_index* h) {
 // that (at least one per CU, at most what LDS shares and bitmap memory allow): its workgroups of a call with few
 // overflows exit at once, and a launch of thousands of them delays the stream's next batch (-7 % QPS at ef = 32).
 LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint32_t ef, int pass,
-                       uint32_t handed = 0xFFFFFFFFu, uint32_t learned = 0) {
+                       uint32_t handed = 0xFFFFFFFFu, uint32_t learned = 0, uint32_t learned_mean = 0) {
   LaunchShape sh{};
   const uint64_t top_bytes = align16(8ull * ef);
   const uint32_t cus = R.cus, lds = R.lds_per_cu;
@@ -852,28 +852,46 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
   uint64_t budget = lds;
   if (pass == PASS_LDS) {
     // u16 quotient entries (VisitedLds<1>) when the id space fits them and they let more wavefronts share a CU with
-    // next_candidates still >= 5·ef entries (u32: 4·ef).  Tables of pow2(48·ef) entries, sized for the wavefronts of
-    // two batches in flight.  Smaller tables for four batches (pow2(24·ef): 4,096 entries and up to 11 wavefronts per
-    // CU at ef = 128 instead of 8,192 and 7), with the in-place spill catching the queries that outgrow them, were
-    // slower: 1.76-1.84 M against 1.94 M QPS (profiles/r03/ab1_merge_spill_tables.jsonl) — the exact kernel is bound
-    // by instruction issue, not by resident wavefronts.  Tuning hooks: the two env knobs.
+    // next_candidates still >= 5·ef entries (u32: 4·ef).  Tables of pow2(48·ef) entries, or the previous call's
+    // most-visited query, sized for the wavefronts of two batches in flight.  Smaller tables for four batches
+    // (pow2(24·ef): 4,096 entries and up to 11 wavefronts per CU at ef = 128 instead of 8,192 and 7), with the
+    // in-place spill catching the queries that outgrow them, were slower: 1.76-1.84 M against 1.94 M QPS
+    // (profiles/r03/ab1_merge_spill_tables.jsonl).  But where the table sized for the worst query leaves fewer than
+    // four wavefronts per CU, the mean-sized one (learned_mean) is taken: DEEP-shaped 10M ids at ef = 256, 16,384
+    // u16 entries and 3 wavefronts per CU against 4,096 u32 entries and 6, 0.48 M against 0.72 M QPS
+    // (profiles/r03/config_lines_cfg3_10m*.jsonl).  Tuning hooks: the two env knobs.
     const uint32_t per_ef = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_EXACT_TABLE_PER_EF", 48)));
     const uint32_t batches = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_EXACT_TARGET_BATCHES", 2)));
-    sh.vis_cap = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(per_ef * ef)));
-    if (learned && (learned < sh.vis_cap || (handed != 0xFFFFFFFFu && handed > 0))) sh.vis_cap = learned;  // as fast
-    sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
     const uint32_t want = std::min<uint32_t>(batches * ((nq + cus - 1) / cus), 16u);
-    auto waves = [&](uint64_t need) {
-      return std::max<uint32_t>(1, std::min<uint32_t>(want, static_cast<uint32_t>(lds / need)));
-    };
-    const uint32_t w32 = waves(search_lds_bytes(ef, 4 * ef, sh.vis_cap, 4));
-    const uint32_t w16 = waves(search_lds_bytes(ef, 5 * ef, sh.vis_cap, 2));
     uint32_t bits = 14;
     while (bits < 32 && (1ull << bits) < h->id_space) ++bits;
-    const bool can16 = env_int("SHINE_DEBUG_VIS16", 1) != 0 && bits <= log2_ceil(sh.vis_cap) + 10;
-    sh.vis16 = can16 && (w16 > w32 || env_int("SHINE_DEBUG_VIS16", -1) == 1) ? 1 : 0;
+    auto fit = [&](uint32_t vis_cap, uint32_t& vis16) {  // entry width and resident wavefronts for a table size
+      auto waves = [&](uint64_t need) {
+        return std::max<uint32_t>(1, std::min<uint32_t>(want, static_cast<uint32_t>(lds / need)));
+      };
+      const uint32_t w32 = waves(search_lds_bytes(ef, 4 * ef, vis_cap, 4));
+      const uint32_t w16 = waves(search_lds_bytes(ef, 5 * ef, vis_cap, 2));
+      const bool can16 = env_int("SHINE_DEBUG_VIS16", 1) != 0 && bits <= log2_ceil(vis_cap) + 10;
+      vis16 = can16 && (w16 > w32 || env_int("SHINE_DEBUG_VIS16", -1) == 1) ? 1 : 0;
+      return vis16 ? w16 : w32;
+    };
+    sh.vis_cap = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(per_ef * ef)));
+    if (learned && (learned < sh.vis_cap || (handed != 0xFFFFFFFFu && handed > 0))) sh.vis_cap = learned;  // as fast
+    wpc = fit(sh.vis_cap, sh.vis16);
+    if (wpc < 4 && learned_mean && learned_mean < sh.vis_cap && spill_enabled()) {
+      uint32_t v16 = 0;
+      const uint32_t w = fit(learned_mean, v16);
+      if (w > wpc) {
+        sh.vis_cap = learned_mean;
+        sh.vis16 = v16;
+        wpc = w;
+      }
+    }
+    if (const char* e = std::getenv("SHINE_DEBUG_VISCAP")) {  // test hook
+      sh.vis_cap = static_cast<uint32_t>(std::atoll(e));
+      wpc = fit(sh.vis_cap, sh.vis16);
+    }
     sh.vis_bits = std::max(bits, log2_ceil(sh.vis_cap) + 1);
-    wpc = sh.vis16 ? w16 : w32;
     budget = (lds / wpc) & ~15u;
   } else if (pass == PASS_WHOLE_CU) {
     sh.vis_cap = 16384;
@@ -963,11 +981,12 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     const LaunchShape sh =
         pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu, h->id_space, learned_fast, handed > 0,
                                           elem_is_byte(h->elem))
-                          : pick_shape(h, R, nq, ef, pass, handed, learned);
+                          : pick_shape(h, R, nq, ef, pass, handed, learned, learned_fast);
     if (i == 0) {
       S.last_table = sh.vis_cap;
-      const uint32_t lw = pass == PASS_FAST ? learned_fast : learned;
-      S.last_learned = lw != 0 && sh.vis_cap == lw;  // the table came from learning, not the fixed rule
+      // the table came from learning, not the fixed rule
+      S.last_learned = (learned_fast != 0 && sh.vis_cap == learned_fast) ||
+                       (pass != PASS_FAST && learned != 0 && sh.vis_cap == learned);
       if (env_int("SHINE_DEBUG_SHAPE", 0))  // diagnostics: the main pass's shape and what it was learned from
         std::fprintf(stderr, "shape: pass %d nq %u ef %u table %u vis16 %u grid %u learned %u vmax %u handed %u floor %u\n",
                      pass, nq, ef, sh.vis_cap, sh.vis16, sh.grid, learned, S.seen.p[3] ? S.seen.p[4] : 0u, handed,
