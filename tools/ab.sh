@@ -14,4 +14,4 @@ for rep in 1 2; do
     SHINE_GPU_LIB=$L timeout -k 10 300 python -u tools/lib_probe.py --runs $RUNS --tag $L >> $O/probe.jsonl 2>> $O/probe.log || { echo "probe $L failed"; tail -20 $O/probe.log; exit 1; }
   done
 done
-cat $O/probe.jsonl
+[ -f $O/probe.jsonl ] && cat $O/probe.jsonl; true
