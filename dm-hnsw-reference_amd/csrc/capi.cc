@@ -145,6 +145,7 @@ struct Scratch {
   uint32_t table_floor = 0;      // a learned table that overflowed is never learned again below twice its size
   uint32_t last_ef = 0;          // ef of the last call: what it visited says nothing about another ef
   uint32_t last_nq = 0;          // queries of the last call (seen[5] / last_nq: the mean a query marked visited)
+  bool last_fast = false;        // the last call's main pass was the fast kernel
   void release() {
     for (auto* b : {&visited, &vlog, &counter, &ovf, &qs, &spill_flags}) b->release();
     heaps.release();
@@ -963,7 +964,10 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   const bool fast_mode = h->search_mode == SHINE_MODE_FAST;
   const bool fast_kernel = fast_mode && ef <= kFastMaxEf && h->M0 <= 64;
   const uint32_t handed = S.seen.p[3] ? S.seen.p[0] : 0;  // [3] = 1 once a call has written the counts
-  if (handed && S.last_learned) S.table_floor = std::max(S.table_floor, 2 * S.last_table);  // it was too small
+  // a learned table that handed queries on was too small — unless the pass spills its tables in place: then only the
+  // exact pass hands queries on, for its next_candidates capacity, which a larger table would only shrink
+  if (handed && S.last_learned && (S.last_fast || !spill_enabled()))
+    S.table_floor = std::max(S.table_floor, 2 * S.last_table);
   if (ef != S.last_ef) S.table_floor = 0;
   // the fast pass sizes its table for the mean query when it can spill in place; the exact pass keeps the maximum
   // (its tables sized from the mean ran slower, profiles/r03/ab1_merge_spill_tables.jsonl)
@@ -984,6 +988,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
                           : pick_shape(h, R, nq, ef, pass, handed, learned, learned_fast);
     if (i == 0) {
       S.last_table = sh.vis_cap;
+      S.last_fast = pass == PASS_FAST;
       // the table came from learning, not the fixed rule
       S.last_learned = (learned_fast != 0 && sh.vis_cap == learned_fast) ||
                        (pass != PASS_FAST && learned != 0 && sh.vis_cap == learned);
