@@ -15,7 +15,7 @@ import numpy as np
 
 p = argparse.ArgumentParser()
 p.add_argument("trace")
-p.add_argument("--kernel", default="search_fast_kernel<128, 0, float, 2, 2, false")
+p.add_argument("--kernel", default="search_fast_kernel<128, 0, float, 2, 2,")
 p.add_argument("--skip", type=int, default=15)
 p.add_argument("--count", type=int, default=20)
 p.add_argument("--out")
