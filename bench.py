@@ -241,7 +241,7 @@ def sharded_leg(a, world: int):
                                                            "SHINE_BENCH_ARGV")}
     env["OMP_NUM_THREADS"] = str(max(1, min(host_threads(), 16 * world)))
     t0 = time.time()
-    r = child_json(cmd, env=env, timeout=float(os.environ.get("SHINE_SHARDED_LEG_TIMEOUT", "900")))
+    r = child_json(cmd, env=env, timeout=float(os.environ.get("SHINE_SHARDED_LEG_TIMEOUT", "480")))
     keys = ("value", "ms_per_step", "n_gpus", "gpu_slots", "recall_at_10", "search_mode", "scaling", "one_gpu_value",
             "speedup_vs_one_gpu", "reads", "bounds", "config", "data", "stub")
     out = {k: r[k] for k in keys if k in r}
