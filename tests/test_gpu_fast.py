@@ -235,6 +235,32 @@ def test_learned_table_sizes_keep_results(mode, gpu_available):
         _check_tie_free_exact(runs[-1], ref, 0.95)
 
 
+def test_exact_mode_relearns_oversized_tables(gpu_available, monkeypatch, capfd):
+    """Exact mode with fixed tables far too large for the queries (64·ef entries at ef = 256: 16,384, three
+    wavefronts per CU): the next calls on the stream run on tables learned from the first (capi.cc pick_shape:
+    the worst query's size, or the mean-sized one where that leaves fewer than four wavefronts per CU), read from
+    SHINE_DEBUG_SHAPE's stderr line, and every call returns the oracle's ids, distances and counters."""
+    base = D.deep_like(6000, seed=83, d=96)
+    q = D.deep_like(300, seed=84, d=96)
+    dumps, _, _ = O.build(base, 16, 100, 1, 1, seed=8)
+    ref = O.OracleIndex(dumps, 96, 16, 1).knn(q, 10, 256, threads=8)
+    monkeypatch.setenv("SHINE_DEBUG_SHAPE", "1")
+    monkeypatch.setenv("SHINE_EXACT_TABLE_PER_EF", "64")
+    tables = []
+    with shine_amd.Index.from_buffers(dumps, 96, 16, 1, gpus=[0]) as idx:
+        idx.set_search_mode(L.MODE_EXACT)
+        for _ in range(3):
+            capfd.readouterr()
+            r = idx.knn(q, 10, 256)
+            err = capfd.readouterr().err
+            tables.append(int(err.split(" table ")[1].split()[0]))
+            assert (r.qstats[:, L.QS_STATUS] == 0).all()
+            np.testing.assert_array_equal(r.ids, ref[0])
+            np.testing.assert_array_equal(r.dists.view(np.uint32), ref[1].view(np.uint32))
+            np.testing.assert_array_equal(r.qstats[:, :5], ref[2][:, :5])
+    assert tables[0] == 16384 and tables[1] < tables[0] and tables[2] == tables[1], tables
+
+
 @pytest.mark.parametrize("vis16", ["0", "1"])
 @pytest.mark.parametrize("gen,dim,metric,ef", [(D.deep_like, 96, 0, 128), (D.sift_like, 128, 0, 128),
                                                 (D.deep_like, 96, 1, 256)])
