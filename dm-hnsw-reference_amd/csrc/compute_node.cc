@@ -298,6 +298,8 @@ void add(shine_stats& a, const shine_stats& b) {
   a.remote_reads_in_bytes += b.remote_reads_in_bytes;
   a.cache_hits += b.cache_hits;
   a.cache_misses += b.cache_misses;
+  a.node_reads += b.node_reads;
+  a.node_cache_hits += b.node_cache_hits;
   a.kernel_ms += b.kernel_ms;
 }
 
@@ -468,10 +470,16 @@ int run(const Config& c) {
   qj.num("queries_per_sec", static_cast<uint64_t>(query_s > 0 ? th.stats.processed / query_s : 0));
   qj.str("compute_recall", compute_recall ? "true" : "false");
   Json cj;
-  cj.num("hits_total", th.stats.cache_hits);
-  cj.num("misses_total", th.stats.cache_misses);
+  // statistics.hh:171-173: hits over every record lookup (a compute node reads every record remotely); the reads of
+  // records another GPU holds are reported separately (off_stripe_*)
+  const uint64_t reads = th.stats.node_reads, hits = th.stats.node_cache_hits;
+  cj.num("hits_total", hits);
+  cj.num("misses_total", reads - std::min(reads, hits));
+  cj.num("hit_rate", reads ? static_cast<double>(hits) / static_cast<double>(reads) : 0.0);
+  cj.num("off_stripe_hits_total", th.stats.cache_hits);
+  cj.num("off_stripe_misses_total", th.stats.cache_misses);
   const uint64_t lookups = th.stats.cache_hits + th.stats.cache_misses;
-  cj.num("hit_rate", lookups ? static_cast<double>(th.stats.cache_hits) / static_cast<double>(lookups) : 0.0);
+  cj.num("off_stripe_hit_rate", lookups ? static_cast<double>(th.stats.cache_hits) / static_cast<double>(lookups) : 0.0);
   if (c.use_cache) cj.num("cache_size_ratio", c.cache_size_ratio);
   Json gj;  // not in the reference: the GPU side of the same run
   gj.num("device_bytes_per_gpu", info.device_bytes);
