@@ -130,6 +130,19 @@ def max_over_ranks(x: float, dist, device: str) -> float:
     return float(t.item())
 
 
+def check_same_index(dist, torch, info, world: int, rank: int, device: str):
+    """The entry-point all-gather (RCCL on GPUs, gloo in the CPU test; once, outside the timed region): every compute
+    node reads the entry point from memory node 1 (rdma_reads.hh:74-99) — here every rank gathers every other's
+    (entry uid, level, records) and checks that all serve the same index before any query runs."""
+    mine = torch.tensor([info["entry_uid"], info["max_level"], info["num_nodes"]], dtype=torch.int64, device=device)
+    every = torch.empty(world * 3, dtype=torch.int64, device=device)  # flat: gloo takes no (world, 3) output
+    dist.all_gather_into_tensor(every, mine)
+    every = every.view(world, 3)
+    if not (every == mine).all():
+        raise SystemExit(f"rank {rank}: ranks disagree on the entry point / index: {every.tolist()}")
+    return every
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -293,15 +306,7 @@ def main():
     log(f"rank {rank}: index on GPU {local}: {info['num_nodes']} nodes, max level {info['max_level']}, "
         f"{info['device_bytes'] / 2**20:.0f} MiB ({rows} rows); device {info['cus']} CUs, {info['lds_per_cu']} B LDS per CU")
     if dist:
-        # the entry-point all-gather (RCCL; once, outside the timed region): every compute node reads the entry point
-        # from memory node 1 (rdma_reads.hh:74-99) — here every rank gathers every other's (uid, level, records) and
-        # checks that all serve the same index before any query runs
-        mine = torch.tensor([info["entry_uid"], info["max_level"], info["num_nodes"]], dtype=torch.int64,
-                            device=f"cuda:{local}")
-        every = torch.empty((world, 3), dtype=torch.int64, device=f"cuda:{local}")
-        dist.all_gather_into_tensor(every, mine)
-        if not (every == mine).all():
-            raise SystemExit(f"rank {rank}: ranks disagree on the entry point / index: {every.tolist()}")
+        check_same_index(dist, torch, info, world, rank, f"cuda:{local}")
 
     # queries: rank r takes ids ≡ r (mod G) of a common pool (read_data.hh:57-58)
     nq_rank = a.batch * a.nbatches
@@ -604,6 +609,8 @@ def stub_rank(a):
         t = torch.ones(1)
         dist.all_reduce(t)
         seen = int(t.item())
+        # the same entry-point check the GPU ranks run, over gloo, on a stand-in index description
+        check_same_index(dist, torch, {"entry_uid": 7, "max_level": 3, "num_nodes": 1000}, world, rank, "cpu")
         dist.destroy_process_group()
     else:
         seen = 1
