@@ -978,8 +978,9 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   int chain[3], n_pass = 0;
   if (start <= 0) chain[n_pass++] = fast_kernel ? PASS_FAST : PASS_LDS;
   else if (start == 1) chain[n_pass++] = PASS_WHOLE_CU;
-  if (start <= 2) chain[n_pass++] = PASS_LIGHT;
-  if (!env_int("SHINE_DEBUG_NO_GLOBAL", 0)) chain[n_pass++] = PASS_GLOBAL;  // measurement hook
+  const bool main_only = env_int("SHINE_DEBUG_MAIN_ONLY", 0) != 0;  // measurement hook: no fallback passes
+  if (start <= 2 && !main_only) chain[n_pass++] = PASS_LIGHT;
+  if (!env_int("SHINE_DEBUG_NO_GLOBAL", 0) && !main_only) chain[n_pass++] = PASS_GLOBAL;  // measurement hook
   for (int i = 0; i < n_pass; ++i) {
     const int pass = chain[i];
     const LaunchShape sh =
