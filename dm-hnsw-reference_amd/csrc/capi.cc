@@ -766,7 +766,8 @@ uint32_t learned_table(const Scratch& S) {
 // config_lines_cfg3_10m_final.jsonl), and a table sized for the maximum holds half the wavefronts per CU.  Never below
 // the floor a call that exhausted the spill bitmaps set.
 uint32_t learned_mean_table(const Scratch& S) {
-  if (!S.seen.p || !S.seen.p[3] || !S.last_nq || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
+  // (the visited sum is a u32 word: calls of more than 2^20 queries could wrap it, and learn nothing here)
+  if (!S.seen.p || !S.seen.p[3] || !S.last_nq || S.last_nq > (1u << 20) || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
   const uint32_t mean = S.seen.p[5] / S.last_nq;
   if (mean == 0) return 0;
   return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, pow2_at_least(mean + mean / 4 + 64)}));
