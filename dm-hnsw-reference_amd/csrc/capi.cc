@@ -773,6 +773,19 @@ uint32_t learned_mean_table(const Scratch& S) {
   return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, pow2_at_least(mean + mean / 4 + 64)}));
 }
 
+// The exact pass's learned table, with the in-place spill: just the previous call's worst query (eighths/8 × its
+// visited count, SHINE_EXACT_LEARN_EIGHTHS, default 9), which then replaces the fixed size in either direction — a
+// query beyond it spills in place instead of being re-run.  Without the spill: learned_table (1.625 ×).
+uint32_t learned_exact_table(const Scratch& S) {
+  if (!spill_enabled()) return learned_table(S);
+  if (!S.seen.p || !S.seen.p[3] || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
+  const uint64_t vmax = S.seen.p[4];
+  if (vmax == 0) return 0;
+  const uint64_t eighths = static_cast<uint64_t>(std::max<int64_t>(8, env_int("SHINE_EXACT_LEARN_EIGHTHS", 9)));
+  const uint64_t want = std::min<uint64_t>(16384, vmax * eighths / 8);
+  return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, pow2_at_least(static_cast<uint32_t>(want))}));
+}
+
 LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds_per_cu, uint64_t id_space,
                             uint32_t learned = 0, bool grow = false, bool byte_rows = false) {
   LaunchShape sh{};
@@ -863,7 +876,7 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
     // u16 entries and 3 wavefronts per CU against 4,096 u32 entries and 6, 0.48 M against 0.72 M QPS
     // (profiles/r03/config_lines_cfg3_10m*.jsonl).  Tuning hooks: the two env knobs.
     const uint32_t per_ef = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_EXACT_TABLE_PER_EF", 48)));
-    const uint32_t batches = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_EXACT_TARGET_BATCHES", 2)));
+    const uint32_t batches = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_EXACT_TARGET_BATCHES", 3)));
     const uint32_t want = std::min<uint32_t>(batches * ((nq + cus - 1) / cus), 16u);
     uint32_t bits = 14;
     while (bits < 32 && (1ull << bits) < h->id_space) ++bits;
@@ -878,7 +891,10 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
       return vis16 ? w16 : w32;
     };
     sh.vis_cap = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(per_ef * ef)));
-    if (learned && (learned < sh.vis_cap || (handed != 0xFFFFFFFFu && handed > 0))) sh.vis_cap = learned;  // as fast
+    // a learned size replaces the fixed one: with the spill in either direction, else only to shrink (or to grow
+    // after a call that handed queries on)
+    if (learned && (spill_enabled() || learned < sh.vis_cap || (handed != 0xFFFFFFFFu && handed > 0)))
+      sh.vis_cap = learned;
     wpc = fit(sh.vis_cap, sh.vis16);
     if (wpc < 4 && learned_mean && learned_mean < sh.vis_cap && spill_enabled()) {
       uint32_t v16 = 0;
@@ -972,7 +988,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   if (ef != S.last_ef) S.table_floor = 0;
   // the fast pass sizes its table for the mean query when it can spill in place; the exact pass keeps the maximum
   // (its tables sized from the mean ran slower, profiles/r03/ab1_merge_spill_tables.jsonl)
-  const uint32_t learned = ef != S.last_ef ? 0 : learned_table(S);
+  const uint32_t learned = ef != S.last_ef ? 0 : learned_exact_table(S);
   const uint32_t learned_fast = ef != S.last_ef ? 0 : spill_enabled() ? learned_mean_table(S) : learned;
   S.last_ef = ef;
   S.last_nq = nq;
