@@ -774,8 +774,11 @@ uint32_t learned_mean_table(const Scratch& S) {
 }
 
 // The exact pass's learned table, with the in-place spill: just the previous call's worst query (eighths/8 × its
-// visited count, SHINE_EXACT_LEARN_EIGHTHS, default 9), which then replaces the fixed size in either direction — a
-// query beyond it spills in place instead of being re-run.  Without the spill: learned_table (1.625 ×).
+// visited count, SHINE_EXACT_LEARN_EIGHTHS, default 9), never below 2,048 entries (SHINE_EXACT_LEARN_MIN), which then
+// replaces the fixed size in either direction — a query beyond it spills in place instead of being re-run.  At
+// ef = 128 on the bench's index that is 4,096 entries and 11 wavefronts per CU instead of 8,192 and 7: 3.51 M against
+// 2.38 M QPS (profiles/r03/exact_learned_scan.jsonl); at ef = 32 a 1,024-entry table spilled too often (9.7 M against
+// 10.6 M), hence the floor.  Without the spill: learned_table (1.625 ×).
 uint32_t learned_exact_table(const Scratch& S) {
   if (!spill_enabled()) return learned_table(S);
   if (!S.seen.p || !S.seen.p[3] || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
@@ -783,7 +786,8 @@ uint32_t learned_exact_table(const Scratch& S) {
   if (vmax == 0) return 0;
   const uint64_t eighths = static_cast<uint64_t>(std::max<int64_t>(8, env_int("SHINE_EXACT_LEARN_EIGHTHS", 9)));
   const uint64_t want = std::min<uint64_t>(16384, vmax * eighths / 8);
-  return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, pow2_at_least(static_cast<uint32_t>(want))}));
+  const uint32_t lo = static_cast<uint32_t>(std::max<int64_t>(1024, env_int("SHINE_EXACT_LEARN_MIN", 2048)));
+  return std::min<uint32_t>(16384, std::max<uint32_t>({lo, S.table_floor, pow2_at_least(static_cast<uint32_t>(want))}));
 }
 
 LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds_per_cu, uint64_t id_space,
