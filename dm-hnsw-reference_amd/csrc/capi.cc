@@ -779,12 +779,15 @@ uint32_t learned_mean_table(const Scratch& S) {
 // ef = 128 on the bench's index that is 4,096 entries and 11 wavefronts per CU instead of 8,192 and 7: 3.51 M against
 // 2.38 M QPS (profiles/r03/exact_learned_scan.jsonl); at ef = 32 a 1,024-entry table spilled too often (9.7 M against
 // 10.6 M), hence the floor.  Without the spill: learned_table (1.625 ×).
-uint32_t learned_exact_table(const Scratch& S) {
+uint32_t learned_exact_table(const Scratch& S, uint32_t ef) {
   if (!spill_enabled()) return learned_table(S);
   if (!S.seen.p || !S.seen.p[3] || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
   const uint64_t vmax = S.seen.p[4];
   if (vmax == 0) return 0;
-  const uint64_t eighths = static_cast<uint64_t>(std::max<int64_t>(8, env_int("SHINE_EXACT_LEARN_EIGHTHS", 9)));
+  // at ef <= 32 the tables are small and a half-empty one probed faster than a fuller one (10.6 M against 9.7 M QPS
+  // at ef = 32, profiles/r03/exact_learned_scan_floor.jsonl): the round-2 margin there
+  const uint64_t eighths =
+      static_cast<uint64_t>(std::max<int64_t>(8, env_int("SHINE_EXACT_LEARN_EIGHTHS", ef <= 32 ? 13 : 9)));
   const uint64_t want = std::min<uint64_t>(16384, vmax * eighths / 8);
   const uint32_t lo = static_cast<uint32_t>(std::max<int64_t>(1024, env_int("SHINE_EXACT_LEARN_MIN", 2048)));
   return std::min<uint32_t>(16384, std::max<uint32_t>({lo, S.table_floor, pow2_at_least(static_cast<uint32_t>(want))}));
@@ -992,7 +995,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   if (ef != S.last_ef) S.table_floor = 0;
   // the fast pass sizes its table for the mean query when it can spill in place; the exact pass keeps the maximum
   // (its tables sized from the mean ran slower, profiles/r03/ab1_merge_spill_tables.jsonl)
-  const uint32_t learned = ef != S.last_ef ? 0 : learned_exact_table(S);
+  const uint32_t learned = ef != S.last_ef ? 0 : learned_exact_table(S, ef);
   const uint32_t learned_fast = ef != S.last_ef ? 0 : spill_enabled() ? learned_mean_table(S) : learned;
   S.last_ef = ef;
   S.last_nq = nq;
