@@ -104,6 +104,43 @@ struct DistArgs {
   float* out;                 // [nq][n_per]
 };
 
+// GPU batch builder (build_impl.h kernels, gpu_build.cc host side).  One batch = node ids batch_start ..
+// batch_start + n_lists0 - 1 inserted against the graph as it stood before the batch.
+struct BuildArgs {
+  DevGraph g;                 // the graph being built: f32 rows (device layout), lists, ep / ep_level before the batch
+  uint32_t* adj0w;            // writable views of g.adj0 / g.adjU
+  uint32_t* adjUw;
+  const float* base;          // the caller's rows, unpermuted [N][dim] (the batch's nodes as queries)
+  uint32_t ef, M;             // ef_construction; neighbours a new node selects (select_heuristic(top, M), hnsw.hh:157)
+  // candidate lists, ef entries each, ascending, INV-padded: rows 0 .. n_lists0-1 level 0 of the batch's nodes (the
+  // fast search kernel's output), then n_listsU upper-level lists (build_upper_kernel)
+  uint32_t* cand_ids;
+  float* cand_d;
+  uint32_t n_lists0, n_listsU, batch_start;
+  const uint32_t* list_node;  // [n_listsU] node and level of upper list j
+  const uint32_t* list_level;
+  // upper-level beams: batch nodes whose insert searches levels >= 1
+  const uint32_t* up_node;    // [n_up]
+  const uint32_t* up_first;   // [n_up] index of the node's first upper list (global); up_first_base: the batch's first
+  const uint32_t* up_levels;  // [n_up] L = min(level, top): lists at levels L .. 1, in that order
+  uint32_t up_first_base, n_up, vis_cap;
+  // reverse-edge requests [n_lists0 + n_listsU][M]: target row key (level 0: the node; level l: N + its upper row;
+  // key_none: no request), the new node, its distance; req_pos = the position (the sort's values)
+  uint32_t *req_key, *req_src, *req_pos;
+  float* req_d;
+  uint32_t key_none;
+  // the requests sorted by key (stable): skey / sval (positions); seg[0 .. *nseg) the first position of every key
+  const uint32_t* skey;
+  const uint32_t* sval;
+  uint32_t n_req;
+  const uint32_t* seg;
+  const uint32_t* nseg;
+  uint32_t* work;             // prune work-queue head (zero before the launch)
+  const uint32_t* row_owner;  // [upper rows] the node owning each
+  unsigned long long* stats;  // [0] appended rows [1] pruned rows [2] pools truncated to 64 [3] upper beams stopped
+};
+enum BuildKernel { BUILD_UPPER = 0, BUILD_SELECT = 1, BUILD_PRUNE = 2 };
+
 // LDS layout of a search workgroup: top[ef] | next[cap] | visited table[vis_cap] (entry_bytes each) | scratch
 // ids[64], dists[64]
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
@@ -158,7 +195,8 @@ bool dim_supported(uint32_t dim, int elem);
 #define SHINE_DIMS(X) X(16) X(32) X(64) X(96) X(100) X(128) X(200) X(256)
 #define SHINE_DECLARE_DIM(DD)                                                                                       \
   hipError_t launch_search_d##DD(int metric, int elem, uint32_t grid, const SearchArgs& a, hipStream_t s);          \
-  hipError_t launch_distance_d##DD(int metric, int elem, const DistArgs& a, hipStream_t s);
+  hipError_t launch_distance_d##DD(int metric, int elem, const DistArgs& a, hipStream_t s);                        \
+  hipError_t launch_build_d##DD(int which, int metric, uint32_t grid, const BuildArgs& a, hipStream_t s);
 SHINE_DIMS(SHINE_DECLARE_DIM)
 #undef SHINE_DECLARE_DIM
 // byte rows: one translation unit per (dimension, signedness), kernels_dim.hip with -DSHINE_BYTES=2 (u8) / 3 (i8)
@@ -174,6 +212,25 @@ SHINE_BYTE_DIMS(SHINE_DECLARE_BDIM)
 // Returns hipSuccess or the launch error.  grid = number of persistent search slots (one wavefront each).
 hipError_t launch_search(uint32_t dim, int metric, int elem, uint32_t grid, const SearchArgs& a, hipStream_t s);
 hipError_t launch_distance(uint32_t dim, int metric, int elem, const DistArgs& a, hipStream_t s);
+// GPU batch builder: one of BuildKernel over `grid` workgroups (f32 rows)
+hipError_t launch_build(uint32_t dim, int metric, int which, uint32_t grid, const BuildArgs& a, hipStream_t s);
+
+// Dimension-independent builder kernels (build_kernels.hip)
+hipError_t launch_iota(uint32_t* out, uint64_t n, hipStream_t s);
+// rows [n][dim] f32 unpermuted → device layout (kernels.h permuted_index) f32 / f16 / byte rows (elem 0 / 1 / 2 / 3);
+// from_device_layout: the source is already f32 in the device layout (a layout change of the element type only)
+hipError_t launch_rows_to_device(const float* src, void* dst, uint64_t n, uint32_t dim, int elem, bool from_device_layout,
+                                 hipStream_t s);
+// a batch's search counters: out[0] += distcomps, out[1] += searches that ended with a status
+hipError_t launch_qstats_sum(const uint32_t* qs, uint32_t nq, unsigned long long* out, hipStream_t s);
+// *flag |= 1 if any of `total` f32 components is not exactly a u8 (elem 2) / i8 (elem 3) value
+hipError_t launch_fits_bytes(const float* src, uint64_t total, int elem, uint32_t* flag, hipStream_t s);
+// segment starts of the sorted request keys (keys < key_none): seg[atomic] = i where key[i] != key[i-1]
+hipError_t launch_segments(const uint32_t* skey, uint32_t n, uint32_t key_none, uint32_t* seg, uint32_t* nseg,
+                           hipStream_t s);
+// stable radix sort of (key, value) pairs on the low `bits` key bits; temp == nullptr: *temp_bytes = the need
+hipError_t radix_sort_u32_pairs(void* temp, size_t* temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                                const uint32_t* vals_in, uint32_t* vals_out, uint32_t n, uint32_t bits, hipStream_t s);
 
 // Dynamic record cache updates between calls (capi.cc apply_dynamic), in order on one stream: drop the departing
 // device ids from cslot; copy the admitted records' rows (row_bytes each, from the GPU's view of the vectors) into

@@ -50,6 +50,14 @@ hipError_t launch_distance(uint32_t dim, int metric, int elem, const DistArgs& a
   return hipErrorInvalidValue;
 }
 
+hipError_t launch_build(uint32_t dim, int metric, int which, uint32_t grid, const BuildArgs& a, hipStream_t s) {
+#define SHINE_CASE(DD) \
+  if (dim == DD) return launch_build_d##DD(which, metric, grid, a, s);
+  SHINE_DIMS(SHINE_CASE)
+#undef SHINE_CASE
+  return hipErrorInvalidValue;
+}
+
 namespace {
 
 __global__ __launch_bounds__(256) void cache_drop_kernel(const uint32_t* ids, uint32_t n, uint32_t* cslot) {

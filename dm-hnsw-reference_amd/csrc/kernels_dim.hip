@@ -1,6 +1,9 @@
 // One vector dimension's kernel instantiations (built once per dimension with -DSHINE_DIM=D; see kernels.h), or,
 // with -DSHINE_BYTES=2 / 3, that dimension's byte-row (u8 / i8) instantiations.
 #include "kernels_impl.h"
+#ifndef SHINE_BYTES
+#include "build_impl.h"
+#endif
 
 #ifndef SHINE_DIM
 #error "build with -DSHINE_DIM=<dimension>"
@@ -50,6 +53,11 @@ hipError_t SHINE_CAT(launch_distance_d, SHINE_DIM)(int metric, int elem, const D
     return metric == 0 ? launch_distance_t<SHINE_DIM, 0, __half>(a, s) : launch_distance_t<SHINE_DIM, 1, __half>(a, s);
 #endif
   return hipErrorInvalidValue;
+}
+
+hipError_t SHINE_CAT(launch_build_d, SHINE_DIM)(int which, int metric, uint32_t grid, const BuildArgs& a,
+                                                hipStream_t s) {
+  return metric == 0 ? launch_build_t<SHINE_DIM, 0>(which, grid, a, s) : launch_build_t<SHINE_DIM, 1>(which, grid, a, s);
 }
 
 #endif

@@ -100,6 +100,33 @@ class GraphStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved0"}
 
 
+class GpuBuildStats(C.Structure):
+    _fields_ = [
+        ("num_nodes", C.c_uint64),
+        ("num_upper_rows", C.c_uint64),
+        ("batches", C.c_uint64),
+        ("upper_lists", C.c_uint64),
+        ("requests", C.c_uint64),
+        ("rows_appended", C.c_uint64),
+        ("rows_pruned", C.c_uint64),
+        ("pools_truncated", C.c_uint64),
+        ("upper_beams_stopped", C.c_uint64),
+        ("search_failures", C.c_uint64),
+        ("distcomps", C.c_uint64),
+        ("max_level", C.c_uint32),
+        ("entry_uid", C.c_uint32),
+        ("ms_total", C.c_double),
+        ("ms_search", C.c_double),
+        ("ms_upper", C.c_double),
+        ("ms_select", C.c_double),
+        ("ms_sort", C.c_double),
+        ("ms_prune", C.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 P = C.c_void_p
 U32, U64, I32 = C.c_uint32, C.c_uint64, C.c_int
 PU8 = C.POINTER(C.c_uint8)
@@ -141,6 +168,14 @@ PROTOTYPES = {
     "shine_build_distcomps": (U64, [P]),
     "shine_build_write": (I32, [P, C.c_char_p, U32, U32]),
     "shine_build_free": (I32, [P]),
+    "shine_gpu_build": (I32, [P, I32, U64, U32, U32, U32, I32, U32, I32, C.c_double, U32, C.POINTER(P)]),
+    "shine_gpu_build_get_stats": (I32, [P, C.POINTER(GpuBuildStats)]),
+    "shine_gpu_build_dumps": (I32, [P, U32]),
+    "shine_gpu_build_dump_size": (U64, [P, U32]),
+    "shine_gpu_build_dump_data": (P, [P, U32]),
+    "shine_gpu_build_write": (I32, [P, C.c_char_p]),
+    "shine_gpu_build_open": (I32, [P, I32, C.POINTER(P)]),
+    "shine_gpu_build_free": (I32, [P]),
 }
 
 _lib = None

@@ -75,6 +75,87 @@ def tti_like(n: int, seed: int = 1, d: int = 200) -> np.ndarray:
     return (x * np.float32(0.8)).astype(np.float32)
 
 
+_KINDS = {
+    # kind: (latent, centres, spectrum, model_key, cs, post)
+    "sift_like": (64, 1024, 0.35, 1, 1.0, "sift"),
+    "deep_like": (32, 512, 0.5, 2, 2.5, "unit"),
+    "tti_like": (48, 512, 0.5, 3, 2.5, "tti"),
+}
+
+
+def generate_device(kind: str, n: int, seed: int = 1, d: int | None = None, device: str = "cuda", chunk: int = 1 << 22):
+    """The same model as `kind` (sift_like / deep_like / tti_like: centres, spectrum and projection from the fixed model
+    seed) sampled with torch on the GPU, for 10M-100M-record workloads whose numpy generation would take minutes of host
+    time and tens of GB of host memory.  Draws come from torch's generator, so the rows differ from the numpy
+    functions' rows of the same seed; the distribution is the same.  Returns a float32 tensor (n, d) on `device`."""
+    import torch
+    latent, centres, spectrum, key, cs, post = _KINDS[kind]
+    d = d or {"sift_like": 128, "deep_like": 96, "tti_like": 200}[kind]
+    C, scale, P = _model(d, latent, centres, spectrum, cs, key)
+    Ct = torch.from_numpy(C).to(device)
+    st = torch.from_numpy(scale).to(device)
+    Pt = torch.from_numpy(P.T.copy()).to(device)
+    g = torch.Generator(device=device)
+    g.manual_seed(int(seed))
+    out = torch.empty((n, d), dtype=torch.float32, device=device)
+    sstd = None
+    if post == "sift":
+        if d not in _sift_std:
+            _sift_std[d] = _model_std(d, latent, centres, spectrum, key, cs)
+        sstd = _sift_std[d]
+    for s in range(0, n, chunk):
+        m = min(chunk, n - s)
+        lab = torch.randint(0, centres, (m,), generator=g, device=device)
+        z = (Ct[lab] + torch.randn((m, latent), generator=g, device=device)) * st
+        x = z @ Pt
+        if post == "sift":
+            x = torch.clamp(torch.round(x * (40.0 / sstd) + 50.0), 0.0, 255.0) + 0.0
+        else:
+            x = x / torch.clamp(torch.linalg.vector_norm(x, dim=1, keepdim=True), min=1e-12)
+            if post == "tti":
+                x = x * 0.8
+        out[s:s + m] = x
+        del lab, z, x
+    return out
+
+
+def ground_truth_device(base, queries, k: int, metric: int, qblock: int = 512, bchunk: int = 1 << 23,
+                        refine: int = 32):
+    """Exact top-k of every query over a GPU-resident base of any size: f32 distances per (query block, base chunk)
+    keep the `refine` best candidates per query, whose distances are then recomputed in float64 and the best k taken
+    (ties by id).  The candidates are a superset of the true top-k unless more than `refine` - k rows fall within the
+    f32 error of the k-th distance.  metric 0 = squared L2, 1 = 1 - <q, x>.  Returns an (nq, k) int64 numpy array."""
+    import torch
+    nq, n = queries.shape[0], base.shape[0]
+    out = np.empty((nq, k), dtype=np.int64)
+    for qs in range(0, nq, qblock):
+        q = queries[qs:qs + qblock]
+        qn = (q * q).sum(1, keepdim=True)
+        cand_d, cand_i = [], []
+        for bs in range(0, n, bchunk):
+            b = base[bs:bs + bchunk]
+            dot = q @ b.T
+            dist = qn + (b * b).sum(1)[None, :] - 2.0 * dot if metric == 0 else 1.0 - dot
+            r = min(refine, dist.shape[1])
+            v, i = torch.topk(dist, r, dim=1, largest=False)
+            cand_d.append(v)
+            cand_i.append(i + bs)
+            del dot, dist
+        ci = torch.cat(cand_i, 1)
+        cd = torch.cat(cand_d, 1)
+        _, sel = torch.topk(cd, min(refine, cd.shape[1]), dim=1, largest=False)
+        ci = torch.gather(ci, 1, sel)
+        rows = base[ci].double()                       # (qb, refine, d)
+        q64 = q.double()[:, None, :]
+        exact = ((rows - q64) ** 2).sum(2) if metric == 0 else 1.0 - (rows * q64).sum(2)
+        ex = exact.cpu().numpy()
+        ids = ci.cpu().numpy()
+        for r in range(ex.shape[0]):
+            o = np.lexsort((ids[r], ex[r]))[:k]
+            out[qs + r] = ids[r][o]
+    return out
+
+
 def brute_force_knn(base: np.ndarray, queries: np.ndarray, k: int, metric: int = 0, chunk: int = 256):
     """Exact top-k (ties by id), distances in f64.  metric 0 = squared L2, 1 = 1 - <q, x>."""
     b = base.astype(np.float64)

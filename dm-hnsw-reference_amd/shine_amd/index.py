@@ -207,6 +207,67 @@ def build(base: np.ndarray, M: int, ef_construction: int, metric: int = L.METRIC
     return dumps, dc
 
 
+class GpuBuild:
+    """shine_gpu_build: the GPU batch builder (HNSW::insert on one MI355X, include/shine_gpu.h).  `base` is a numpy
+    array (host rows) or an integer device pointer to n x dim f32 rows on GPU `gpu` (then n and dim are required).
+    Use `open()` for a search handle over the built graph, `dumps()` for the reference's dump images."""
+
+    def __init__(self, base, M: int, ef_construction: int, metric: int = L.METRIC_L2, seed: int = 1234, gpu: int = 0,
+                 n: int | None = None, dim: int | None = None, batch_fraction: float = 0.0, max_batch: int = 0):
+        self._h = C.c_void_p()
+        if isinstance(base, np.ndarray):
+            b = np.ascontiguousarray(base, dtype=np.float32)
+            n, dim = b.shape
+            ptr, on_dev = _ptr(b), 0
+        else:
+            if n is None or dim is None:
+                raise ValueError("a device pointer needs n and dim")
+            ptr, on_dev = C.c_void_p(int(base)), 1
+        self.n, self.dim, self.M, self.efc = int(n), int(dim), M, ef_construction
+        L.check(L.lib().shine_gpu_build(ptr, on_dev, self.n, self.dim, M, ef_construction, metric, seed, gpu,
+                                        float(batch_fraction), int(max_batch), C.byref(self._h)))
+        self.metric = metric
+
+    def stats(self) -> dict:
+        st = L.GpuBuildStats()
+        L.check(L.lib().shine_gpu_build_get_stats(self._h, C.byref(st)))
+        return st.as_dict()
+
+    def dumps(self, n_shards: int = 1) -> list[np.ndarray]:
+        L.check(L.lib().shine_gpu_build_dumps(self._h, n_shards))
+        out = []
+        for s in range(n_shards):
+            n = L.lib().shine_gpu_build_dump_size(self._h, s)
+            p = L.lib().shine_gpu_build_dump_data(self._h, s)
+            out.append(np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(n,)).copy())
+        return out
+
+    def write(self, directory: str) -> None:
+        L.check(L.lib().shine_gpu_build_write(self._h, str(directory).encode()))
+
+    def open(self, elem: int = L.ELEM_F32) -> "Index":
+        h = C.c_void_p()
+        L.check(L.lib().shine_gpu_build_open(self._h, elem, C.byref(h)))
+        return Index(h.value, self.dim, self.metric)
+
+    def close(self):
+        if self._h is not None and self._h.value:
+            L.lib().shine_gpu_build_free(self._h)
+        self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def plan_regions(dumps, dim: int, M: int, metric: int, k: int) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
     """Host-only region planner of SHINE_PLACE_SHARDED_REGIONS: fetch_level(500) + balanced k-means.
     Returns (centroids [k or 2k, dim], region of every uid, region of every centroid)."""

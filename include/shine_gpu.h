@@ -315,6 +315,56 @@ uint64_t shine_build_distcomps(shine_build_t b);
 int shine_build_write(shine_build_t b, const char* dir, uint32_t M, uint32_t ef_construction); /* dump/ files */
 int shine_build_free(shine_build_t b);
 
+/* ----------------------------------------------------------------------------------------------------------
+ * GPU batch build (SURVEY §8f row 2 at 10M-100M records): HNSW::insert (hnsw.hh:40-251) and select_heuristic
+ * (:482-522) on one MI355X.  Levels are drawn exactly as shine_build draws them (std::mt19937(seed), hnsw.hh:48; the
+ * first record takes level 0 and a record above the top level takes top + 1, :56-111).  Records are inserted in id
+ * order in batches of consecutive ids, every record of a batch against the graph as it stood before the batch:
+ * level-0 candidates come from the fast search kernel (knn with k = ef = ef_construction), upper levels from a beam
+ * kernel, select_heuristic(M) gives each record its lists, and the reverse edges of a batch are applied per target
+ * row (appended, or the row re-pruned with select_heuristic(m_max) over its old and new entries together).  A record
+ * that raises the top level is inserted alone, so the entry-point protocol (:56-111, 234-248) is the reference's.
+ * Deterministic for fixed inputs.  Batches hold floor(batch_fraction x records already inserted) records (at least 1,
+ * at most max_batch; 0 / 0 = defaults 0.02 and 1 << 20).
+ * base: n x dim f32 rows, on the host (base_on_device = 0) or in device memory of GPU gpu_id (1: read during the call
+ * only).  The result stays on that GPU: open it as a search handle (shine_gpu_build_open) and / or write the reference's
+ * dump layout (shine_gpu_build_dumps, memory node of each record drawn like shine_build's).
+ * -------------------------------------------------------------------------------------------------------- */
+typedef struct shine_gpu_builder* shine_gpu_build_t;
+typedef struct shine_gpu_build_stats {
+  uint64_t num_nodes;
+  uint64_t num_upper_rows;       /* neighbour lists at levels >= 1 */
+  uint64_t batches;
+  uint64_t upper_lists;          /* upper-level candidate lists searched */
+  uint64_t requests;             /* reverse-edge requests (selected neighbours) */
+  uint64_t rows_appended;        /* target rows that took their new entries as appends */
+  uint64_t rows_pruned;          /* target rows re-pruned with select_heuristic(m_max) */
+  uint64_t pools_truncated;      /* re-prunes whose old + new entries exceeded 64 (the 64 closest were kept) */
+  uint64_t upper_beams_stopped;  /* upper-level beams stopped by a full visited table */
+  uint64_t search_failures;      /* level-0 searches that ended with a status (none expected) */
+  uint64_t distcomps;            /* distance computations of the level-0 searches */
+  uint32_t max_level, entry_uid;
+  double ms_total;               /* wall time of shine_gpu_build */
+  /* device time per phase, with SHINE_BUILD_PROFILE=1 (each batch then waits for its phases); else 0 */
+  double ms_search, ms_upper, ms_select, ms_sort, ms_prune;
+} shine_gpu_build_stats;
+int shine_gpu_build(const float* base, int base_on_device, uint64_t n, uint32_t dim, uint32_t M,
+                    uint32_t ef_construction, int metric, uint32_t seed, int gpu_id, double batch_fraction,
+                    uint32_t max_batch, shine_gpu_build_t* out);
+int shine_gpu_build_get_stats(shine_gpu_build_t b, shine_gpu_build_stats* out);
+/* The reference's dump images ([free_ptr | ep_ptr | records], memory_node.hh:15-27, 185-201) of the built index over
+ * n_shards memory nodes, in host memory (records in id order within each node). */
+int shine_gpu_build_dumps(shine_gpu_build_t b, uint32_t n_shards);
+uint64_t shine_gpu_build_dump_size(shine_gpu_build_t b, uint32_t shard);
+const uint8_t* shine_gpu_build_dump_data(shine_gpu_build_t b, uint32_t shard);
+/* <dir>/dump/index_m{M}_efc{efC}_node{i}_of{N}.dat (compute_node.cc:426-430) from shine_gpu_build_dumps' images */
+int shine_gpu_build_write(shine_gpu_build_t b, const char* dir);
+/* The built index as a search handle (replica on the build's GPU; elem F32, F16, U8 or I8, the last two only when every
+ * component is exactly such a byte value).  The device arrays move into the handle: afterwards the build handle keeps
+ * its dump images and statistics only. */
+int shine_gpu_build_open(shine_gpu_build_t b, int elem, shine_index_t* out);
+int shine_gpu_build_free(shine_gpu_build_t b);
+
 #ifdef __cplusplus
 }
 #endif

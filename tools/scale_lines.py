@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""BASELINE.json configs at full size on one MI355X, with indexes built by the GPU batch builder (shine_gpu_build).
+
+  cmp1m    SIFT-shaped 1M x 128, M=16, efC=200: the CPU builder (16 threads) and the GPU builder on the same rows;
+           recall@10 at ef=128 of both (fast mode, 10K queries), build times, and the oracle's knn on the GPU-built
+           dump against exact mode on a sample (bitwise)
+  cfg3     DEEP-shaped 10M x 96, inner product, ef=256, batch 4096 (configs[2])
+  cfg4     DEEP-shaped 100M x 96, L2, ef=128, batch 1024 (configs[3]), one replica: 51 GB of rows + lists
+  cfg5     TTI-shaped 50M x 200, inner product, fp16 rows, ef=250, batch 1024, Zipf alpha 1.0 query mix (configs[4])
+  cfg5_10m the cfg5 shape at 10M records, one replica (the fp16 / d=200 kernel on its own)
+
+Rows are generated on the GPU (shine_amd.datasets.generate_device), the index is built from them in HBM, ground truth
+comes from an f32 scan refined in float64, and the timed search reuses tools/config_lines.py's measure(): four batches
+in flight, HIP events, algorithmic bytes over the launches' span.  One JSON line per workload and mode.
+
+Usage: python tools/scale_lines.py --which cfg4 [--n 100000000] [--out gpurun_out/scale_lines.jsonl]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "dm-hnsw-reference_amd"))
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tools"))
+sys.path.insert(0, str(ROOT / "oracle"))
+from bench import host_threads, log  # noqa: E402
+from config_lines import Heartbeat, measure  # noqa: E402
+
+WORKLOADS = {
+    # name: kind, n, dim, metric, elem, M, efc, ef, batch, zipf alpha (None: plain queries)
+    "cfg3": ("deep_like", 10_000_000, 96, 1, 0, 16, 200, 256, 4096, None),
+    "cfg4": ("deep_like", 100_000_000, 96, 0, 0, 16, 200, 128, 1024, None),
+    "cfg5": ("tti_like", 50_000_000, 200, 1, 1, 16, 200, 250, 1024, 1.0),
+    "cfg5_10m": ("tti_like", 10_000_000, 200, 1, 1, 16, 200, 250, 1024, 1.0),
+}
+
+
+def build_gpu(torch, shine_amd, base_t, M, efc, metric, a, label):
+    n, dim = base_t.shape
+    t0 = time.time()
+    with Heartbeat(f"{label}: GPU build {n} x {dim}"):
+        gb = shine_amd.GpuBuild(base_t.data_ptr(), M, efc, metric, seed=1234, n=n, dim=dim,
+                                batch_fraction=a.batch_fraction, max_batch=a.max_batch)
+    wall = time.time() - t0
+    st = gb.stats()
+    st["wall_s"] = wall
+    st["inserts_per_s"] = n / wall
+    log(f"{label}: built {n} x {dim} in {wall:.1f}s ({st['batches']} batches, {n / wall / 1e6:.2f} M inserts/s)")
+    return gb, st
+
+
+def queries(torch, D, kind, dim, nq, alpha):
+    if alpha is None:
+        return D.generate_device(kind, nq, seed=2, d=dim)
+    pool = D.generate_device(kind, 500_000, seed=2, d=dim).cpu().numpy()  # skew.py's query pool (500k)
+    q, _, _ = D.zipf_query_mix(pool, nq, alpha, seed=3)
+    return torch.from_numpy(np.ascontiguousarray(q)).cuda()
+
+
+def run(name, a):
+    import torch
+    import shine_amd
+    from shine_amd import datasets as D
+    kind, n, dim, metric, elem, M, efc, ef, batch, alpha = WORKLOADS[name]
+    n = a.n or n
+    base_t = D.generate_device(kind, n, seed=1, d=dim)
+    nq = batch * a.nbatches
+    q = queries(torch, D, kind, dim, nq, alpha)
+    with Heartbeat(f"{name}: ground truth"):
+        gt = D.ground_truth_device(base_t, q, a.k, metric)
+    gb, st = build_gpu(torch, shine_amd, base_t, M, efc, metric, a, name)
+    del base_t
+    torch.cuda.empty_cache()
+    idx = gb.open(elem)
+    gb.close()
+    ns = argparse.Namespace(**{**vars(a), "ef": a.ef or str(ef), "nbatches": a.nbatches})
+    lines = []
+    for line in measure(torch, idx, name, ns, q, gt, batch, 1, ef):
+        line["config"].update({"generator": kind, "n": n, "dim": dim, "metric": "IP" if metric else "L2", "M": M,
+                               "efc": efc, "placement": "replica", "gpu_slots": [0],
+                               "zipf_alpha": alpha, "queries": nq})
+        line["dtype"] = "f16 records, f32 accumulate" if elem == 1 else "f32"
+        line["build"] = st
+        line["data"] = "synthetic (GPU-generated, seeded); index built in-run on the GPU (shine_gpu_build)"
+        log(json.dumps(line))
+        lines.append(line)
+    idx.close()
+    return lines
+
+
+def run_cmp1m(a):
+    """CPU builder vs GPU builder on the same 1M SIFT-shaped rows (VERDICT r3 item 1's acceptance)."""
+    import torch
+    import shine_amd
+    from shine_amd import datasets as D
+    import oracle as O
+    L = shine_amd._lib
+    n, dim, M, efc, ef, k = a.n or 1_000_000, 128, 16, 200, 128, a.k
+    base = D.sift_like(n, seed=1, d=dim)
+    q = D.sift_like(10_240, seed=2, d=dim)
+    base_t = torch.from_numpy(base).cuda()
+    qd = torch.from_numpy(q).cuda()
+    gt = D.ground_truth_device(base_t, qd, k, 0)
+    t0 = time.time()
+    with Heartbeat("cmp1m: CPU build"):
+        cpu_dumps, _ = shine_amd.build(base, M, efc, 0, 1, seed=1234, threads=host_threads())
+    cpu_s = time.time() - t0
+    gb, st = build_gpu(torch, shine_amd, base_t, M, efc, 0, a, "cmp1m")
+    gpu_dumps = gb.dumps(1)
+    line = {"workload": "cmp1m", "n": n, "dim": dim, "M": M, "efc": efc, "ef": ef, "queries": int(q.shape[0]),
+            "cpu_build_s": cpu_s, "cpu_build_threads": host_threads(), "gpu_build": st}
+    res = {}
+    for label, dumps in (("cpu", cpu_dumps), ("gpu", gpu_dumps)):
+        with shine_amd.Index.from_buffers(dumps, dim, M, 0, gpus=[0]) as idx:
+            idx.set_search_mode(L.MODE_FAST)
+            r = idx.knn(q, k, ef)
+            res[label] = r
+            line[f"recall_{label}"] = D.recall_at_k(r.ids, gt, k)
+            line[f"mean_distcomps_{label}"] = float(r.qstats[:, 0].mean())
+            for e2 in (32, 48, 64):
+                line[f"recall_{label}_ef{e2}"] = D.recall_at_k(idx.knn(q, k, e2).ids, gt, k)
+            if label == "gpu":
+                idx.set_search_mode(L.MODE_EXACT)
+                ex = idx.knn(q[:512], k, ef)
+                ref_ids, ref_d, ref_qs = O.OracleIndex(dumps, dim, M, 0).knn(q[:512], k, ef, threads=host_threads())
+                line["oracle_equals_exact_on_gpu_dump"] = bool(
+                    np.array_equal(ex.ids, ref_ids) and np.array_equal(ex.dists.view(np.uint32), ref_d.view(np.uint32))
+                    and np.array_equal(ex.qstats[:, :5], ref_qs[:, :5]))
+                line["oracle_sample"] = 512
+    line["recall_gap"] = line["recall_cpu"] - line["recall_gpu"]
+    gs = shine_amd.graph_stats(gpu_dumps, dim, M)
+    line["gpu_graph"] = gs
+    line["cpu_graph"] = shine_amd.graph_stats(cpu_dumps, dim, M)
+    gb.close()
+    log(json.dumps(line))
+    return [line]
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--which", default="cmp1m")
+    p.add_argument("--n", type=int, default=0, help="override the workload's record count")
+    p.add_argument("--k", type=int, default=10)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=4)
+    p.add_argument("--nbatches", type=int, default=10)
+    p.add_argument("--ef", default="")
+    p.add_argument("--modes", default="fast,exact")
+    p.add_argument("--inflight", type=int, default=4)
+    p.add_argument("--batch-fraction", type=float, default=0.0)
+    p.add_argument("--max-batch", type=int, default=0)
+    p.add_argument("--out", default=str(ROOT / "gpurun_out" / "scale_lines.jsonl"))
+    a = p.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    Path(a.out).parent.mkdir(parents=True, exist_ok=True)
+    for name in a.which.split(","):
+        for line in (run_cmp1m(a) if name == "cmp1m" else run(name, a)):
+            print(json.dumps(line), flush=True)
+            with open(a.out, "a") as f:
+                f.write(json.dumps(line) + "\n")
+
+
+if __name__ == "__main__":
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    main()
