@@ -578,6 +578,9 @@ def main():
                          "mean_distcomps_per_query": float(qs_h[:, 0].mean())},
             "cpu_baseline": cpu,
             "hw_queues": HW_QUEUES or "HIP default (4)",
+            # provenance of the measured library: its source hash must equal the tree's (a stale .so is visible here)
+            "build_id": shine_amd._lib.build_id(),
+            "tree_source_hash": shine_amd._lib.source_hash(),
         }
     idx.close()
     if dist:

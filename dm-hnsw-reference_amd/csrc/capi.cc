@@ -561,9 +561,12 @@ uint32_t learned_table(const Scratch& S) {
 // config_lines_cfg3_10m_final.jsonl), and a table sized for the maximum holds half the wavefronts per CU.  Never below
 // the floor a call that exhausted the spill bitmaps set.
 uint32_t learned_mean_table(const Scratch& S) {
-  // (the visited sum is a u32 word: calls of more than 2^20 queries could wrap it, and learn nothing here)
-  if (!S.seen.p || !S.seen.p[3] || !S.last_nq || S.last_nq > (1u << 20) || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
-  const uint32_t mean = S.seen.p[5] / S.last_nq;
+  // (the visited sum is a u32 word of per-query counts capped at 16,384: calls of up to 2^18 queries cannot wrap it;
+  // seen[6] is the queries of the call that wrote the sum, which need not be the last one enqueued)
+  if (!S.seen.p || !S.seen.p[3] || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
+  const uint32_t nq = S.seen.p[6];
+  if (nq == 0 || nq > (1u << 18)) return 0;
+  const uint32_t mean = S.seen.p[5] / nq;
   if (mean == 0) return 0;
   return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, pow2_at_least(mean + mean / 4 + 64)}));
 }
@@ -860,7 +863,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     a.log_cap = kLogCap;
     a.counter = S.counter.p + i;
     a.vis_max = S.counter.p + 3;
-    a.vis_sum = S.counter.p + 8;
+    a.vis_sum = i == 0 ? S.counter.p + 8 : nullptr;  // the main pass's queries only: a hand-on counts once
     a.fast = pass == PASS_FAST ? 1u : 0u;
     a.vis16 = sh.vis16;
     a.vis_bits = sh.vis_bits;
@@ -999,6 +1002,11 @@ int search_enqueue(shine_index* h, uint32_t slot, const float* d_q, uint32_t nq,
 }
 
 void index_release(shine_index* h) { release_index(h); }
+
+int index_from_graph(HostGraph&& G, int elem, const int* gpu_ids, uint32_t n_gpus, int placement, double cache_fraction,
+                     shine_index_t* out) {
+  return make_index(std::move(G), elem, gpu_ids, n_gpus, placement, cache_fraction, out);
+}
 
 }  // namespace shine
 
@@ -1306,6 +1314,13 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     std::vector<std::string> errs(G);
     std::vector<std::thread> th;
     th.reserve(G);
+    // Device-API searches on other streams of a slot may still be reading the arena: the updates below rewrite its
+    // rows and cslot, so every stream of the slot drains first (as shine_cache_update does).  Those calls' logged
+    // misses are applied here too.
+    for (uint32_t r = 0; r < G; ++r) {
+      HIP_TRY(hipSetDevice(h->reps[r].device));
+      HIP_TRY(hipDeviceSynchronize());
+    }
     for (uint32_t r = 0; r < G; ++r)
       th.emplace_back([&, r] {
         per[r] = shine_stats{};

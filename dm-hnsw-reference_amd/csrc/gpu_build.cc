@@ -581,6 +581,77 @@ int shine_gpu_build_open(shine_gpu_build_t b, int elem, shine_index_t* out) {
   return SHINE_OK;
 }
 
+int shine_gpu_build_open_ex(shine_gpu_build_t b, uint32_t n_shards, int elem, const int* gpu_ids, uint32_t n_gpus,
+                            int placement, double cache_fraction, shine_index_t* out) {
+  if (!b || !out) return set_error(SHINE_ERR_ARG, "NULL argument");
+  if (!b->h) return set_error(SHINE_ERR_ARG, "the built arrays already moved into an index handle");
+  if (n_shards == 0 || n_shards > 65535) return set_error(SHINE_ERR_ARG, "n_shards must be in [1, 65535]");
+  const uint64_t N = b->N;
+  const uint32_t dim = b->dim, M = b->M, M0 = b->M0;
+  Replica& R = b->h->reps[0];
+  HIP_TRY(hipSetDevice(R.device));
+  HIP_TRY(hipStreamSynchronize(R.stream));
+  try {
+    // the records as the dump parser would lay them out (graph.cc parse_dumps): memory node s's records in id order,
+    // node1's first, every list entry a dense id; memory nodes drawn as shine_gpu_build_dumps draws them
+    std::mt19937 shard_rng(b->seed ^ 0x9E3779B9u);
+    std::uniform_int_distribution<uint32_t> sd(0, n_shards - 1);
+    std::vector<uint32_t> shard(N);
+    std::vector<uint64_t> start(n_shards + 1, 0);
+    for (uint64_t i = 0; i < N; ++i) {
+      shard[i] = sd(shard_rng);
+      ++start[shard[i] + 1];
+    }
+    for (uint32_t s = 0; s < n_shards; ++s) start[s + 1] += start[s];
+    std::vector<uint32_t> dense(N);
+    {
+      std::vector<uint64_t> fill(start.begin(), start.end() - 1);
+      for (uint64_t i = 0; i < N; ++i) dense[i] = static_cast<uint32_t>(fill[shard[i]]++);
+    }
+    std::vector<float> vdev(N * dim);
+    std::vector<uint32_t> adj0(N * M0), adjU(b->R * M);
+    HIP_TRY(hipMemcpy(vdev.data(), R.vec.p, vdev.size() * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(adj0.data(), R.adj0.p, adj0.size() * 4, hipMemcpyDeviceToHost));
+    if (!adjU.empty()) HIP_TRY(hipMemcpy(adjU.data(), R.adjU.p, adjU.size() * 4, hipMemcpyDeviceToHost));
+    HostGraph G;
+    G.L.dim = dim;
+    G.L.M = M;
+    G.metric = b->metric;
+    G.N = N;
+    G.n_shards = n_shards;
+    G.shard_start = start;
+    G.vec.resize(N * dim);
+    G.uid.resize(N);
+    G.level.resize(N);
+    G.up_base.resize(N);
+    G.adj0.assign(N * M0, kInvalid);
+    std::vector<uint32_t> perm(dim);
+    for (uint32_t k = 0; k < dim; ++k) perm[k] = permuted_index(dim, k);
+    for (uint64_t i = 0; i < N; ++i) {
+      const uint64_t g = dense[i];
+      const float* row = vdev.data() + i * dim;
+      float* dst = G.vec.data() + g * dim;
+      for (uint32_t k = 0; k < dim; ++k) dst[k] = row[perm[k]];
+      G.uid[g] = static_cast<uint32_t>(i);
+      G.level[g] = b->level[i];
+      G.up_base[g] = b->up_base[i];  // the upper rows keep the build's order: rows are reached through up_base only
+      for (uint32_t j = 0; j < M0; ++j) {
+        const uint32_t x = adj0[i * M0 + j];
+        G.adj0[g * M0 + j] = x == kInvalid ? kInvalid : dense[x];
+      }
+    }
+    G.adjU.resize(adjU.size());
+    for (size_t j = 0; j < adjU.size(); ++j) G.adjU[j] = adjU[j] == kInvalid ? kInvalid : dense[adjU[j]];
+    G.ep = dense[b->ep];
+    G.ep_level = b->ep_level;
+    G.lists_unique = true;
+    std::vector<float>().swap(vdev);
+    return index_from_graph(std::move(G), elem, gpu_ids, n_gpus, placement, cache_fraction, out);
+  } catch (const std::bad_alloc&) {
+    return set_error(SHINE_ERR_NOMEM, "out of host memory for the host graph");
+  }
+}
+
 int shine_gpu_build_free(shine_gpu_build_t b) {
   delete b;
   return SHINE_OK;

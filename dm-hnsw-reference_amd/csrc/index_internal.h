@@ -219,6 +219,9 @@ struct IndexState {
 int search_enqueue(shine_index* h, uint32_t slot, const float* d_q, uint32_t nq, uint32_t k, uint32_t ef,
                    uint32_t* d_ids, float* d_dists, uint32_t* d_qs, hipStream_t s);
 void index_release(shine_index* h);
+// An index handle over a host graph (as shine_open_buffers_ex builds one from parsed dumps).
+int index_from_graph(HostGraph&& G, int elem, const int* gpu_ids, uint32_t n_gpus, int placement, double cache_fraction,
+                     shine_index_t* out);
 
 }  // namespace shine
 

@@ -73,7 +73,7 @@ struct SearchArgs {
   uint32_t* access;          // cache warmup (nullable): per device id, reads of the record (vector or list)
   uint32_t* call_counters;   // last pass of a call (nullable): the call's kCallWords counter words; the last workgroup
   uint32_t* host_counts;     // to finish copies words 4..6 to host_counts[0..2] (host memory), sets host_counts[3] = 1,
-                             // copies words 3 and 8 to host_counts[4] and [5] and zeroes the words for the next call
+                             // copies words 3 and 8 to host_counts[4] and [5], the call's nq to [6], and zeroes the words for the next call
                              // on the stream (word 7 counts finished groups)
   uint32_t* vis_max;         // every pass (nullable): the call's counter word 3, the most nodes any query marked
                              // visited (atomicMax per query) — sizes the next call's visited tables

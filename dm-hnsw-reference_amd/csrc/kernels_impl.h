@@ -408,12 +408,26 @@ __device__ __forceinline__ void load_byte_row(NbrBuf<D, E, P>& B, int p, const E
   }
 }
 
-// Issue the loads of pass p: this lane's group evaluates node `id` (INV: nothing to load).
-template <int D, typename E, int P>
-__device__ __forceinline__ void issue_pass(NbrBuf<D, E, P>& B, int p, const E* __restrict__ vec, u32 id, int c4) {
+// Off-stripe record x of a dynamic-cache view (DevGraph::cslot): its arena row when cached, else its xGMI row.
+__device__ __forceinline__ u32 read_class(const DevGraph& g, u32 x, u32 cached);
+template <int D, typename E>
+__device__ __forceinline__ const E* cached_row(const DevGraph& g, const E* row, u32 x) {
+  if (read_class(g, x, 0u) == 2u) {
+    const u32 c = g.cslot[x];
+    if (c != INV) return static_cast<const E*>(g.cvec) + static_cast<u64>(c) * kRowElems<D, E>;
+  }
+  return row;
+}
+
+// Issue the loads of pass p: this lane's group evaluates node `id` (INV: nothing to load).  CACHE (the ACCT = 2 kernels
+// of a dynamic-cache view): a cached off-stripe record is read from this GPU's arena, as the read accounting counts it.
+template <int D, typename E, int P, bool CACHE = false>
+__device__ __forceinline__ void issue_pass(NbrBuf<D, E, P>& B, int p, const E* __restrict__ vec, u32 id, int c4,
+                                           const DevGraph* cg = nullptr) {
   using L = Lay<D, E>;
   if (id != INV) {
     const E* row = vec + static_cast<u64>(id) * kRowElems<D, E>;
+    if constexpr (CACHE) row = cached_row<D, E>(*cg, row, id);
     if constexpr (kByte<E>) {
       load_byte_row<D, E, P>(B, p, row, c4);
     } else {
@@ -583,15 +597,15 @@ __device__ __forceinline__ void pass_dists(const QueryRegs<D, E>& Q, const NbrBu
 }
 
 // slots p0 .. p0 + 16P - 1 of the list (those below n)
-template <int D, int METRIC, typename E, int P>
+template <int D, int METRIC, typename E, int P, bool CACHE = false>
 __device__ __forceinline__ void dist_chunk(const E* __restrict__ vec, const QueryRegs<D, E>& Q, const u32* sc_ids,
-                                           float* sc_d, int p0, int n, int lane) {
+                                           float* sc_d, int p0, int n, int lane, const DevGraph* cg = nullptr) {
   const int g4 = lane >> 2, c4 = lane & 3;
   NbrBuf<D, E, P> B;
 #pragma unroll
   for (int p = 0; p < P; ++p) {
     const int slot = p0 + 16 * p + g4;
-    issue_pass<D, E, P>(B, p, vec, slot < n ? sc_ids[slot] : INV, c4);
+    issue_pass<D, E, P, CACHE>(B, p, vec, slot < n ? sc_ids[slot] : INV, c4, cg);
   }
   float out[P];
   pass_dists<D, METRIC, E, P>(Q, B, out);
@@ -605,12 +619,12 @@ __device__ __forceinline__ void dist_chunk(const E* __restrict__ vec, const Quer
 // sc_d[j] = dist(q, vec[sc_ids[j]]) for j < n.  All 64 lanes must call it.  Two passes (32 slots) at a time while
 // more than 16 remain, then one: a list of <= 16 fresh nodes (an upper-level
 // list, most level-0 expansions of the heap kernel) costs one pass of VALU instead of two.
-template <int D, int METRIC, typename E>
+template <int D, int METRIC, typename E, bool CACHE = false>
 __device__ __forceinline__ void dist_list(const E* __restrict__ vec, const QueryRegs<D, E>& Q, const u32* sc_ids,
-                                          float* sc_d, int n, int lane) {
+                                          float* sc_d, int n, int lane, const DevGraph* cg = nullptr) {
   int p0 = 0;
-  for (; n - p0 > 16; p0 += 32) dist_chunk<D, METRIC, E, 2>(vec, Q, sc_ids, sc_d, p0, n, lane);
-  if (p0 < n) dist_chunk<D, METRIC, E, 1>(vec, Q, sc_ids, sc_d, p0, n, lane);
+  for (; n - p0 > 16; p0 += 32) dist_chunk<D, METRIC, E, 2, CACHE>(vec, Q, sc_ids, sc_d, p0, n, lane, cg);
+  if (p0 < n) dist_chunk<D, METRIC, E, 1, CACHE>(vec, Q, sc_ids, sc_d, p0, n, lane, cg);
 }
 
 // Exact visited set (hashset_t<RemotePtr>, types.hh:14-15) on dense node ids.
@@ -740,7 +754,7 @@ __device__ __forceinline__ void entry_and_descent(const SearchArgs& A, const E* 
   if (lane == 0) sc_ids[0] = ep;
   count_vec_reads<ACCT>(A, rc, lane == 0, ep, qi, true);
   wave_sync();
-  dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, 1, lane);
+  dist_list<D, METRIC, E, ACCT == 2>(vec, Q, sc_ids, sc_d, 1, lane, &A.g);
   wave_sync();
   closest = sc_d[0];
   ++st_dist;
@@ -764,7 +778,7 @@ __device__ __forceinline__ void entry_and_descent(const SearchArgs& A, const E* 
       if (valid) sc_ids[lane] = e;
       count_vec_reads<ACCT>(A, rc, valid, e, qi, true);  // upper-level lists are replicated: only vectors can be remote
       wave_sync();
-      dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, cnt, lane);
+      dist_list<D, METRIC, E, ACCT == 2>(vec, Q, sc_ids, sc_d, cnt, lane, &A.g);
       wave_sync();
       // first neighbour (list order) attaining the minimum; adopted only if strictly closer (:378)
       float bd = (lane < cnt) ? sc_d[lane] : __builtin_inff();
@@ -866,6 +880,13 @@ struct VisitedLds<0> {
       if (x < A.g.N) atomicOr(&bits[x >> 5], 1u << (x & 31));
     }
   }
+  // the table's ids back out of the bitmap (whole words to zero: the bitmap goes back all zero)
+  __device__ __forceinline__ void unspill(u32* __restrict__ bits, const SearchArgs& A, int lane) const {
+    for (u32 i = lane; i <= mask; i += 64) {
+      const u32 x = t[i];
+      if (x < A.g.N) bits[x >> 5] = 0u;
+    }
+  }
   __device__ __forceinline__ bool at_home(u32 x) const { return t[vhash(x, shift)] == x; }
   // the word at x's home slot (one read); home_match: x sits at home in that word
   __device__ __forceinline__ u32 probe(u32 x) const { return t[vhash(x, shift)]; }
@@ -926,6 +947,20 @@ struct VisitedLds<1> {
         const u32 home = (b - (v & ((1u << dbits) - 1u))) & bmask_b;
         const u32 x = (((home << rbits) | (v >> dbits)) * A.vis_mul_inv) & bmask;
         if (x < A.g.N) atomicOr(&bits[x >> 5], 1u << (x & 31));
+      }
+    }
+  }
+  __device__ __forceinline__ void unspill(u32* __restrict__ bits, const SearchArgs& A, int lane) const {
+    const u32 nw = A.vis_cap >> 1;
+    for (u32 i = lane; i < nw; i += 64) {
+      const u32 w = t[i], b = i >> 2;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const u32 v = half ? (w >> 16) : (w & 0xFFFFu);
+        if (v == 0xFFFFu) continue;
+        const u32 home = (b - (v & ((1u << dbits) - 1u))) & bmask_b;
+        const u32 x = (((home << rbits) | (v >> dbits)) * A.vis_mul_inv) & bmask;
+        if (x < A.g.N) bits[x >> 5] = 0u;
       }
     }
   }
@@ -1031,6 +1066,7 @@ __device__ __forceinline__ void finish_call(const SearchArgs& A, int lane) {
   host[2] = h2;
   host[4] = __atomic_load_n(&c[3], __ATOMIC_RELAXED);
   host[5] = __atomic_load_n(&c[8], __ATOMIC_RELAXED);
+  host[6] = A.nq;  // the call the sum belongs to (several calls may be in flight on the stream)
   host[3] = 1u;
 #pragma unroll
   for (int i = 0; i < static_cast<int>(kCallWords); ++i) __atomic_store_n(&c[i], 0u, __ATOMIC_RELAXED);
@@ -1050,6 +1086,38 @@ __device__ __forceinline__ int claim_spill_bitmap(const SearchArgs& A, int lane)
   }
   got = bcast(got);
   return got == INV ? -1 : static_cast<int>(got);
+}
+
+// Every bit a query sets in its spill bitmap after the spill is logged in the bitmap's vlog row (SearchArgs::vlog, free
+// while the main pass runs: only the fallback passes use it, later on the stream), so that handing the bitmap back
+// zeroes the table's ids and the logged ones only — O(visited) instead of the whole id space (12.5 MB per spilled query
+// at 100M ids).  A log past log_cap falls back to zeroing every word.
+__device__ __forceinline__ void spill_log(const SearchArgs& A, int sslot, u32& n, bool active, u32 id, int lane) {
+  const u64 m = __ballot(active);
+  if (!m) return;
+  const u64 below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  if (active) {
+    const u32 pos = n + static_cast<u32>(__popcll(m & below));
+    if (pos < A.log_cap) A.vlog[static_cast<u64>(sslot) * A.log_cap + pos] = id;
+  }
+  n += static_cast<u32>(__popcll(m));
+}
+
+// Hand the spill bitmap back all zero, then drop its flag (every lane stores the same flag word: see the fast kernel).
+template <class VTab>
+__device__ __forceinline__ void spill_release(const VTab& vt, const SearchArgs& A, int sslot, u32 n, int lane) {
+  u32* sb = A.visited + static_cast<u64>(sslot) * A.words_per_slot;
+  if (n > A.log_cap) {
+    for (u64 w = lane; w < A.words_per_slot; w += 64) sb[w] = 0u;
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the log's stores, before its loads
+    vt.unspill(sb, A, lane);
+    const u32* lg = A.vlog + static_cast<u64>(sslot) * A.log_cap;
+    for (u32 i = lane; i < n; i += 64) sb[__hip_atomic_load(&lg[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 5] = 0u;
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __threadfence();
+  __hip_atomic_store(&A.spill_flags[sslot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int D, int METRIC, typename E, int VIS, int ACCT, int VT = 0, bool PROF = false>
@@ -1095,6 +1163,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
     u32 st_dist = 0, st_vup = 0, st_vl0 = 0, st_lup = 0, st_ll0 = 0, st_maxnext = 0, status = 0;
     ReadCount rc;
     int sslot = -1;  // VIS == 0: the spill bitmap this query holds (wave-uniform), -1 = the LDS table
+    u32 slog = 0;    // ids logged since the spill (spill_log)
 
     // ---- entry point + greedy descent (hnsw.hh:256-287) ---------------------------------------------------
     PHASE(1)
@@ -1170,6 +1239,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
             fresh = (atomicOr(&bm[e >> 5], bit) & bit) == 0;
           }
         }
+        if (VIS == 0 && sslot >= 0) spill_log(A, sslot, slog, fresh, e, lane);
         if constexpr (VIS == 0) {
           // In-place spill (as the fast kernel): the table is too full, or an id landed too far from its home
           // bucket — the table moves to an HBM bitmap and the query goes on there instead of being handed to the
@@ -1188,6 +1258,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
               const u32 bit = 1u << (e & 31);
               fresh = (atomicOr(&sb[e >> 5], bit) & bit) == 0u;
             }
+            spill_log(A, sslot, slog, vovf, e, lane);
           }
         }
         const u64 fm = __ballot(fresh);
@@ -1209,7 +1280,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         if (nf == 0) continue;
         PHASE(4)
         wave_sync();
-        dist_list<D, METRIC, E>(vec, Q, sc_ids, sc_d, nf, lane);
+        dist_list<D, METRIC, E, ACCT == 2>(vec, Q, sc_ids, sc_d, nf, lane, &A.g);
         wave_sync();
         PHASE(5)
         // lane j < nf holds fresh neighbour j (list order)
@@ -1306,7 +1377,9 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
     }
     if (status == ST_OVERFLOW && A.out_list && lane == 0) A.out_list[atomicAdd(A.out_count, 1u)] = qi;
     if (A.vis_max && lane == 0) atomicMax(A.vis_max, nvis);
-    if (A.vis_sum && lane == 0) atomicAdd(A.vis_sum, nvis);  // visited-table occupancy, for the next call's shape
+    // visited-table occupancy, for the next call's shape (capped at the largest table, so that the call's sum cannot
+    // wrap below 2^18 queries)
+    if (A.vis_sum && lane == 0) atomicAdd(A.vis_sum, nvis < 16384u ? nvis : 16384u);
     if (A.qstats && lane == 0) {
       u32* qs = A.qstats + static_cast<u64>(qi) * kQsWords;
       qs[0] = st_dist;
@@ -1320,14 +1393,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
       write_read_counts(qs, rc);
     }
 
-    if (VIS == 0 && sslot >= 0) {  // hand the spill bitmap back all zero (as the fast kernel, which explains why
-                                   // every lane stores the flag)
-      u32* sb = A.visited + static_cast<u64>(sslot) * A.words_per_slot;
-      for (u64 w = lane; w < A.words_per_slot; w += 64) sb[w] = 0u;
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      __threadfence();
-      __hip_atomic_store(&A.spill_flags[sslot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (VIS == 0 && sslot >= 0) spill_release(vt, A, sslot, slog, lane);  // the bitmap back all zero
     if (VIS >= 1) {  // visited_nodes.clear() (:475): clear exactly the words this query touched
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (!log_overflow) {
@@ -1395,10 +1461,7 @@ __device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restri
                                            const DevGraph& g) {
   if constexpr (ACCT == 2) {  // dynamic cache: each lane resolves its own list slot to a row, the groups share it
     const E* row = vec + static_cast<u64>(e == INV ? pad : e) * kRowElems<D, E>;
-    if (e != INV && read_class(g, e, 0u) == 2u) {
-      const u32 c = g.cslot[e];
-      if (c != INV) row = static_cast<const E*>(g.cvec) + static_cast<u64>(c) * kRowElems<D, E>;
-    }
+    if (e != INV) row = cached_row<D, E>(g, row, e);
     const u64 rp = reinterpret_cast<u64>(row);
 #pragma unroll
     for (int p = 0; p < P; ++p) {
@@ -1502,6 +1565,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHINE_FAST_M
     // (Plain code, no lambda: a bitmap pointer assigned through a lambda's reference capture compiled to a constant
     // null base on this toolchain.)
     int sslot = -1;  // the bitmap this query holds (wave-uniform), -1 = the LDS table
+    u32 slog = 0;    // ids logged since the spill (spill_log)
 
     while (status == 0) {
       ++st_ll0;  // read_neighborlist (:436-438)
@@ -1527,6 +1591,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHINE_FAST_M
           const u32 bit = 1u << (e & 31);
           fresh = (atomicOr(&sb[e >> 5], bit) & bit) == 0u;
         }
+        spill_log(A, sslot, slog, fresh, e, lane);
       } else if constexpr (VT == 1) {
         if (cand) {
           const int r = ehint_known ? vis.begin(e, ehint, pw, pexp, pold) : 2;
@@ -1551,6 +1616,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHINE_FAST_M
         EVENT(3)
         if (lost) atomicOr(&sb[e >> 5], 1u << (e & 31));
         pw = INV;
+        spill_log(A, sslot, slog, lost || vovf, e, lane);
         if (vovf) {
           const u32 bit = 1u << (e & 31);
           fresh = (atomicOr(&sb[e >> 5], bit) & bit) == 0u;
@@ -1596,6 +1662,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHINE_FAST_M
           vis.spill(sb, A, lane);
           EVENT(3)
           if (vovf) atomicOr(&sb[e >> 5], 1u << (e & 31));
+          spill_log(A, sslot, slog, vovf, e, lane);
         }
       }
 
@@ -1770,7 +1837,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHINE_FAST_M
     }
     if (status == ST_OVERFLOW && A.out_list && lane == 0) A.out_list[atomicAdd(A.out_count, 1u)] = qi;
     if (A.vis_max && lane == 0) atomicMax(A.vis_max, nvis);
-    if (A.vis_sum && lane == 0) atomicAdd(A.vis_sum, nvis);  // visited-table occupancy, for the next call's shape
+    // visited-table occupancy, for the next call's shape (capped at the largest table, so that the call's sum cannot
+    // wrap below 2^18 queries)
+    if (A.vis_sum && lane == 0) atomicAdd(A.vis_sum, nvis < 16384u ? nvis : 16384u);
     if (A.qstats && lane == 0) {
       u32* qs = A.qstats + static_cast<u64>(qi) * kQsWords;
       qs[0] = st_dist;
@@ -1783,16 +1852,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHINE_FAST_M
       qs[7] = status == 0 ? static_cast<u32>(cs < static_cast<int>(A.k) ? cs : A.k) : 0u;
       write_read_counts(qs, rc);
     }
-    if (sslot >= 0) {  // hand the bitmap back all zero: the stores land before the flag drops
-      u32* sb = A.visited + static_cast<u64>(sslot) * A.words_per_slot;
-      for (u64 w = lane; w < A.words_per_slot; w += 64) sb[w] = 0u;
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      __threadfence();
-      // Every lane stores the same zero (one dword).  A lane-0 branch here, the last statement of the item loop,
-      // was jump-threaded into the next item's lane-0 fetch: the wave split, lanes 1-63 ran an item without lane 0
-      // and faulted (tests/test_gpu_fast.py::test_fast_mode_spills_in_place_and_stays_exact).
-      __hip_atomic_store(&A.spill_flags[sslot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    // Hand the bitmap back all zero: the stores land before the flag drops.  Every lane stores the same zero flag
+    // (one dword): a lane-0 branch there, the last statement of the item loop, was jump-threaded into the next item's
+    // lane-0 fetch, the wave split, lanes 1-63 ran an item without lane 0 and faulted
+    // (tests/test_gpu_fast.py::test_fast_mode_spills_in_place_and_stays_exact).
+    if (sslot >= 0) spill_release(vis, A, sslot, slog, lane);
   }
   clk.flush(A.prof, lane);
   finish_call(A, lane);

@@ -161,6 +161,7 @@ PROTOTYPES = {
     "shine_close": (I32, [P]),
     "shine_selftest_heap": (I32, [I32, P, P, P, U32, U32, P, P, P]),
     "shine_last_error": (C.c_char_p, []),
+    "shine_build_id": (C.c_char_p, []),
     "shine_graph_stats_buffers": (I32, [C.POINTER(PU8), C.POINTER(U64), U32, U32, U32, C.POINTER(GraphStats)]),
     "shine_build": (I32, [P, U64, U32, U32, U32, I32, U32, U32, U32, C.POINTER(P)]),
     "shine_build_dump_size": (U64, [P, U32]),
@@ -175,6 +176,7 @@ PROTOTYPES = {
     "shine_gpu_build_dump_data": (P, [P, U32]),
     "shine_gpu_build_write": (I32, [P, C.c_char_p]),
     "shine_gpu_build_open": (I32, [P, I32, C.POINTER(P)]),
+    "shine_gpu_build_open_ex": (I32, [P, U32, I32, C.POINTER(I32), U32, I32, C.c_double, C.POINTER(P)]),
     "shine_gpu_build_free": (I32, [P]),
 }
 
@@ -212,6 +214,22 @@ def _one_hip_runtime() -> None:
 def check(rc: int) -> None:
     if rc != OK:
         raise ShineError(rc, lib().shine_last_error().decode(errors="replace"))
+
+
+def build_id() -> str:
+    """The loaded library's provenance (shine_build_id): "src <source hash> git <head at build time>"."""
+    return lib().shine_build_id().decode()
+
+
+def source_hash() -> str:
+    """The source hash the Makefile would compile into a library built from this tree (csrc/Makefile SRC_HASH)."""
+    import hashlib
+    csrc = PKG_ROOT / "csrc"
+    names = sorted(p.name for p in csrc.iterdir() if p.is_file() and p.suffix in (".cc", ".h", ".hip"))
+    h = hashlib.sha1()
+    for path in [csrc / n for n in names] + [HEADER, csrc / "Makefile"]:
+        h.update(path.read_bytes())
+    return h.hexdigest()[:16]
 
 
 def declared_symbols() -> list[str]:

@@ -250,6 +250,16 @@ class GpuBuild:
         L.check(L.lib().shine_gpu_build_open(self._h, elem, C.byref(h)))
         return Index(h.value, self.dim, self.metric)
 
+    def open_ex(self, n_shards: int = 1, elem: int = L.ELEM_F32, gpus=None, placement: str = "replica",
+                cache: float = 0.0) -> "Index":
+        """shine_gpu_build_open_ex: any placement (e.g. sharded over GPU slots), the records on n_shards memory nodes
+        as dumps(n_shards) would put them; the build keeps its arrays."""
+        g, ng = _gpus(gpus)
+        h = C.c_void_p()
+        L.check(L.lib().shine_gpu_build_open_ex(self._h, n_shards, elem, g, ng, _placement(placement), float(cache),
+                                                C.byref(h)))
+        return Index(h.value, self.dim, self.metric)
+
     def close(self):
         if self._h is not None and self._h.value:
             L.lib().shine_gpu_build_free(self._h)

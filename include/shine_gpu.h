@@ -206,7 +206,8 @@ int shine_cache_warmup(shine_index_t h, const float* queries, const uint32_t* qu
  *   (stream-ordered before the next call on the slot's stream); random draws come from SplitMix64 seeded with
  *   `seed` + slot, so runs are reproducible (oracle/cache_ref.py restates the policy).  Results never depend on it.
  *   Needs a sharded handle of >= 2 slots opened with cache_fraction 0.  Device-API calls (shine_knn_batch_device)
- *   read the cache but their misses are applied only by shine_cache_update. */
+ *   read the cache; their logged misses are applied by the next shine_cache_update or shine_knn_batch, which first
+ *   wait for every stream of the device (the update rewrites arena rows a search in flight could be reading). */
 #define SHINE_CACHE_STATIC 0
 #define SHINE_CACHE_DYNAMIC 1
 int shine_set_cache_policy(shine_index_t h, int policy, double ratio_percent, uint64_t seed);
@@ -286,6 +287,9 @@ int shine_selftest_heap(int is_max, const int32_t* ops, const float* vals, const
 
 const char* shine_last_error(void);
 
+/* Provenance of this library: "src <hash of every source it was built from> git <head at build time>". */
+const char* shine_build_id(void);
+
 /* Host-only graph diagnostics over dump images (no device needed): how much of the index a search can reach.
  * A level-0 search follows level-0 lists only (hnsw.hh:436-438) from where the greedy descent ends, so a record
  * outside reachable_l0 can never be returned, whatever ef.  Used to tell an index property from a search bug. */
@@ -363,6 +367,11 @@ int shine_gpu_build_write(shine_gpu_build_t b, const char* dir);
  * component is exactly such a byte value).  The device arrays move into the handle: afterwards the build handle keeps
  * its dump images and statistics only. */
 int shine_gpu_build_open(shine_gpu_build_t b, int elem, shine_index_t* out);
+/* The built index under any placement of shine_open_ex (e.g. SHINE_PLACE_SHARDED over 8 GPUs): the records spread over
+ * n_shards memory nodes exactly as shine_gpu_build_dumps spreads them, laid out as shine_open_buffers_ex lays out those
+ * dumps — without writing or parsing them.  The build handle keeps its arrays (shine_gpu_build_open may follow). */
+int shine_gpu_build_open_ex(shine_gpu_build_t b, uint32_t n_shards, int elem, const int* gpu_ids, uint32_t n_gpus,
+                            int placement, double cache_fraction, shine_index_t* out);
 int shine_gpu_build_free(shine_gpu_build_t b);
 
 #ifdef __cplusplus

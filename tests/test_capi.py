@@ -23,6 +23,30 @@ def test_library_exports_every_declared_symbol():
     assert set(L.PROTOTYPES) == set(declared)
 
 
+def test_library_was_built_from_this_tree():
+    """shine_build_id carries the hash of every source the library was built from: a stale libshine_gpu.so (sources
+    edited after the build) fails here instead of being measured."""
+    bid = L.build_id().split()
+    assert bid[0] == "src" and bid[2] == "git", bid
+    assert bid[1] == L.source_hash(), f"libshine_gpu.so was built from other sources ({bid[1]} != {L.source_hash()})"
+
+
+def test_gpu_builder_rejects_bad_arguments():
+    import ctypes as C
+    h = C.c_void_p()
+    lib = L.lib()
+    base = (C.c_float * 16)()
+    assert lib.shine_gpu_build(None, 0, 10, 16, 8, 32, 0, 1, 0, 0.0, 0, C.byref(h)) == L.ERR_ARG
+    assert lib.shine_gpu_build(base, 0, 1, 16, 8, 32, 0, 1, 0, 0.0, 0, C.byref(h)) == L.ERR_ARG   # n < 2
+    assert lib.shine_gpu_build(base, 0, 10, 16, 1, 32, 0, 1, 0, 0.0, 0, C.byref(h)) == L.ERR_ARG   # M < 2
+    assert lib.shine_gpu_build(base, 0, 10, 16, 8, 600, 0, 1, 0, 0.0, 0, C.byref(h)) == L.ERR_ARG  # efC > 512
+    assert lib.shine_gpu_build(base, 0, 10, 17, 8, 32, 0, 1, 0, 0.0, 0, C.byref(h)) == L.ERR_ARG   # no kernel for dim
+    assert lib.shine_gpu_build(base, 0, 10, 16, 8, 32, 2, 1, 0, 0.0, 0, C.byref(h)) == L.ERR_ARG   # metric
+    assert lib.shine_gpu_build(base, 0, 10, 16, 8, 32, 0, 1, 0, 1.5, 0, C.byref(h)) == L.ERR_ARG   # batch fraction
+    assert lib.shine_gpu_build_dumps(None, 1) == L.ERR_ARG
+    assert lib.shine_gpu_build_open(None, 0, C.byref(h)) == L.ERR_ARG
+
+
 def test_header_has_no_torch_or_hip_types():
     import re
     code = re.sub(r"/\*.*?\*/", "", L.HEADER.read_text(), flags=re.S)  # declarations only, comments dropped

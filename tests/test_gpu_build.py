@@ -141,3 +141,24 @@ def test_gpu_build_from_device_rows_and_row_kinds(gpu_available):
     assert D.recall_at_k(r16.ids, gt, 10) > 0.9
     del bt
     torch.cuda.synchronize()
+
+
+def test_gpu_build_open_ex_equals_its_dumps(gpu_available):
+    """shine_gpu_build_open_ex lays the build out as the dumps of the same memory nodes would be: sharded over two GPU
+    slots (one device: every stripe its own allocation) it answers exactly as those dumps opened the same way, and as
+    the replica."""
+    n, M, efc = 20_000, 8, 64
+    base = D.deep_like(n, seed=51)
+    q = D.deep_like(200, seed=52)
+    with shine_amd.GpuBuild(base, M, efc, 0, seed=3) as gb:
+        dumps = gb.dumps(4)
+        with gb.open_ex(4, gpus=[0, 0], placement="sharded", cache=0.1) as sh, \
+                shine_amd.Index.from_buffers(dumps, 96, M, 0, gpus=[0, 0], placement="sharded", cache=0.1) as shd:
+            a, b = sh.knn(q, 10, 48), shd.knn(q, 10, 48)
+            assert sh.info()["id_space"] == shd.info()["id_space"]
+        with gb.open() as rep:
+            c = rep.knn(q, 10, 48)
+    np.testing.assert_array_equal(a.ids, b.ids)
+    np.testing.assert_array_equal(a.dists.view(np.uint32), b.dists.view(np.uint32))
+    np.testing.assert_array_equal(a.qstats, b.qstats)
+    np.testing.assert_array_equal(a.ids, c.ids)

@@ -1,4 +1,4 @@
-"""Properties at a larger scale (200K SIFT-shaped records, M=16, ef=128, the bench's search parameters).
+"""Properties at a larger scale (200K SIFT-shaped records, M=16, efC=200, ef=128: the bench's build and search parameters).
 
 Size-independent checks, cheap enough for the GPU suite:
 * exact mode equals the oracle (ids, bitwise distances, counters) on a sample of the queries;
@@ -20,7 +20,7 @@ def test_bench_parameters_at_200k(gpu_available):
     import torch
     base = D.sift_like(200_000, seed=91)
     q = D.sift_like(1024, seed=92)
-    dumps, _ = shine_amd.build(base, 16, 100, 0, 1, seed=8, threads=16)
+    dumps, _ = shine_amd.build(base, 16, 200, 0, 1, seed=8, threads=16)
     with shine_amd.Index.from_buffers(dumps, 128, 16, 0, gpus=[0]) as idx:
         ex = idx.knn(q, 10, 128)
         idx.set_search_mode(L.MODE_FAST)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """BASELINE.json configs at full size on one MI355X, with indexes built by the GPU batch builder (shine_gpu_build).
 
-  cmp1m    SIFT-shaped 1M x 128, M=16, efC=200: the CPU builder (16 threads) and the GPU builder on the same rows;
+  cmp    SIFT-shaped 1M x 128, M=16, efC=200: the CPU builder (16 threads) and the GPU builder on the same rows;
            recall@10 at ef=128 of both (fast mode, 10K queries), build times, and the oracle's knn on the GPU-built
            dump against exact mode on a sample (bitwise)
   cfg3     DEEP-shaped 10M x 96, inner product, ef=256, batch 4096 (configs[2])
@@ -96,41 +96,49 @@ def run(name, a):
     return lines
 
 
-def run_cmp1m(a):
+def run_cmp(a):
     """CPU builder vs GPU builder on the same 1M SIFT-shaped rows (VERDICT r3 item 1's acceptance)."""
     import torch
     import shine_amd
     from shine_amd import datasets as D
     import oracle as O
     L = shine_amd._lib
-    n, dim, M, efc, ef, k = a.n or 1_000_000, 128, 16, 200, 128, a.k
-    base = D.sift_like(n, seed=1, d=dim)
-    q = D.sift_like(10_240, seed=2, d=dim)
+    n, dim, M, efc, ef, k = a.n or 1_000_000, a.cmp_dim, 16, 200, 128, a.k
+    metric = a.cmp_metric
+    base = getattr(D, a.cmp_kind)(n, seed=1, d=dim)
+    q = getattr(D, a.cmp_kind)(10_240, seed=2, d=dim)
     base_t = torch.from_numpy(base).cuda()
     qd = torch.from_numpy(q).cuda()
-    gt = D.ground_truth_device(base_t, qd, k, 0)
+    gt = D.ground_truth_device(base_t, qd, k, metric)
     t0 = time.time()
-    with Heartbeat("cmp1m: CPU build"):
-        cpu_dumps, _ = shine_amd.build(base, M, efc, 0, 1, seed=1234, threads=host_threads())
+    with Heartbeat("cmp: CPU build"):
+        cpu_dumps, _ = shine_amd.build(base, M, efc, metric, 1, seed=1234, threads=host_threads())
     cpu_s = time.time() - t0
-    gb, st = build_gpu(torch, shine_amd, base_t, M, efc, 0, a, "cmp1m")
-    gpu_dumps = gb.dumps(1)
-    line = {"workload": "cmp1m", "n": n, "dim": dim, "M": M, "efc": efc, "ef": ef, "queries": int(q.shape[0]),
-            "cpu_build_s": cpu_s, "cpu_build_threads": host_threads(), "gpu_build": st}
+    line = {"workload": "cmp", "kind": a.cmp_kind, "metric": metric, "n": n, "dim": dim, "M": M, "efc": efc,
+            "ef": ef, "queries": int(q.shape[0]), "cpu_build_s": cpu_s, "cpu_build_threads": host_threads()}
+    builds = [("cpu", cpu_dumps)]
+    for fr in [float(x) for x in a.cmp_fracs.split(",")]:
+        a.batch_fraction = fr
+        gb, st = build_gpu(torch, shine_amd, base_t, M, efc, metric, a, "cmp")
+        label = "gpu" if len(builds) == 1 else f"gpu_frac{fr}"
+        line[f"{label}_build"] = st
+        builds.append((label, gb.dumps(1)))
+        gb.close()
+    gpu_dumps = builds[1][1]
     res = {}
-    for label, dumps in (("cpu", cpu_dumps), ("gpu", gpu_dumps)):
-        with shine_amd.Index.from_buffers(dumps, dim, M, 0, gpus=[0]) as idx:
+    for label, dumps in builds:
+        with shine_amd.Index.from_buffers(dumps, dim, M, metric, gpus=[0]) as idx:
             idx.set_search_mode(L.MODE_FAST)
             r = idx.knn(q, k, ef)
             res[label] = r
             line[f"recall_{label}"] = D.recall_at_k(r.ids, gt, k)
             line[f"mean_distcomps_{label}"] = float(r.qstats[:, 0].mean())
-            for e2 in (32, 48, 64):
+            for e2 in (32, 48, 64, 256):
                 line[f"recall_{label}_ef{e2}"] = D.recall_at_k(idx.knn(q, k, e2).ids, gt, k)
-            if label == "gpu":
+            if label == "gpu" and a.cmp_oracle:
                 idx.set_search_mode(L.MODE_EXACT)
                 ex = idx.knn(q[:512], k, ef)
-                ref_ids, ref_d, ref_qs = O.OracleIndex(dumps, dim, M, 0).knn(q[:512], k, ef, threads=host_threads())
+                ref_ids, ref_d, ref_qs = O.OracleIndex(dumps, dim, M, metric).knn(q[:512], k, ef, threads=host_threads())
                 line["oracle_equals_exact_on_gpu_dump"] = bool(
                     np.array_equal(ex.ids, ref_ids) and np.array_equal(ex.dists.view(np.uint32), ref_d.view(np.uint32))
                     and np.array_equal(ex.qstats[:, :5], ref_qs[:, :5]))
@@ -139,14 +147,13 @@ def run_cmp1m(a):
     gs = shine_amd.graph_stats(gpu_dumps, dim, M)
     line["gpu_graph"] = gs
     line["cpu_graph"] = shine_amd.graph_stats(cpu_dumps, dim, M)
-    gb.close()
     log(json.dumps(line))
     return [line]
 
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--which", default="cmp1m")
+    p.add_argument("--which", default="cmp")
     p.add_argument("--n", type=int, default=0, help="override the workload's record count")
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--steps", type=int, default=20)
@@ -157,13 +164,18 @@ def main():
     p.add_argument("--inflight", type=int, default=4)
     p.add_argument("--batch-fraction", type=float, default=0.0)
     p.add_argument("--max-batch", type=int, default=0)
+    p.add_argument("--cmp-kind", default="sift_like")
+    p.add_argument("--cmp-dim", type=int, default=128)
+    p.add_argument("--cmp-metric", type=int, default=0)
+    p.add_argument("--cmp-oracle", type=int, default=1)
+    p.add_argument("--cmp-fracs", default="0.02", help="cmp: GPU builds at these batch fractions")
     p.add_argument("--out", default=str(ROOT / "gpurun_out" / "scale_lines.jsonl"))
     a = p.parse_args()
     import torch
     torch.cuda.set_device(0)
     Path(a.out).parent.mkdir(parents=True, exist_ok=True)
     for name in a.which.split(","):
-        for line in (run_cmp1m(a) if name == "cmp1m" else run(name, a)):
+        for line in (run_cmp(a) if name == "cmp" else run(name, a)):
             print(json.dumps(line), flush=True)
             with open(a.out, "a") as f:
                 f.write(json.dumps(line) + "\n")
