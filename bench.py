@@ -177,6 +177,8 @@ def parse():
                         "byte values as in the reference's .u8bin inputs); results are bitwise the same")
     p.add_argument("--no-rows-compare", action="store_true",
                    help="skip timing fast mode on the other row storage (byte rows next to f32, or f32 next to bytes)")
+    p.add_argument("--builder", choices=["gpu", "cpu"], default="gpu",
+                   help="index build: the GPU batch builder (seconds) or the parallel CPU restatement of HNSW::insert")
     p.add_argument("--placement", choices=["replica", "sharded"], default="replica")
     p.add_argument("--slots", type=int, default=0, help="sharded leg: GPU slots (default --gpus)")
     p.add_argument("--cache-frac", type=float, default=0.05,
@@ -184,7 +186,9 @@ def parse():
     p.add_argument("--sharded-leg", choices=["auto", "on", "off"], default="auto",
                    help="after the replica measurement, run the cfg-4-shaped sharded leg over the same N GPUs in a child "
                         "process and carry it in the same JSON line (auto: when N > 1)")
-    p.add_argument("--sharded-n", type=int, default=2_000_000, help="sharded leg: records of the DEEP-shaped index")
+    p.add_argument("--sharded-n", type=int, default=10_000_000,
+                   help="sharded leg: records of the DEEP-shaped index (10M: every GPU's stripe of vectors and lists is "
+                        "~640 MB at 8 GPUs, well above the 256 MiB Infinity Cache)")
     # the launcher hands its flags to the rank processes through the environment: torch.distributed.run's own parser
     # would take bench.py's abbreviations (--n) for its options
     extra = json.loads(os.environ.get("SHINE_BENCH_ARGV", "[]"))
@@ -283,7 +287,7 @@ def main():
     import shine_amd
     from shine_amd import datasets as D
 
-    key = hashlib.sha1(f"{a.n}-{a.dim}-{a.M}-{a.efc}-{a.shards}-sift_like-v3".encode()).hexdigest()[:12]
+    key = hashlib.sha1(f"{a.n}-{a.dim}-{a.M}-{a.efc}-{a.shards}-sift_like-v3-{a.builder}".encode()).hexdigest()[:12]
     cache = Path(a.cache) / key
     t0 = time.time()
     base = D.sift_like(a.n, seed=1, d=a.dim)
@@ -292,6 +296,13 @@ def main():
 
     def build():
         t0 = time.time()
+        if a.builder == "gpu":  # the GPU batch builder on this rank's GPU (include/shine_gpu.h shine_gpu_build)
+            with shine_amd.GpuBuild(base, a.M, a.efc, shine_amd.METRIC_L2, seed=1234, gpu=local) as gb:
+                dumps = gb.dumps(a.shards)
+                st = gb.stats()
+            log(f"built index on GPU {local}: {sum(d.size for d in dumps) / 2**20:.0f} MiB in {time.time() - t0:.1f}s "
+                f"({st['batches']} batches, GPU build {st['ms_total'] / 1e3:.2f}s)")
+            return dumps
         dumps, bdc = shine_amd.build(base, a.M, a.efc, shine_amd.METRIC_L2, a.shards, seed=1234,
                                      threads=host_threads())
         log(f"built index: {sum(d.size for d in dumps) / 2**20:.0f} MiB in {time.time() - t0:.1f}s "
@@ -555,7 +566,7 @@ def main():
             "dtype": "f32",
             "rows": rows,
             "data": "synthetic SIFT-shaped (byte-valued f32 records, 1M x 128, as SIFT's .u8bin), random-seeded; "
-                    "index built in-run",
+                    f"index built in-run ({'GPU batch builder' if a.builder == 'gpu' else 'CPU builder'})",
             "recall_at_10": recall,
             **(host or {}),
             "search_mode": modes[0],
@@ -659,25 +670,24 @@ def run_sharded(a):
     gpus, rows = sharded_plan(S, ndev, a.batch * S, a.nbatches)
     phys = len(set(gpus))
     dim, M, efc, ef, shards = 96, 16, 200, 128, 8
-    key = hashlib.sha1(f"{a.n}-{dim}-{M}-{efc}-{shards}-deep_like-l2-v1".encode()).hexdigest()[:12]
-    cache = Path(a.cache) / key
-    base = D.deep_like(a.n, seed=1, d=dim)
-    paths = [cache / "dump" / shine_amd.dump_name(M, efc, i, shards) for i in range(shards)]
-
-    def build():
-        t0 = time.time()
-        dumps, _ = shine_amd.build(base, M, efc, shine_amd.METRIC_L2, shards, seed=1234, threads=host_threads())
-        log(f"built sharded index: {sum(d.size for d in dumps) / 2**20:.0f} MiB in {time.time() - t0:.1f}s")
-        return dumps
-
-    prepare_dumps(paths, 0, None, build)
-    idx = shine_amd.Index.open(paths, dim, M, shine_amd.METRIC_L2, gpus=gpus, placement="sharded", cache=a.cache_frac)
+    # the index is built on GPU 0 by the GPU batch builder (10M records in seconds) and laid out over the slots as its
+    # 8 memory-node dumps would be (shine_gpu_build_open_ex), without writing or parsing them
+    base_t = D.generate_device("deep_like", a.n, seed=1, d=dim)
+    t0 = time.time()
+    gb = shine_amd.GpuBuild(base_t.data_ptr(), M, efc, shine_amd.METRIC_L2, seed=1234, n=a.n, dim=dim)
+    log(f"built the sharded leg's index ({a.n} x {dim}) on GPU 0 in {time.time() - t0:.1f}s")
+    t0 = time.time()
+    idx = gb.open_ex(shards, gpus=gpus, placement="sharded", cache=a.cache_frac)
     info = idx.info()
     log(f"sharded index: {info['num_nodes']} nodes over {S} slots ({phys} GPUs), id space {info['id_space']}, "
-        f"{info['device_bytes'] / 2**20:.0f} MiB per GPU, cache fraction {info['cache_fraction']:.3f}")
+        f"{info['device_bytes'] / 2**20:.0f} MiB per GPU, cache fraction {info['cache_fraction']:.3f}, laid out in "
+        f"{time.time() - t0:.1f}s")
     nb, B, k = a.nbatches, a.batch * S, a.k
-    q = D.deep_like(B * nb, seed=2, d=dim)
-    gt = ground_truth(torch, base, q, k, 0)
+    q_t = D.generate_device("deep_like", B * nb, seed=2, d=dim)
+    gt = D.ground_truth_device(base_t, q_t, k, 0)
+    q = q_t.cpu().numpy()
+    del base_t, q_t
+    torch.cuda.empty_cache()
     qd, ids, qs, streams = [], [], [], []
     for s in range(S):
         dev = torch.device("cuda", gpus[s])
@@ -731,7 +741,7 @@ def run_sharded(a):
         hits, misses = int(st[:, 10:12].sum()), int(st[:, 8:10].sum())
         node_reads = int(st[:, 0].sum())  # every distance computation reads one record (rdma::read_node)
         qps = a.steps * B / el
-        one = one_gpu_rate(a, torch, shine_amd, paths, dim, M, ef, k, q, rows, mode) if mode_name == "fast" else None
+        one = one_gpu_rate(a, torch, shine_amd, gb, dim, M, ef, k, q, rows, mode) if mode_name == "fast" else None
         xgmi_in = 7 * 153e9
         line = {
             "metric": "QPS at recall@10, cfg4-shaped sharded index (DEEP-like 96-d L2, 8 memory-node dumps)",
@@ -740,7 +750,8 @@ def run_sharded(a):
             "scaling": "weak in queries (a.batch per slot per step) over one fixed index",
             "one_gpu_value": one, "speedup_vs_one_gpu": (qps / one) if one else None,
             "dtype": "f32", "search_mode": mode_name, "recall_at_10": recall,
-            "data": f"synthetic DEEP-shaped (L2-normalised f32, {a.n} x 96; N reduced from 100M), index built in-run",
+            "data": f"synthetic DEEP-shaped (L2-normalised f32, {a.n} x 96, GPU-generated; N reduced from 100M), index "
+                    f"built in-run on GPU 0 (shine_gpu_build)",
             "config": {"workload": "cfg4-shaped sharded knn, M=16 efC=200 ef=128 k=10", "n": a.n, "dim": dim,
                        "M": M, "efc": efc, "ef": ef, "k": k, "shards": shards, "batch": B, "batch_per_slot": a.batch,
                        "placement": "sharded", "gpus": gpus, "cache_fraction": info["cache_fraction"],
@@ -761,14 +772,15 @@ def run_sharded(a):
         log(json.dumps(line))
         lines.append(line)
     idx.close()
+    gb.close()
     print(json.dumps(lines[0]), flush=True)
 
 
-def one_gpu_rate(a, torch, shine_amd, paths, dim, M, ef, k, q, rows, mode):
-    """The same dumps as a replica on GPU 0, the same global batches (each slot's share one launch, in flight on
-    rotating streams): the one-GPU rate the sharded leg's speedup is quoted against."""
+def one_gpu_rate(a, torch, shine_amd, gb, dim, M, ef, k, q, rows, mode):
+    """The same index as a replica on GPU 0 (the build's own arrays), the same global batches (each slot's share one
+    launch, in flight on rotating streams): the one-GPU rate the sharded leg's speedup is quoted against."""
     nb, S = len(rows), len(rows[0])
-    with shine_amd.Index.open(paths, dim, M, shine_amd.METRIC_L2, gpus=[0]) as ix:
+    with gb.open_ex(1, gpus=[0]) as ix:
         ix.set_search_mode(mode)
         with torch.cuda.device(0):
             streams = [torch.cuda.Stream() for _ in range(max(1, a.inflight))]

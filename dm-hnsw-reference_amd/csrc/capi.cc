@@ -790,6 +790,17 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   // exact pass hands queries on, for its next_candidates capacity, which a larger table would only shrink
   if (handed && S.last_learned && (S.last_fast || !spill_enabled()))
     S.table_floor = std::max(S.table_floor, 2 * S.last_table);
+  // A learned fast table that sent more than SHINE_FAST_SPILL_PERMILLE / 1000 (default 4) of its call's queries to a
+  // spill bitmap is grown: a spilled query tests and sets every later visit in HBM (random words of an id-space bitmap,
+  // 12.5 MB at 100M ids), which made the call's slowest queries slower still — on the 100M-record DEEP-shaped index at
+  // ef = 128, 4,096 entries (9 wavefronts per CU, ~0.5 % spilled) ran at 2.18 M QPS against 3.44 M with 8,192 entries
+  // (4 per CU) (profiles/r04/diag100m_tables.jsonl).
+  {
+    const uint64_t spilled = S.seen.p[3] ? S.seen.p[7] : 0, seen_nq = S.seen.p[3] ? S.seen.p[6] : 0;
+    const int64_t permille = env_int("SHINE_FAST_SPILL_PERMILLE", 4);
+    if (permille > 0 && spilled && S.last_learned && S.last_fast && spilled * 1000 > seen_nq * static_cast<uint64_t>(permille))
+      S.table_floor = std::max(S.table_floor, 2 * S.last_table);
+  }
   if (ef != S.last_ef) S.table_floor = 0;
   // the fast pass sizes its table for the mean query when it can spill in place; the exact pass keeps the maximum
   // (its tables sized from the mean ran slower, profiles/r03/ab1_merge_spill_tables.jsonl)
@@ -864,6 +875,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     a.counter = S.counter.p + i;
     a.vis_max = S.counter.p + 3;
     a.vis_sum = i == 0 ? S.counter.p + 8 : nullptr;  // the main pass's queries only: a hand-on counts once
+    a.spill_count = i == 0 ? S.counter.p + 9 : nullptr;
     a.fast = pass == PASS_FAST ? 1u : 0u;
     a.vis16 = sh.vis16;
     a.vis_bits = sh.vis_bits;

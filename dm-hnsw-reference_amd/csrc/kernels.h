@@ -44,7 +44,7 @@ struct DevGraph {
 };
 
 // Counter words of one call on a stream (SearchArgs::call_counters).
-constexpr uint32_t kCallWords = 9;
+constexpr uint32_t kCallWords = 10;
 
 // Per-query counter words (u32) written by the search kernels; include/shine_gpu.h SHINE_QS_*.
 constexpr uint32_t kQsWords = 12;
@@ -93,6 +93,8 @@ struct SearchArgs {
   // (the query is handed on to the next pass instead).
   uint32_t* spill_flags;
   uint32_t spill_slots;
+  uint32_t* spill_count;     // main pass (nullable): the call's counter word 9, queries that spilled (copied to
+                             // host_counts[7]): a learned table that spills too often is grown (capi.cc)
 };
 
 struct DistArgs {

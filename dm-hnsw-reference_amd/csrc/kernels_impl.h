@@ -357,12 +357,16 @@ struct ChunkT<__half> {
   using type = uint2;
 };
 
-// The neighbour vectors of P passes (16 slots each) in VGPRs.
+// The neighbour vectors of P passes (16 slots each) in VGPRs.  The scalar tail (distance.hh:112-115, d = 100 / 200) is
+// loaded as whole 16-byte words, one load instruction per 16 bytes instead of one per element (d = 200 fp16 rows: 1
+// load instead of 8 next to the lane's 12 chunk loads), and widened where lane c = 3 adds it.
 template <int D, typename E, int P, bool BYTES = kByte<E>>
 struct NbrBuf {
   using L = Lay<D, E>;
+  static constexpr int TQ = L::TAIL > 0 ? (L::TAIL * static_cast<int>(sizeof(E)) + 15) / 16 : 1;
+  static_assert(L::TAIL * sizeof(E) % 16 == 0, "the tail of a row must be whole 16-byte words");
   typename ChunkT<E>::type x[P][L::NCH];
-  float xt[P][L::TAILA];  // scalar tail, lane c = 3 only
+  uint4 xt[P][TQ];
 };
 // Byte rows: the lane's NCH chunk words (contiguous in the row, kernels.h permuted_index_bytes) and the tail bytes
 // as whole words; widened to f32 where the distances consume them.
@@ -434,9 +438,11 @@ __device__ __forceinline__ void issue_pass(NbrBuf<D, E, P>& B, int p, const E* _
       using C = typename ChunkT<E>::type;
 #pragma unroll
       for (int u = 0; u < L::NCH; ++u) B.x[p][u] = *reinterpret_cast<const C*>(row + u * 16 + c4 * 4);
-      if (c4 == 3) {
+      if constexpr (L::TAIL > 0) {
+        if (c4 == 3) {
 #pragma unroll
-        for (int t = 0; t < L::TAIL; ++t) B.xt[p][t] = to_f32(row[L::DB + t]);
+          for (int t = 0; t < NbrBuf<D, E, P>::TQ; ++t) B.xt[p][t] = reinterpret_cast<const uint4*>(row + L::DB)[t];
+        }
       }
     }
   }
@@ -453,8 +459,10 @@ __device__ __forceinline__ void issue_row(NbrBuf<D, E, P>& B, int p, const E* __
     using C = typename ChunkT<E>::type;
 #pragma unroll
     for (int u = 0; u < L::NCH; ++u) B.x[p][u] = *reinterpret_cast<const C*>(row + u * 16 + c4 * 4);
+    if constexpr (L::TAIL > 0) {
 #pragma unroll
-    for (int t = 0; t < L::TAIL; ++t) B.xt[p][t] = to_f32(row[L::DB + t]);
+      for (int t = 0; t < NbrBuf<D, E, P>::TQ; ++t) B.xt[p][t] = reinterpret_cast<const uint4*>(row + L::DB)[t];
+    }
   }
 }
 
@@ -591,7 +599,16 @@ __device__ __forceinline__ void pass_dists(const QueryRegs<D, E>& Q, const NbrBu
       for (int t = 0; t < L::TAILA; ++t) xt[t] = L::TAIL > 0 ? byte_f32<E>(B.xt[p][t >> 2], t & 3) : 0.f;
       out[p] = add_tail<D, METRIC, E>(Q, xt, fold8(acc[p]));
     } else {
-      out[p] = add_tail<D, METRIC, E>(Q, B.xt[p], fold8(acc[p]));
+      float xt[L::TAILA];
+      if constexpr (L::TAIL > 0) {
+        E te[NbrBuf<D, E, P>::TQ * 16 / sizeof(E)];
+        __builtin_memcpy(te, B.xt[p], sizeof(te));
+#pragma unroll
+        for (int t = 0; t < L::TAIL; ++t) xt[t] = to_f32(te[t]);
+      } else {
+        xt[0] = 0.f;
+      }
+      out[p] = add_tail<D, METRIC, E>(Q, xt, fold8(acc[p]));
     }
   }
 }
@@ -1067,6 +1084,7 @@ __device__ __forceinline__ void finish_call(const SearchArgs& A, int lane) {
   host[4] = __atomic_load_n(&c[3], __ATOMIC_RELAXED);
   host[5] = __atomic_load_n(&c[8], __ATOMIC_RELAXED);
   host[6] = A.nq;  // the call the sum belongs to (several calls may be in flight on the stream)
+  host[7] = __atomic_load_n(&c[9], __ATOMIC_RELAXED);
   host[3] = 1u;
 #pragma unroll
   for (int i = 0; i < static_cast<int>(kCallWords); ++i) __atomic_store_n(&c[i], 0u, __ATOMIC_RELAXED);
@@ -1077,6 +1095,7 @@ __device__ __forceinline__ int claim_spill_bitmap(const SearchArgs& A, int lane)
   if (A.spill_slots == 0) return -1;
   u32 got = INV;
   if (lane == 0) {
+    if (A.spill_count) atomicAdd(A.spill_count, 1u);
     const u32 n = A.spill_slots;
     for (u32 i = 0, j = blockIdx.x % n; i < n; ++i, j = j + 1 == n ? 0u : j + 1)
       if (atomicCAS(&A.spill_flags[j], 0u, 1u) == 0u) {

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""Diagnostics (GPU box): the DEEP-shaped 100M-record index (GPU-built), fast / exact search shapes and timings per ef
-through the host API (kernel time, hand-ons), with the spill on and off, and recall against ground truth.
+"""Diagnostics (GPU box): the DEEP-shaped 100M-record index (GPU-built), QPS with four batches in flight per search
+mode and ef under environment variants (visited-table policy hooks), and recall against float64 ground truth.
 
-Usage: python tools/diag_100m.py [--n 100000000] [--efs 64,128,256]
+Usage: python tools/diag_100m.py [--n 100000000] [--runs fast:128,exact:128] [--envs ";SHINE_DEBUG_NO_SPILL=1"]
 """
 from __future__ import annotations
 
@@ -29,9 +29,9 @@ def main():
     p.add_argument("--kind", default="deep_like")
     p.add_argument("--dim", type=int, default=96)
     p.add_argument("--metric", type=int, default=0)
-    p.add_argument("--efs", default="64,128,256")
-    p.add_argument("--calls", type=int, default=4)
-    p.add_argument("--envs", default=",SHINE_DEBUG_NO_SPILL=1")
+    p.add_argument("--runs", default="fast:64,fast:128,fast:256,exact:128")
+    p.add_argument("--steps", type=int, default=40)
+    p.add_argument("--envs", default=";SHINE_DEBUG_NO_SPILL=1;SHINE_DEBUG_VISCAP=8192")
     a = p.parse_args()
     import torch
     import shine_amd
@@ -49,27 +49,43 @@ def main():
     torch.cuda.empty_cache()
     idx = gb.open()
     qh = q.cpu().numpy()
-    os.environ["SHINE_DEBUG_SHAPE"] = "1"
-    for env in a.envs.split(","):
-        k_, _, v_ = env.partition("=")
-        if k_:
-            os.environ[k_] = v_
-        for mode_name, mode in (("fast", L.MODE_FAST), ("exact", L.MODE_EXACT)):
-            idx.set_search_mode(mode)
-            for ef in [int(x) for x in a.efs.split(",")]:
-                rows = []
-                for c in range(a.calls):
-                    b = c % 4
-                    r = idx.knn(qh[b * 1024:(b + 1) * 1024], 10, ef)
-                    rows.append((r.stats["kernel_ms"], r.stats["overflow_retries"]))
-                rec = D.recall_at_k(r.ids, gt[(b * 1024):(b + 1) * 1024], 10)
-                vis = r.qstats[:, 1].astype(np.int64) + r.qstats[:, 2]
-                log(json.dumps({"env": env, "mode": mode_name, "ef": ef, "kernel_ms": [x[0] for x in rows],
-                                "handed_on": [x[1] for x in rows], "recall": rec,
-                                "visited_mean": float(vis.mean()), "visited_p99": float(np.percentile(vis, 99)),
-                                "visited_max": int(vis.max()), "distcomps": float(r.qstats[:, 0].mean())}))
-        if k_:
-            del os.environ[k_]
+    B, S, nb = 1024, 4, 4
+    ids = torch.empty((nb, B, 10), dtype=torch.int32, device="cuda")
+    qs = torch.zeros((nb, B, L.QS_WORDS), dtype=torch.int32, device="cuda")
+    streams = [torch.cuda.Stream() for _ in range(S)]
+
+    def run(steps, ef):
+        for i in range(steps):
+            b = i % nb
+            idx.knn_device(q[b * B:(b + 1) * B].data_ptr(), B, 10, ef, ids[b].data_ptr(), None, qs[b].data_ptr(),
+                           stream=streams[i % S].cuda_stream)
+
+    for env in a.envs.split(";"):
+        for kv in env.split(","):
+            k_, _, v_ = kv.partition("=")
+            if k_:
+                os.environ[k_] = v_
+        for spec in a.runs.split(","):
+            mode_name, ef = spec.split(":")
+            ef = int(ef)
+            idx.set_search_mode(L.MODE_FAST if mode_name == "fast" else L.MODE_EXACT)
+            run(2 * nb, ef)
+            torch.cuda.synchronize()
+            st = qs.cpu().numpy().view(np.uint32).reshape(-1, L.QS_WORDS)
+            rec = D.recall_at_k(ids.cpu().numpy().view(np.uint32).reshape(-1, 10), gt[:nb * B], 10)
+            t0 = time.perf_counter()
+            run(a.steps, ef)
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            vis = st[:, 1].astype(np.int64) + st[:, 2]
+            log(json.dumps({"env": env, "mode": mode_name, "ef": ef, "qps": a.steps * B / el, "recall": rec,
+                            "failed": int((st[:, 6] != 0).sum()), "visited_mean": float(vis.mean()),
+                            "visited_p99": float(np.percentile(vis, 99)), "visited_max": int(vis.max()),
+                            "distcomps": float(st[:, 0].mean())}))
+        for kv in env.split(","):
+            k_, _, _ = kv.partition("=")
+            if k_:
+                del os.environ[k_]
     idx.close()
     gb.close()
 
