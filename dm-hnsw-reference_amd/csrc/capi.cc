@@ -571,6 +571,15 @@ uint32_t learned_mean_table(const Scratch& S) {
   return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, pow2_at_least(mean + mean / 4 + 64)}));
 }
 
+// The previous call's worst query with 1/8 to spare (large id spaces, see enqueue_search).
+uint32_t learned_max_table(const Scratch& S) {
+  if (!S.seen.p || !S.seen.p[3] || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
+  const uint64_t vmax = S.seen.p[4];
+  if (vmax == 0) return 0;
+  return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, pow2_at_least(static_cast<uint32_t>(
+                                                                                  std::min<uint64_t>(16384, vmax * 9 / 8)))}));
+}
+
 // The exact pass's learned table, with the in-place spill: just the previous call's worst query (eighths/8 × its
 // visited count, SHINE_EXACT_LEARN_EIGHTHS, default 9), never below 2,048 entries (SHINE_EXACT_LEARN_MIN), which then
 // replaces the fixed size in either direction — a query beyond it spills in place instead of being re-run.  At
@@ -790,14 +799,13 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   // exact pass hands queries on, for its next_candidates capacity, which a larger table would only shrink
   if (handed && S.last_learned && (S.last_fast || !spill_enabled()))
     S.table_floor = std::max(S.table_floor, 2 * S.last_table);
-  // A learned fast table that sent more than SHINE_FAST_SPILL_PERMILLE / 1000 (default 4) of its call's queries to a
-  // spill bitmap is grown: a spilled query tests and sets every later visit in HBM (random words of an id-space bitmap,
-  // 12.5 MB at 100M ids), which made the call's slowest queries slower still — on the 100M-record DEEP-shaped index at
-  // ef = 128, 4,096 entries (9 wavefronts per CU, ~0.5 % spilled) ran at 2.18 M QPS against 3.44 M with 8,192 entries
-  // (4 per CU) (profiles/r04/diag100m_tables.jsonl).
+  // Tuning hook (off by default): a learned fast table that sent more than SHINE_FAST_SPILL_PERMILLE / 1000 of its
+  // call's queries to a spill bitmap is grown.  It cost 30 % at cfg 3 (10M ids, batch 4096), where residency matters
+  // more than the spills (profiles/r04/scale_cfg3_cfg5_10m_v2_floor.jsonl), and did not help at 100M ids, where the
+  // u32 table's load was the cost (profiles/r04/diag100m_*.jsonl).
   {
     const uint64_t spilled = S.seen.p[3] ? S.seen.p[7] : 0, seen_nq = S.seen.p[3] ? S.seen.p[6] : 0;
-    const int64_t permille = env_int("SHINE_FAST_SPILL_PERMILLE", 4);
+    const int64_t permille = env_int("SHINE_FAST_SPILL_PERMILLE", 0);
     if (permille > 0 && spilled && S.last_learned && S.last_fast && spilled * 1000 > seen_nq * static_cast<uint64_t>(permille))
       S.table_floor = std::max(S.table_floor, 2 * S.last_table);
   }
@@ -805,7 +813,16 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   // the fast pass sizes its table for the mean query when it can spill in place; the exact pass keeps the maximum
   // (its tables sized from the mean ran slower, profiles/r03/ab1_merge_spill_tables.jsonl)
   const uint32_t learned = ef != S.last_ef ? 0 : learned_exact_table(S, ef);
-  const uint32_t learned_fast = ef != S.last_ef ? 0 : spill_enabled() ? learned_mean_table(S) : learned;
+  // Where a spill bitmap outgrows an XCD's 4 MiB L2 (more than 2^25 ids) a spilled query's later visits are random
+  // atomics that miss L2, each expansion waiting for one: the spilled queries (the longest ones anyway) then set the
+  // batch's time.  There the fast table is sized for the previous call's worst query instead (9/8 of it): on the
+  // 100M-record index at ef = 128, 8,192 entries ran at 3.41 M QPS against 2.36 M with the mean-sized 4,096 (1.98 M
+  // against 1.26 M with one batch in flight, where residency is the same) (profiles/r04/diag100m_tables_inflight.jsonl).
+  const bool l2_bitmap = h->words_per_slot * 4 <= (4ull << 20);
+  const uint32_t learned_fast = ef != S.last_ef                    ? 0
+                                : !spill_enabled()                 ? learned
+                                : l2_bitmap                        ? learned_mean_table(S)
+                                                                   : learned_max_table(S);
   S.last_ef = ef;
   S.last_nq = nq;
   int chain[3], n_pass = 0;

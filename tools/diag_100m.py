@@ -38,7 +38,7 @@ def main():
     from shine_amd import datasets as D
     L = shine_amd._lib
     base = D.generate_device(a.kind, a.n, seed=1, d=a.dim)
-    q = D.generate_device(a.kind, 4096, seed=2, d=a.dim)
+    q = D.generate_device(a.kind, 8192, seed=2, d=a.dim)
     with Heartbeat("gt"):
         gt = D.ground_truth_device(base, q, 10, a.metric)
     t0 = time.time()
@@ -49,16 +49,17 @@ def main():
     torch.cuda.empty_cache()
     idx = gb.open()
     qh = q.cpu().numpy()
-    B, S, nb = 1024, 4, 4
+    B, nb = 1024, 8
     ids = torch.empty((nb, B, 10), dtype=torch.int32, device="cuda")
     qs = torch.zeros((nb, B, L.QS_WORDS), dtype=torch.int32, device="cuda")
-    streams = [torch.cuda.Stream() for _ in range(S)]
+    all_streams = [torch.cuda.Stream() for _ in range(8)]
+    streams = all_streams[:4]
 
     def run(steps, ef):
         for i in range(steps):
             b = i % nb
             idx.knn_device(q[b * B:(b + 1) * B].data_ptr(), B, 10, ef, ids[b].data_ptr(), None, qs[b].data_ptr(),
-                           stream=streams[i % S].cuda_stream)
+                           stream=streams[i % len(streams)].cuda_stream)
 
     for env in a.envs.split(";"):
         for kv in env.split(","):
@@ -66,19 +67,22 @@ def main():
             if k_:
                 os.environ[k_] = v_
         for spec in a.runs.split(","):
-            mode_name, ef = spec.split(":")
+            mode_name, ef, *inf = spec.split(":")
             ef = int(ef)
+            streams = all_streams[:int(inf[0]) if inf else 4]
             idx.set_search_mode(L.MODE_FAST if mode_name == "fast" else L.MODE_EXACT)
             run(2 * nb, ef)
             torch.cuda.synchronize()
             st = qs.cpu().numpy().view(np.uint32).reshape(-1, L.QS_WORDS)
             rec = D.recall_at_k(ids.cpu().numpy().view(np.uint32).reshape(-1, 10), gt[:nb * B], 10)
+            torch.cuda.synchronize()
             t0 = time.perf_counter()
             run(a.steps, ef)
             torch.cuda.synchronize()
             el = time.perf_counter() - t0
             vis = st[:, 1].astype(np.int64) + st[:, 2]
-            log(json.dumps({"env": env, "mode": mode_name, "ef": ef, "qps": a.steps * B / el, "recall": rec,
+            log(json.dumps({"env": env, "mode": mode_name, "ef": ef, "inflight": len(streams), "qps": a.steps * B / el,
+                            "recall": rec,
                             "failed": int((st[:, 6] != 0).sum()), "visited_mean": float(vis.mean()),
                             "visited_p99": float(np.percentile(vis, 99)), "visited_max": int(vis.max()),
                             "distcomps": float(st[:, 0].mean())}))
