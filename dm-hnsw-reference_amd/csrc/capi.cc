@@ -504,6 +504,7 @@ struct LaunchShape {
 
 // spilled visited tables a main pass (fast or exact) may hold at once (SearchArgs::spill_flags)
 constexpr uint32_t kSpillSlots = 64;
+constexpr uint64_t kXcdL2Bytes = 4ull << 20;  // L2 of one XCD (MI355X_MICROARCH.md)
 bool spill_enabled();
 
 // the inverse of an odd multiplier mod 2^32 (Newton: each step doubles the correct low bits)
@@ -813,16 +814,32 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   // the fast pass sizes its table for the mean query when it can spill in place; the exact pass keeps the maximum
   // (its tables sized from the mean ran slower, profiles/r03/ab1_merge_spill_tables.jsonl)
   const uint32_t learned = ef != S.last_ef ? 0 : learned_exact_table(S, ef);
-  // Where a spill bitmap outgrows an XCD's 4 MiB L2 (more than 2^25 ids) a spilled query's later visits are random
-  // atomics that miss L2, each expansion waiting for one: the spilled queries (the longest ones anyway) then set the
-  // batch's time.  There the fast table is sized for the previous call's worst query instead (9/8 of it): on the
-  // 100M-record index at ef = 128, 8,192 entries ran at 3.41 M QPS against 2.36 M with the mean-sized 4,096 (1.98 M
-  // against 1.26 M with one batch in flight, where residency is the same) (profiles/r04/diag100m_tables_inflight.jsonl).
-  const bool l2_bitmap = h->words_per_slot * 4 <= (4ull << 20);
-  const uint32_t learned_fast = ef != S.last_ef                    ? 0
-                                : !spill_enabled()                 ? learned
-                                : l2_bitmap                        ? learned_mean_table(S)
-                                                                   : learned_max_table(S);
+  // The fast table: sized for the previous call's mean query (mean-sized, spilling the rest) or its worst one
+  // (max-sized, 9/8 of it).  A spilled query's later visits are atomics on its HBM bitmap, and the spilled queries are
+  // the longest ones, which set their batch's time: where the max-sized table still holds the wavefronts one batch
+  // puts on a CU it is taken — on the 100M-record index at ef = 128, 8,192 entries ran at 3.41 M QPS against 2.36 M
+  // mean-sized (1.98 M against 1.26 M with one batch in flight, same residency; profiles/r04/
+  // diag100m_tables_inflight.jsonl) — else residency wins and the table is mean-sized: DEEP-shaped 10M at ef = 256 and
+  // batch 4,096 (16 wavefronts per CU wanted) ran at 3.0 M QPS mean-sized against 2.1 M with larger tables (profiles/
+  // r04/scale_cfg3_cfg5_10m_v2_floor.jsonl).  Bucketed u32 tables and HBM hash tables as the spill target were tried and
+  // were slower at both sizes (profiles/r04/*_reverted.jsonl).  SHINE_FAST_TABLE_MAX=0 / 1 forces either (tuning).
+  //   Only where a spill bitmap outgrows an XCD's 4 MiB L2: at 10M ids (1.25 MB bitmaps) the spills stay cheap and the
+  // mean-sized table's residency wins even with one batch (cfg5-shaped 10M at ef = 250: 1.82 M mean-sized against
+  // 1.59 M max-sized, profiles/r04/scale_cfg3_cfg5_10m_v6_maxtable.jsonl).
+  uint32_t learned_fast = 0, learned_mean = 0;
+  if (ef == S.last_ef) {
+    if (!spill_enabled()) {
+      learned_fast = learned;
+    } else {
+      const uint32_t mean_t = learned_mean_table(S), max_t = learned_max_table(S);
+      const uint64_t need = std::min<uint64_t>(16, (nq + R.cus - 1) / R.cus);
+      const bool max_fits = max_t && R.lds_per_cu / search_fast_lds_bytes(max_t, ef, 4) >= need;
+      const bool beyond_l2 = 4ull * h->words_per_slot > kXcdL2Bytes;
+      const int64_t force = env_int("SHINE_FAST_TABLE_MAX", -1);
+      learned_fast = (force == 1 || (force < 0 && max_fits && beyond_l2)) ? max_t : mean_t;
+      learned_mean = mean_t;
+    }
+  }
   S.last_ef = ef;
   S.last_nq = nq;
   int chain[3], n_pass = 0;
@@ -836,7 +853,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     const LaunchShape sh =
         pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu, h->id_space, learned_fast, handed > 0,
                                           elem_is_byte(h->elem))
-                          : pick_shape(h, R, nq, ef, pass, handed, learned, learned_fast);
+                          : pick_shape(h, R, nq, ef, pass, handed, learned, learned_mean);
     if (i == 0) {
       S.last_table = sh.vis_cap;
       S.last_fast = pass == PASS_FAST;
