@@ -1990,6 +1990,9 @@ hipError_t launch_search_acct(uint32_t grid, const SearchArgs& a, hipStream_t s)
       if constexpr (!AC && D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
         if (a.prof && !wide && a.ef > 64 && a.ef <= 128) return runf(search_fast_kernel<D, METRIC, E, 2, 2, AC, VT, true>);
       }
+      if constexpr (!AC && D == 200 && METRIC == 1 && std::is_same_v<E, __half>) {  // cfg5's shape (fp16, IP, ef 250)
+        if (a.prof && !wide && a.ef > 128 && a.ef <= 256) return runf(search_fast_kernel<D, METRIC, E, 4, 2, AC, VT, true>);
+      }
       if (a.ef <= 64)
         return wide ? runf(search_fast_kernel<D, METRIC, E, 1, 4, AC, VT>) : runf(search_fast_kernel<D, METRIC, E, 1, 2, AC, VT>);
       if (a.ef <= 128)

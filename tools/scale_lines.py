@@ -79,20 +79,35 @@ def run(name, a):
     gb, st = build_gpu(torch, shine_amd, base_t, M, efc, metric, a, name)
     del base_t
     torch.cuda.empty_cache()
-    idx = gb.open(elem)
+    lines = []
+    # slots > 1: the same graph as `slots` memory-node dumps under SHINE_PLACE_SHARDED over GPU slots that repeat this
+    # box's device (the 8-slot emulation of configs[3]/[4]); every slot answers 1/slots of each batch.  The replica
+    # goes last: open() moves the build's arrays into it.
+    for slots in sorted({int(s) for s in a.slots.split(",")}, reverse=True):
+        if slots == 1:
+            idx, placement = gb.open(elem), "replica"
+        else:
+            idx, placement = gb.open_ex(slots, elem=elem, gpus=[0] * slots, placement="sharded"), "sharded"
+        lines += run_measure(torch, idx, name, a, q, gt, batch, slots, ef, kind, n, dim, metric, M, efc, placement,
+                             alpha, nq, elem, st)
+        idx.close()
     gb.close()
+    return lines
+
+
+def run_measure(torch, idx, name, a, q, gt, batch, slots, ef, kind, n, dim, metric, M, efc, placement, alpha, nq,
+                elem, st):
     ns = argparse.Namespace(**{**vars(a), "ef": a.ef or str(ef), "nbatches": a.nbatches})
     lines = []
-    for line in measure(torch, idx, name, ns, q, gt, batch, 1, ef):
+    for line in measure(torch, idx, name, ns, q, gt, batch, slots, ef):
         line["config"].update({"generator": kind, "n": n, "dim": dim, "metric": "IP" if metric else "L2", "M": M,
-                               "efc": efc, "placement": "replica", "gpu_slots": [0],
+                               "efc": efc, "placement": placement, "gpu_slots": [0] * slots,
                                "zipf_alpha": alpha, "queries": nq})
         line["dtype"] = "f16 records, f32 accumulate" if elem == 1 else "f32"
         line["build"] = st
         line["data"] = "synthetic (GPU-generated, seeded); index built in-run on the GPU (shine_gpu_build)"
         log(json.dumps(line))
         lines.append(line)
-    idx.close()
     return lines
 
 
@@ -162,6 +177,8 @@ def main():
     p.add_argument("--ef", default="")
     p.add_argument("--modes", default="fast,exact")
     p.add_argument("--inflight", type=int, default=4)
+    p.add_argument("--slots", default="1", help="GPU slots per layout, e.g. 1,8: the same graph as a replica and "
+                                                "as 8 sharded memory-node dumps on this device")
     p.add_argument("--batch-fraction", type=float, default=0.0)
     p.add_argument("--max-batch", type=int, default=0)
     p.add_argument("--cmp-kind", default="sift_like")
