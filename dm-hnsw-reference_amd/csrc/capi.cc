@@ -634,14 +634,24 @@ LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds
   auto resident = [&](uint32_t t, uint32_t entry_bytes) {
     return std::min<uint64_t>(target, lds_per_cu / search_fast_lds_bytes(t, ef, entry_bytes));
   };
+  // test hook: the id space the u16 entries are sized for, widened (SHINE_DEBUG_VIS_BITS=24 puts a small index's ids
+  // through the full 15-bit remainders of 4,096-entry two-choice tables)
+  bits = std::max<uint32_t>(bits, static_cast<uint32_t>(std::min<int64_t>(31, env_int("SHINE_DEBUG_VIS_BITS", 0))));
+  // u16 entries: in linear-probed buckets (VisitedLds<1>, >= 3 distance bits) where the id space allows, else in
+  // two-choice buckets (VisitedLds<2>, a 15-bit remainder and a bucket bit); SHINE_DEBUG_VIS16 = 0 / 1 / 2 forces
+  auto kind16 = [&](uint32_t t) -> uint32_t {
+    return bits <= log2u(t) + 10 ? 1u : bits <= log2u(t) + 12 ? 2u : 0u;
+  };
   const uint32_t t32 = table_for(4), t16 = table_for(2);
-  const bool can16 = env_int("SHINE_DEBUG_VIS16", 1) != 0 && bits <= log2u(t16) + 10;
+  const int64_t force16 = env_int("SHINE_DEBUG_VIS16", -1);
+  const bool can16 = force16 != 0 && kind16(t16) != 0 && (kind16(t16) == 1 || env_int("SHINE_TWO_CHOICE", 1) != 0);
   const uint64_t w32 = resident(t32, 4), w16 = can16 ? resident(t16, 2) : 0;
-  sh.vis16 = can16 && (w16 > w32 || (w16 == w32 && t16 > t32)) ? 1 : 0;
-  if (env_int("SHINE_DEBUG_VIS16", -1) == 1 && can16) sh.vis16 = 1;  // test hook: force the u16 entries
+  sh.vis16 = can16 && (w16 > w32 || (w16 == w32 && t16 > t32)) ? kind16(t16) : 0;
+  if (force16 >= 1 && can16) sh.vis16 = kind16(t16);  // test hook: force the u16 entries
   sh.vis_cap = sh.vis16 ? t16 : t32;
   sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
-  if (sh.vis16 && bits > log2u(sh.vis_cap) + 10) sh.vis16 = 0;  // a forced small table: back to u32 entries
+  if (sh.vis16) sh.vis16 = kind16(sh.vis_cap);  // a forced table size: the entries it allows (0: back to u32)
+  if (force16 == 2 && sh.vis16 == 1 && bits <= log2u(sh.vis_cap) + 12) sh.vis16 = 2;  // test hook: two-choice
   sh.vis_bits = std::max(bits, log2u(sh.vis_cap) + 1);
   const uint64_t need = search_fast_lds_bytes(sh.vis_cap, ef, sh.vis16 ? 2 : 4);
   const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(lds_per_cu / need));

@@ -1064,6 +1064,130 @@ struct VisitedLds<1> {
   }
 };
 
+// VT = 2: u16 entries in two-choice buckets, for id spaces too wide for VT = 1's distance bits (up to 2^(log2(cap) +
+// 12) ids: 4,096 entries in 8 KiB at 24-bit ids, where VT = 1 needs 16,384).  The odd multiply permutes the b-bit id
+// space; the top t bits of the image pick bucket b1, the other r = b - t <= 15 bits (the remainder) are stored with one
+// bit naming the bucket the entry went to: b1, or b2 = b1 ^ alt(remainder), the less filled of the two when the id was
+// inserted (b1 on a tie).  Entries fill a bucket in order and are never removed, so an id in b2 implies that b1 held an
+// entry when it went there: a bucket b1 found empty answers "absent" alone.  The all-ones entry is the empty marker:
+// at r = 15 the remainder 0x7FFF only ever goes to b1.  A lookup reads both buckets (two ds_read_b128 in flight
+// together); both full is an overflow, and the query spills in place.
+struct Bucket2 {
+  uint4 a, b;  // b1, b2 as last read
+};
+template <>
+struct VisitedLds<2> {
+  u32* t;
+  u32 bmask_b, mul, bmask, rbits, rmask, tb;
+  using Hint = Bucket2;
+  __device__ __forceinline__ VisitedLds(void* base, const SearchArgs& A) : t(static_cast<u32*>(base)), mul(A.vis_mul) {
+    tb = 31 - __clz(static_cast<int>(A.vis_cap >> 3));  // buckets of 8 entries
+    bmask_b = (A.vis_cap >> 3) - 1;
+    bmask = A.vis_bits >= 32 ? ~0u : (1u << A.vis_bits) - 1;
+    rbits = A.vis_bits - tb;
+    rmask = (1u << rbits) - 1;
+  }
+  static constexpr u32 kBytes = 2;
+  static __device__ __forceinline__ Hint unknown() {  // guess: both buckets empty
+    return Bucket2{make_uint4(INV, INV, INV, INV), make_uint4(INV, INV, INV, INV)};
+  }
+  __device__ __forceinline__ void clear(const SearchArgs& A, int lane) {
+    uint4* t4 = reinterpret_cast<uint4*>(t);
+    for (u32 i = lane; i < A.vis_cap / 8; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
+  }
+  __device__ __forceinline__ u32 image(u32 x) const { return (x * mul) & bmask; }
+  __device__ __forceinline__ u32 alt(u32 rem) const { return ((rem * 0x85EBCA6Bu) >> (32 - tb)) | 1u; }
+  __device__ __forceinline__ u32 decode(u32 b, u32 v, const SearchArgs& A) const {
+    const u32 rem = v >> 1;
+    const u32 b1 = (v & 1u) ? (b ^ alt(rem)) & bmask_b : b;
+    return (((b1 << rbits) | rem) * A.vis_mul_inv) & bmask;
+  }
+  __device__ __forceinline__ void spill(u32* __restrict__ bits, const SearchArgs& A, int lane) const {
+    const u32 nw = A.vis_cap >> 1;
+    for (u32 i = lane; i < nw; i += 64) {
+      const u32 w = t[i], b = i >> 2;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const u32 v = half ? (w >> 16) : (w & 0xFFFFu);
+        if (v == 0xFFFFu) continue;
+        const u32 x = decode(b, v, A);
+        if (x < A.g.N) atomicOr(&bits[x >> 5], 1u << (x & 31));
+      }
+    }
+  }
+  __device__ __forceinline__ void unspill(u32* __restrict__ bits, const SearchArgs& A, int lane) const {
+    const u32 nw = A.vis_cap >> 1;
+    for (u32 i = lane; i < nw; i += 64) {
+      const u32 w = t[i], b = i >> 2;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const u32 v = half ? (w >> 16) : (w & 0xFFFFu);
+        if (v == 0xFFFFu) continue;
+        const u32 x = decode(b, v, A);
+        if (x < A.g.N) bits[x >> 5] = 0u;
+      }
+    }
+  }
+  __device__ __forceinline__ void insert_first(u32 x) {  // the table is empty: entry 0 of b1
+    const u32 h = image(x);
+    t[(h >> rbits) * 4] = 0xFFFF0000u | ((h & rmask) << 1);
+  }
+  __device__ __forceinline__ uint4 bucket(u32 b) const { return reinterpret_cast<const uint4*>(t)[b]; }
+  __device__ __forceinline__ Hint probe(u32 x) const {
+    const u32 h = image(x), b1 = h >> rbits, b2 = (b1 ^ alt(h & rmask)) & bmask_b;
+    return Bucket2{bucket(b1), bucket(b2)};
+  }
+  __device__ __forceinline__ bool home_match(u32 x, const Hint& w) const {
+    const u32 e = (image(x) & rmask) << 1;
+    return VisitedLds<1>::has(w.a, e) || VisitedLds<1>::has(w.b, e | 1u);
+  }
+  // entries in a bucket (they fill it in order): 2 x the first word with an empty half, + 1 if its low half is taken
+  static __device__ __forceinline__ u32 fill(const uint4& w) {
+    int j;
+    u32 k, word;
+    VisitedLds<1>::first_empty(w, j, k, word);
+    return j < 0 ? 8u : 2u * static_cast<u32>(j) + k;
+  }
+  // from a view of both buckets: 0 = x present, 1 = absent and the compare-and-swap recording it issued (word pw,
+  // expected pexp, returned pold), 2 = absent with both buckets full
+  __device__ __forceinline__ int place(u32 x, const Hint& cur, u32& pw, u32& pexp, u32& pold) const {
+    const u32 h = image(x), rem = h & rmask, b1 = h >> rbits;
+    const u32 e = rem << 1;
+    if (VisitedLds<1>::has(cur.a, e) || VisitedLds<1>::has(cur.b, e | 1u)) return 0;
+    const u32 f1 = fill(cur.a), f2 = fill(cur.b);
+    const bool second = f2 < f1 && rem != 0x7FFFu;
+    if ((second ? f2 : f1) >= 8u) return 2;
+    const uint4& w = second ? cur.b : cur.a;
+    int j;
+    u32 k;
+    VisitedLds<1>::first_empty(w, j, k, pexp);
+    const u32 ent = second ? (e | 1u) : e;
+    pw = (second ? ((b1 ^ alt(rem)) & bmask_b) : b1) * 4 + static_cast<u32>(j);
+    pold = atomicCAS(&t[pw], pexp, k ? ((pexp & 0xFFFFu) | (ent << 16)) : ((pexp & 0xFFFF0000u) | ent));
+    return 1;
+  }
+  // as VisitedLds<1>::begin, with `cur` both buckets as the look-ahead probe read them
+  __device__ __forceinline__ int begin(u32 x, const Hint& cur, u32& pw, u32& pexp, u32& pold) {
+    return place(x, cur, pw, pexp, pold);
+  }
+  __device__ __forceinline__ void finish(u32 x, u32 pexp, u32 pold, bool& ovf) {
+    if (pold != pexp) (void)test_and_set(x, ovf, probe(x));
+  }
+  __device__ __forceinline__ bool test_and_set(u32 x, bool& ovf, Hint cur = unknown()) {
+    for (;;) {
+      u32 pw = 0, pexp = 0, pold = 0;
+      const int r = place(x, cur, pw, pexp, pold);
+      if (r == 0) return false;
+      if (r == 2) {
+        ovf = true;
+        return false;
+      }
+      if (pold == pexp) return true;
+      cur = probe(x);  // a bucket changed under us (or was not as guessed): read both again
+    }
+  }
+};
+
 // End of the last pass of a call: the last workgroup to finish publishes the queries every pass handed on (host
 // memory: the next call sizes its light pass from them, shine_knn_batch reports them) and zeroes the call's counter
 // words for the next call on this stream, so a call needs neither a memset nor a copy of its own.  No fence is
@@ -1611,7 +1735,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHINE_FAST_M
           fresh = (atomicOr(&sb[e >> 5], bit) & bit) == 0u;
         }
         spill_log(A, sslot, slog, fresh, e, lane);
-      } else if constexpr (VT == 1) {
+      } else if constexpr (VT >= 1) {
         if (cand) {
           const int r = ehint_known ? vis.begin(e, ehint, pw, pexp, pold) : 2;
           fresh = r == 2 ? vis.test_and_set(e, vovf, ehint) : r == 1;
@@ -1668,7 +1792,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHINE_FAST_M
         acc = __ballot(fresh && (cs < ef || my_d < cmax));  // fresh keys that can enter (:461)
       }
 
-      if constexpr (VT == 1) {  // the deferred compare-and-swaps, before the table is probed again
+      if constexpr (VT >= 1) {  // the deferred compare-and-swaps, before the table is probed again
         if (pw != INV) vis.finish(e, pexp, pold, vovf);
         if (__ballot(vovf)) {  // a retried insert overflowed: its id is fresh, record it in HBM
           sslot = claim_spill_bitmap(A, lane);
@@ -2001,6 +2125,7 @@ hipError_t launch_search_acct(uint32_t grid, const SearchArgs& a, hipStream_t s)
         return wide ? runf(search_fast_kernel<D, METRIC, E, 4, 4, AC, VT>) : runf(search_fast_kernel<D, METRIC, E, 4, 2, AC, VT>);
       return wide ? runf(search_fast_kernel<D, METRIC, E, 8, 4, AC, VT>) : runf(search_fast_kernel<D, METRIC, E, 8, 2, AC, VT>);
     };
+    if (a.vis16 == 2) return pick(std::integral_constant<int, 2>{});
     return a.vis16 ? pick(std::integral_constant<int, 1>{}) : pick(std::integral_constant<int, 0>{});
   }
   if constexpr (!AC && D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
@@ -2011,6 +2136,7 @@ hipError_t launch_search_acct(uint32_t grid, const SearchArgs& a, hipStream_t s)
     hipLaunchKernelGGL((search_kernel<D, METRIC, E, 2, AC>), dim3(grid), dim3(64), 64 * 4 * 2, s, a);
     return hipGetLastError();
   }
+  if (a.vis16 > 1) return hipErrorInvalidValue;  // two-choice tables: fast kernel only
   if (a.vis_cap > 0) return a.vis16 ? run(search_kernel<D, METRIC, E, 0, AC, 1>) : run(search_kernel<D, METRIC, E, 0, AC, 0>);
   return run(search_kernel<D, METRIC, E, 1, AC>);
 }

@@ -213,6 +213,40 @@ def test_fast_mode_visited_entry_widths_agree(vis16, gpu_available, monkeypatch)
     _check_tie_free_exact(r, ref, 0.95)
 
 
+@pytest.mark.parametrize("viscap,vis_bits,load", [("4096", "24", "875"), ("4096", "24", "100"), ("1024", "22", "1000")],
+                         ids=["24bit_ids", "24bit_ids_spill_by_load", "22bit_ids_full_buckets"])
+def test_two_choice_tables_match_oracle(viscap, vis_bits, load, gpu_available, monkeypatch, capfd):
+    """Two-choice u16 tables (kernels_impl.h VisitedLds<2>) with the id space widened to 22-24 bits
+    (SHINE_DEBUG_VIS_BITS), so entries carry 13-15-bit remainders: 4,096 entries at 24 bits (the cfg3 / cfg5 10M
+    shape), the same with a load limit of 10 % (every query spills in place and its table is decoded into the HBM
+    bitmap), and 1,024 entries used to the last entry (both buckets full: the overflowing insert spills).  Every
+    tie-free query is the oracle's search bit for bit, and the u32 table (VIS16=0) returns the same batch."""
+    base = D.deep_like(6000, seed=97, d=96)
+    q = D.deep_like(300, seed=98, d=96)
+    dumps, _, _ = O.build(base, 16, 100, 0, 1, seed=4)
+    ref = O.OracleIndex(dumps, 96, 16, 0).knn(q, 10, 128, threads=8)
+    monkeypatch.setenv("SHINE_DEBUG_VISCAP", viscap)
+    monkeypatch.setenv("SHINE_DEBUG_VIS_BITS", vis_bits)
+    monkeypatch.setenv("SHINE_DEBUG_VISLOAD", load)
+    monkeypatch.setenv("SHINE_DEBUG_SHAPE", "1")
+    out = {}
+    for vis16 in ("2", "0"):
+        monkeypatch.setenv("SHINE_DEBUG_VIS16", vis16)
+        capfd.readouterr()
+        out[vis16] = _fast_knn(dumps, 96, 16, 0, q, 10, 128)
+        err = capfd.readouterr().err
+        assert f" vis16 {vis16} " in err, err
+    r, w = out["2"], out["0"]
+    _check_tie_free_exact(r, ref, 0.95)
+    # (a query handed on when the 64 spill bitmaps are taken runs the exact kernel, which counts no ties: compare the
+    # queries both runs found tie-free)
+    both = (r.qstats[:, L.QS_TIES] == 0) & (w.qstats[:, L.QS_TIES] == 0)
+    assert both.mean() >= 0.9
+    np.testing.assert_array_equal(r.ids[both], w.ids[both])
+    np.testing.assert_array_equal(r.dists[both].view(np.uint32), w.dists[both].view(np.uint32))
+    np.testing.assert_array_equal(r.qstats[both][:, [0, 1, 2, 3, 4, 7]], w.qstats[both][:, [0, 1, 2, 3, 4, 7]])
+
+
 @pytest.mark.parametrize("mode", [L.MODE_FAST, L.MODE_EXACT])
 def test_learned_table_sizes_keep_results(mode, gpu_available):
     """The visited tables of a call are sized from the previous call's most-visited query on the same stream

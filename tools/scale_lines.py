@@ -88,8 +88,11 @@ def run(name, a):
             idx, placement = gb.open(elem), "replica"
         else:
             idx, placement = gb.open_ex(slots, elem=elem, gpus=[0] * slots, placement="sharded"), "sharded"
-        lines += run_measure(torch, idx, name, a, q, gt, batch, slots, ef, kind, n, dim, metric, M, efc, placement,
-                             alpha, nq, elem, st)
+        for rep in range(a.repeat):  # --repeat: the same measurement again on the same handle (warm-state check)
+            for line in run_measure(torch, idx, name, a, q, gt, batch, slots, ef, kind, n, dim, metric, M, efc,
+                                    placement, alpha, nq, elem, st):
+                line["repeat"] = rep
+                lines.append(line)
         idx.close()
     gb.close()
     return lines
@@ -177,6 +180,7 @@ def main():
     p.add_argument("--ef", default="")
     p.add_argument("--modes", default="fast,exact")
     p.add_argument("--inflight", type=int, default=4)
+    p.add_argument("--repeat", type=int, default=1)
     p.add_argument("--slots", default="1", help="GPU slots per layout, e.g. 1,8: the same graph as a replica and "
                                                 "as 8 sharded memory-node dumps on this device")
     p.add_argument("--batch-fraction", type=float, default=0.0)
