@@ -146,8 +146,8 @@ def check_same_index(dist, torch, info, world: int, rank: int, device: str):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--n", type=int, default=1_000_000)
     p.add_argument("--dim", type=int, default=128)
     p.add_argument("--batch", type=int, default=1024)

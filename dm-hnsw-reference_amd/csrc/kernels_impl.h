@@ -1071,15 +1071,18 @@ struct VisitedLds<1> {
 // inserted (b1 on a tie).  Entries fill a bucket in order and are never removed, so an id in b2 implies that b1 held an
 // entry when it went there: a bucket b1 found empty answers "absent" alone.  The all-ones entry is the empty marker:
 // at r = 15 the remainder 0x7FFF only ever goes to b1.  A lookup reads both buckets (two ds_read_b128 in flight
-// together); both full is an overflow, and the query spills in place.
-struct Bucket2 {
-  uint4 a, b;  // b1, b2 as last read
+// together); both full is an overflow, and the query spills in place.  The look-ahead probe keeps no bucket copies
+// (8 VGPRs live across the merge): it keeps the insert it would make, as three words — the word to swap (or "present"
+// / "both full"), its expected value and its new value.
+struct Plan2 {
+  u32 pw, pexp, pnew;  // pw: the word to compare-and-swap, or kPresent / kFull / INV (not planned)
 };
 template <>
 struct VisitedLds<2> {
+  static constexpr u32 kPresent = 0xFFFFFFFEu, kFull = 0xFFFFFFFDu;
   u32* t;
   u32 bmask_b, mul, bmask, rbits, rmask, tb;
-  using Hint = Bucket2;
+  using Hint = Plan2;
   __device__ __forceinline__ VisitedLds(void* base, const SearchArgs& A) : t(static_cast<u32*>(base)), mul(A.vis_mul) {
     tb = 31 - __clz(static_cast<int>(A.vis_cap >> 3));  // buckets of 8 entries
     bmask_b = (A.vis_cap >> 3) - 1;
@@ -1088,9 +1091,7 @@ struct VisitedLds<2> {
     rmask = (1u << rbits) - 1;
   }
   static constexpr u32 kBytes = 2;
-  static __device__ __forceinline__ Hint unknown() {  // guess: both buckets empty
-    return Bucket2{make_uint4(INV, INV, INV, INV), make_uint4(INV, INV, INV, INV)};
-  }
+  static __device__ __forceinline__ Hint unknown() { return Plan2{INV, 0u, 0u}; }
   __device__ __forceinline__ void clear(const SearchArgs& A, int lane) {
     uint4* t4 = reinterpret_cast<uint4*>(t);
     for (u32 i = lane; i < A.vis_cap / 8; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
@@ -1133,14 +1134,6 @@ struct VisitedLds<2> {
     t[(h >> rbits) * 4] = 0xFFFF0000u | ((h & rmask) << 1);
   }
   __device__ __forceinline__ uint4 bucket(u32 b) const { return reinterpret_cast<const uint4*>(t)[b]; }
-  __device__ __forceinline__ Hint probe(u32 x) const {
-    const u32 h = image(x), b1 = h >> rbits, b2 = (b1 ^ alt(h & rmask)) & bmask_b;
-    return Bucket2{bucket(b1), bucket(b2)};
-  }
-  __device__ __forceinline__ bool home_match(u32 x, const Hint& w) const {
-    const u32 e = (image(x) & rmask) << 1;
-    return VisitedLds<1>::has(w.a, e) || VisitedLds<1>::has(w.b, e | 1u);
-  }
   // entries in a bucket (they fill it in order): 2 x the first word with an empty half, + 1 if its low half is taken
   static __device__ __forceinline__ u32 fill(const uint4& w) {
     int j;
@@ -1148,42 +1141,50 @@ struct VisitedLds<2> {
     VisitedLds<1>::first_empty(w, j, k, word);
     return j < 0 ? 8u : 2u * static_cast<u32>(j) + k;
   }
-  // from a view of both buckets: 0 = x present, 1 = absent and the compare-and-swap recording it issued (word pw,
-  // expected pexp, returned pold), 2 = absent with both buckets full
-  __device__ __forceinline__ int place(u32 x, const Hint& cur, u32& pw, u32& pexp, u32& pold) const {
-    const u32 h = image(x), rem = h & rmask, b1 = h >> rbits;
+  // x against both buckets as they stand: present, both full, or the insert (the less filled bucket's first empty
+  // entry) as a compare-and-swap to make
+  __device__ __forceinline__ Hint probe(u32 x) const {
+    const u32 h = image(x), rem = h & rmask, b1 = h >> rbits, b2 = (b1 ^ alt(rem)) & bmask_b;
+    const uint4 w1 = bucket(b1), w2 = bucket(b2);
     const u32 e = rem << 1;
-    if (VisitedLds<1>::has(cur.a, e) || VisitedLds<1>::has(cur.b, e | 1u)) return 0;
-    const u32 f1 = fill(cur.a), f2 = fill(cur.b);
-    const bool second = f2 < f1 && rem != 0x7FFFu;
-    if ((second ? f2 : f1) >= 8u) return 2;
-    const uint4& w = second ? cur.b : cur.a;
+    if (VisitedLds<1>::has(w1, e) || VisitedLds<1>::has(w2, e | 1u)) return Plan2{kPresent, 0u, 0u};
+    const bool second = fill(w2) < fill(w1) && rem != 0x7FFFu;
     int j;
-    u32 k;
-    VisitedLds<1>::first_empty(w, j, k, pexp);
+    u32 k, old;
+    VisitedLds<1>::first_empty(second ? w2 : w1, j, k, old);
+    if (j < 0) return Plan2{kFull, 0u, 0u};
     const u32 ent = second ? (e | 1u) : e;
-    pw = (second ? ((b1 ^ alt(rem)) & bmask_b) : b1) * 4 + static_cast<u32>(j);
-    pold = atomicCAS(&t[pw], pexp, k ? ((pexp & 0xFFFFu) | (ent << 16)) : ((pexp & 0xFFFF0000u) | ent));
-    return 1;
+    return Plan2{(second ? b2 : b1) * 4 + static_cast<u32>(j), old,
+                 k ? ((old & 0xFFFFu) | (ent << 16)) : ((old & 0xFFFF0000u) | ent)};
   }
-  // as VisitedLds<1>::begin, with `cur` both buckets as the look-ahead probe read them
-  __device__ __forceinline__ int begin(u32 x, const Hint& cur, u32& pw, u32& pexp, u32& pold) {
-    return place(x, cur, pw, pexp, pold);
+  __device__ __forceinline__ bool home_match(u32 /*x*/, const Hint& p) const { return p.pw == kPresent; }
+  // as VisitedLds<1>::begin, from the look-ahead probe's plan: 0 = present, 1 = compare-and-swap issued, 2 = both full
+  __device__ __forceinline__ int begin(u32 /*x*/, const Hint& p, u32& pw, u32& pexp, u32& pold) {
+    if (p.pw == kPresent) return 0;
+    if (p.pw >= kFull) return 2;
+    pw = p.pw;
+    pexp = p.pexp;
+    pold = atomicCAS(&t[pw], p.pexp, p.pnew);
+    return 1;
   }
   __device__ __forceinline__ void finish(u32 x, u32 pexp, u32 pold, bool& ovf) {
     if (pold != pexp) (void)test_and_set(x, ovf, probe(x));
   }
-  __device__ __forceinline__ bool test_and_set(u32 x, bool& ovf, Hint cur = unknown()) {
+  // p: a plan made since the last insert, or unknown() — then the guess that b1 is empty (its word 0 swapped from
+  // all-empty: when that holds, x is in neither bucket), read and planned again when it fails
+  __device__ __forceinline__ bool test_and_set(u32 x, bool& ovf, Hint p = unknown()) {
+    if (p.pw == INV) {
+      const u32 h = image(x);
+      p = Plan2{(h >> rbits) * 4, INV, 0xFFFF0000u | ((h & rmask) << 1)};
+    }
     for (;;) {
-      u32 pw = 0, pexp = 0, pold = 0;
-      const int r = place(x, cur, pw, pexp, pold);
-      if (r == 0) return false;
-      if (r == 2) {
+      if (p.pw == kPresent) return false;
+      if (p.pw == kFull) {
         ovf = true;
         return false;
       }
-      if (pold == pexp) return true;
-      cur = probe(x);  // a bucket changed under us (or was not as guessed): read both again
+      if (atomicCAS(&t[p.pw], p.pexp, p.pnew) == p.pexp) return true;
+      p = probe(x);  // a word changed under us (or was not as guessed): read both buckets again
     }
   }
 };
@@ -1622,12 +1623,16 @@ __device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restri
 
 
 // Waves per SIMD the register allocation must allow (build-time tuning: 4 caps a wave at 128 VGPRs, so 16 wavefronts
-// fit a CU when their LDS tables do).
+// fit a CU when their LDS tables do).  The two-choice tables exist to put more wavefronts on a CU: at d <= 128 and
+// ef <= 256 their kernels are held to 168 VGPRs (3 per SIMD; 173 unconstrained at d = 96, ef = 256, without spills
+// at 168; at ef > 256 the same cap spills).
 #ifndef SHINE_FAST_MIN_WAVES
 #define SHINE_FAST_MIN_WAVES 1
 #endif
+template <int D, int R, int VT>
+constexpr int kFastWaves = VT == 2 && D <= 128 && R <= 4 && SHINE_FAST_MIN_WAVES < 3 ? 3 : SHINE_FAST_MIN_WAVES;
 template <int D, int METRIC, typename E, int R, int P, int ACCT, int VT, bool PROF = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SHINE_FAST_MIN_WAVES))) void search_fast_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kFastWaves<D, R, VT>))) void search_fast_kernel(
     SearchArgs A) {
   PhaseClock<PROF> clk;
   clk.start();

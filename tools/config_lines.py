@@ -211,8 +211,13 @@ def measure(torch, idx, name, a, qd, gt, batch, slots, ef, nb=None):
     ids = torch.empty((nb, batch, a.k), dtype=torch.int32, device="cuda")
     dists = torch.empty((nb, batch, a.k), dtype=torch.float32, device="cuda")
     qs = torch.zeros((nb, batch, shine_amd.QS_WORDS), dtype=torch.int32, device="cuda")
-    # a.inflight batches in flight per slot (step i on stream set i % inflight), as bench.py does
-    streams = [[torch.cuda.Stream() for _ in range(slots)] for _ in range(a.inflight)]
+    # a.inflight batches in flight per slot (step i on stream set i % inflight), as bench.py does, on streams created
+    # directly through HIP (bench.hip_streams): consecutive new streams take consecutive hardware queues, where torch's
+    # stream pool can hand two batches one queue (then they run back to back: a first measurement in a process ran
+    # at 1.41 M QPS against 2.32 M on the next streams, profiles/r04/two_choice_ab_warm.jsonl)
+    from bench import hip_streams
+    flat = hip_streams(torch, a.inflight * slots, torch.cuda.current_device())
+    streams = [flat[i * slots:(i + 1) * slots] for i in range(a.inflight)]
     per = batch // slots  # slot s answers rows [s*per, (s+1)*per) of each batch (id % G in the host API)
 
     def step(i, rec=None):

@@ -174,8 +174,8 @@ def main():
     p.add_argument("--which", default="cmp")
     p.add_argument("--n", type=int, default=0, help="override the workload's record count")
     p.add_argument("--k", type=int, default=10)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=4)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--nbatches", type=int, default=10)
     p.add_argument("--ef", default="")
     p.add_argument("--modes", default="fast,exact")
@@ -203,5 +203,5 @@ def main():
 
 
 if __name__ == "__main__":
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"  # batches in flight on distinct hardware queues (the box exports 4)
     main()

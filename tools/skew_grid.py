@@ -127,5 +127,5 @@ def main():
 
 
 if __name__ == "__main__":
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"  # batches in flight on distinct hardware queues (the box exports 4)
     main()
