@@ -202,6 +202,18 @@ def run_dynamic(name, a, paths, dim, M, metric, elem, gpus, q, gt, batch, ef):
     return line
 
 
+_STREAMS: list = []
+
+
+def reserve_streams(torch, n: int):
+    """n HIP streams created directly (bench.hip_streams) on the first call — made before any other stream of the
+    process, they take consecutive hardware queues of HIP's round-robin — and the same streams on every later call."""
+    if len(_STREAMS) < n:
+        from bench import hip_streams
+        _STREAMS.extend(hip_streams(torch, n - len(_STREAMS), torch.cuda.current_device()))
+    return _STREAMS[:n]
+
+
 def measure(torch, idx, name, a, qd, gt, batch, slots, ef, nb=None):
     """Validation pass, then timed batches on the device (slot s answers rows [s*per, (s+1)*per) of each batch)."""
     import shine_amd
@@ -211,12 +223,11 @@ def measure(torch, idx, name, a, qd, gt, batch, slots, ef, nb=None):
     ids = torch.empty((nb, batch, a.k), dtype=torch.int32, device="cuda")
     dists = torch.empty((nb, batch, a.k), dtype=torch.float32, device="cuda")
     qs = torch.zeros((nb, batch, shine_amd.QS_WORDS), dtype=torch.int32, device="cuda")
-    # a.inflight batches in flight per slot (step i on stream set i % inflight), as bench.py does, on streams created
-    # directly through HIP (bench.hip_streams): consecutive new streams take consecutive hardware queues, where torch's
-    # stream pool can hand two batches one queue (then they run back to back: a first measurement in a process ran
-    # at 1.41 M QPS against 2.32 M on the next streams, profiles/r04/two_choice_ab_warm.jsonl)
-    from bench import hip_streams
-    flat = hip_streams(torch, a.inflight * slots, torch.cuda.current_device())
+    # a.inflight batches in flight per slot (step i on stream set i % inflight), as bench.py does, on the process's
+    # reserved streams (reserve_streams): torch's stream pool, or streams created after the index's own, can hand two
+    # batches one hardware queue, and then they run back to back (cfg5-shaped 10M: 1.41 M against 2.33 M QPS,
+    # profiles/r04/two_choice_ab_warm.jsonl, scale_10m_v8_streams.jsonl)
+    flat = reserve_streams(torch, a.inflight * slots)
     streams = [flat[i * slots:(i + 1) * slots] for i in range(a.inflight)]
     per = batch // slots  # slot s answers rows [s*per, (s+1)*per) of each batch (id % G in the host API)
 

@@ -194,6 +194,8 @@ def main():
     a = p.parse_args()
     import torch
     torch.cuda.set_device(0)
+    from config_lines import reserve_streams
+    reserve_streams(torch, a.inflight * max(int(s) for s in a.slots.split(",")))  # first streams of the process
     Path(a.out).parent.mkdir(parents=True, exist_ok=True)
     for name in a.which.split(","):
         for line in (run_cmp(a) if name == "cmp" else run(name, a)):
