@@ -651,7 +651,7 @@ LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds
   sh.vis_cap = sh.vis16 ? t16 : t32;
   sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
   if (sh.vis16) sh.vis16 = kind16(sh.vis_cap);  // a forced table size: the entries it allows (0: back to u32)
-  if (force16 == 2 && sh.vis16 == 1 && bits <= log2u(sh.vis_cap) + 12) sh.vis16 = 2;  // test hook: two-choice
+  if (force16 == 2 && bits <= log2u(sh.vis_cap) + 12) sh.vis16 = 2;  // test hook: two-choice
   sh.vis_bits = std::max(bits, log2u(sh.vis_cap) + 1);
   const uint64_t need = search_fast_lds_bytes(sh.vis_cap, ef, sh.vis16 ? 2 : 4);
   const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(lds_per_cu / need));
@@ -705,14 +705,24 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
     const uint32_t want = std::min<uint32_t>(batches * ((nq + cus - 1) / cus), 16u);
     uint32_t bits = 14;
     while (bits < 32 && (1ull << bits) < h->id_space) ++bits;
+    bits = std::max<uint32_t>(bits, static_cast<uint32_t>(std::min<int64_t>(31, env_int("SHINE_DEBUG_VIS_BITS", 0))));
     auto fit = [&](uint32_t vis_cap, uint32_t& vis16) {  // entry width and resident wavefronts for a table size
       auto waves = [&](uint64_t need) {
         return std::max<uint32_t>(1, std::min<uint32_t>(want, static_cast<uint32_t>(lds / need)));
       };
       const uint32_t w32 = waves(search_lds_bytes(ef, 4 * ef, vis_cap, 4));
       const uint32_t w16 = waves(search_lds_bytes(ef, 5 * ef, vis_cap, 2));
-      const bool can16 = env_int("SHINE_DEBUG_VIS16", 1) != 0 && bits <= log2_ceil(vis_cap) + 10;
-      vis16 = can16 && (w16 > w32 || env_int("SHINE_DEBUG_VIS16", -1) == 1) ? 1 : 0;
+      // u16 entries: linear-probed buckets (VisitedLds<1>); two-choice buckets (VisitedLds<2>) only on request
+      // (SHINE_EXACT_TWO_CHOICE=1) — the exact kernel's insert has no look-ahead plan, so it pays the guess, a read of
+      // both buckets and the swap, and at cfg 3 (24-bit ids) it ran at 0.90 M against 1.12 M QPS on u32 entries
+      // (profiles/r04/scale_10m_v9_exact_two_choice.jsonl)
+      const uint32_t kind = bits <= log2_ceil(vis_cap) + 10 ? 1u
+                            : bits <= log2_ceil(vis_cap) + 12 && env_int("SHINE_EXACT_TWO_CHOICE", 0) != 0 ? 2u
+                                                                                                            : 0u;
+      const int64_t force16 = env_int("SHINE_DEBUG_VIS16", -1);
+      const bool can16 = force16 != 0 && kind != 0;
+      vis16 = can16 && (w16 > w32 || force16 >= 1) ? kind : 0;
+      if (force16 == 2 && bits <= log2_ceil(vis_cap) + 12) vis16 = 2;  // test hook: two-choice
       return vis16 ? w16 : w32;
     };
     sh.vis_cap = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(per_ef * ef)));

@@ -2141,7 +2141,7 @@ hipError_t launch_search_acct(uint32_t grid, const SearchArgs& a, hipStream_t s)
     hipLaunchKernelGGL((search_kernel<D, METRIC, E, 2, AC>), dim3(grid), dim3(64), 64 * 4 * 2, s, a);
     return hipGetLastError();
   }
-  if (a.vis16 > 1) return hipErrorInvalidValue;  // two-choice tables: fast kernel only
+  if (a.vis_cap > 0 && a.vis16 == 2) return run(search_kernel<D, METRIC, E, 0, AC, 2>);
   if (a.vis_cap > 0) return a.vis16 ? run(search_kernel<D, METRIC, E, 0, AC, 1>) : run(search_kernel<D, METRIC, E, 0, AC, 0>);
   return run(search_kernel<D, METRIC, E, 1, AC>);
 }

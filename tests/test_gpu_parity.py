@@ -284,6 +284,28 @@ def test_exact_mode_spills_in_place(gen, dim, metric, ef, vis16, gpu_available, 
             np.testing.assert_array_equal(one.qstats[:, :5], ref[2][i:i + 8, :5])
 
 
+@pytest.mark.parametrize("viscap,vis_bits", [("4096", "24"), ("1024", "22")], ids=["24bit_ids", "22bit_ids_spill"])
+def test_exact_mode_two_choice_tables(viscap, vis_bits, gpu_available, monkeypatch, capfd):
+    """Exact mode on two-choice u16 tables (VisitedLds<2>, SHINE_DEBUG_VIS16=2) with the id space widened to 22-24
+    bits: 4,096 entries at 24 bits (cfg 3's shape), and 1,024 entries at 22 bits, which every query outgrows (the
+    table spills, decoded into the HBM bitmap).  Ids in heap-array order, distances and every counter equal the
+    oracle's."""
+    base = D.deep_like(6000, seed=313, d=96)
+    q = D.deep_like(200, seed=314, d=96)
+    dumps, _, _ = O.build(base, 16, 100, 1, 1, seed=6)
+    ref = O.OracleIndex(dumps, 96, 16, 1).knn(q, 10, 128, threads=8)
+    monkeypatch.setenv("SHINE_DEBUG_VISCAP", viscap)
+    monkeypatch.setenv("SHINE_DEBUG_VIS_BITS", vis_bits)
+    monkeypatch.setenv("SHINE_DEBUG_VIS16", "2")
+    monkeypatch.setenv("SHINE_DEBUG_SHAPE", "1")
+    with shine_amd.Index.from_buffers(dumps, 96, 16, 1, gpus=[0]) as idx:
+        capfd.readouterr()
+        r = idx.knn(q, 10, 128)
+        err = capfd.readouterr().err
+        assert " vis16 2 " in err, err
+        _check_same(r, *ref)
+
+
 def test_global_heap_capacity_overflow_is_reported(gpu_available, monkeypatch):
     """The last pass's capacity is the only hard limit: a query that outgrows it fails with SHINE_ERR_OVERFLOW in
     its status word and shine_knn_batch returns that status (no silent truncation)."""
