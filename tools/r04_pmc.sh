@@ -27,6 +27,7 @@ for W in ${WHICH//,/ }; do
     --out $O/${W}_pmc.json > /dev/null || { echo "$W pmc summary failed"; exit 1; }
   python3 $R/tools/pmc_summary.py $O/$W/p3/run_counter_collection.csv $O/$W/p4/run_counter_collection.csv --kernel "$K" \
     --out $O/${W}_sq.json > /dev/null || { echo "$W sq summary failed"; exit 1; }
+  rm -rf $O/$W/p1 $O/$W/p2 $O/$W/p3 $O/$W/p4  # every dispatch of the build too: too large to bring back
   echo "$W done"
 done
 echo done
