@@ -479,6 +479,10 @@ __device__ __forceinline__ float byte_f32(u32 w, int i) {
   else return static_cast<float>(static_cast<int>(w << (24 - 8 * i)) >> 24);
 }
 
+__device__ __forceinline__ float half_lo(u32 w) {
+  return __half2float(__ushort_as_half(static_cast<unsigned short>(w & 0xFFFFu)));
+}
+__device__ __forceinline__ float half_hi(u32 w) { return __half2float(__ushort_as_half(static_cast<unsigned short>(w >> 16))); }
 __device__ __forceinline__ f32x2 half2_to_f32x2(u32 w) {
   return f32x2{__half2float(__ushort_as_half(static_cast<unsigned short>(w & 0xFFFFu))),
                __half2float(__ushort_as_half(static_cast<unsigned short>(w >> 16)))};
@@ -583,6 +587,16 @@ __device__ __forceinline__ void pass_dists(const QueryRegs<D, E>& Q, const NbrBu
         const u32 w = B.x[p][u];
         x0 = f32x2{byte_f32<E>(w, 0), byte_f32<E>(w, 1)};
         x1 = f32x2{byte_f32<E>(w, 2), byte_f32<E>(w, 3)};
+      } else if constexpr (METRIC == 1) {
+        // f16 rows, inner product: each accumulator's fmaf on the half widened in place (v_fma_mix_f32 with op_sel
+        // picking the half: the widening is exact, one rounding as fmaf(q, float(x), acc)), 2 instructions per
+        // word instead of 2 conversions and a packed FMA; same operands in the same order per accumulator
+        const u32 w0 = B.x[p][u].x, w1 = B.x[p][u].y;
+        acc[p].x = __builtin_fmaf(Q.q2[2 * u].x, half_lo(w0), acc[p].x);
+        acc[p].y = __builtin_fmaf(Q.q2[2 * u].y, half_hi(w0), acc[p].y);
+        acc[p].x = __builtin_fmaf(Q.q2[2 * u + 1].x, half_lo(w1), acc[p].x);
+        acc[p].y = __builtin_fmaf(Q.q2[2 * u + 1].y, half_hi(w1), acc[p].y);
+        continue;
       } else {
         x0 = half2_to_f32x2(B.x[p][u].x);
         x1 = half2_to_f32x2(B.x[p][u].y);

@@ -32,7 +32,7 @@ sys.path.insert(0, str(ROOT / "dm-hnsw-reference_amd"))
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tools"))
 from bench import log  # noqa: E402
-from config_lines import Heartbeat  # noqa: E402
+from config_lines import Heartbeat, read_classes  # noqa: E402
 
 
 def main():
@@ -42,7 +42,7 @@ def main():
     p.add_argument("--alphas", default="0,0.5,0.75,1.0,1.25,1.5")
     p.add_argument("--ratios", default="2,4,5,6,8,10")
     p.add_argument("--labels", default="baseline,+cache,+adaptive-routing")
-    p.add_argument("--warm", type=int, default=6)
+    p.add_argument("--warm", type=int, default=24)
     p.add_argument("--calls", type=int, default=8)
     p.add_argument("--batch", type=int, default=1024)
     p.add_argument("--ef", type=int, default=250)
@@ -94,13 +94,16 @@ def main():
                 else:
                     idx.set_cache_policy(L.CACHE_DYNAMIC, ratio_percent=ratio, seed=1)
                 hits = reads = 0
-                res, t_meas, adm = [], 0.0, 0
+                res, t_meas, adm, qss, t_warm = [], 0.0, 0, [], 0.0
                 for c in range(a.warm + a.calls):
                     qq = q[c * a.batch:(c + 1) * a.batch]
                     t1 = time.perf_counter()
                     r = idx.knn(qq, k, a.ef, query_ids=np.arange(c * a.batch, (c + 1) * a.batch, dtype=np.uint32))
                     el = time.perf_counter() - t1
-                    if c >= a.warm:
+                    if c < a.warm:
+                        t_warm += el
+                    else:
+                        qss.append(r.qstats)
                         t_meas += el
                         hits += r.stats["node_cache_hits"]
                         reads += r.stats["node_reads"]
@@ -111,6 +114,8 @@ def main():
                 line = {"workload": "cfg5-skew-grid", "label": label, "alpha": alpha, "cache_ratio_percent": ratio,
                         "placement": placement, "gpu_slots": a.slots, "physical_gpus": len(set(gpus)),
                         "cache_hit_rate": hits / max(1, reads), "node_reads": reads,
+                        "read_classes": read_classes(np.concatenate(qss)),
+                        "warmup_s": t_warm,
                         "recall_at_10": D.recall_at_k(got, want, k),
                         "host_api_qps_including_cache_updates": a.calls * a.batch / t_meas,
                         "admitted_during_measured_calls": adm,
