@@ -255,7 +255,9 @@ __device__ __forceinline__ u64 heap_pop(u64* h, int n, int lane, const PopLane& 
     // every hole moved: the walk ends in the deepest hole's winner child, or goes on from it in the next window
     const int cw1 = 2 * a1 + (right ? 1 : 0);
     const int P = H ? __builtin_amdgcn_readlane(cw1, 63 - static_cast<int>(__clzll(H))) : P1;
-    if (!(H >> 31)) {  // no hole at window depth 5: the path ended inside this window
+    // no hole at window depth 5 (the path ended inside this window), or the deepest hole moved into a leaf (P has no
+    // child: at ef = 128 every full pop ends so, and the next window would only place the value)
+    if (!(H >> 31) || 2 * P > len) {
       if (lane == 0) h[P - 1] = value;
       break;
     }
