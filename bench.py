@@ -669,6 +669,17 @@ def run_sharded(a):
     # every slot answers a.batch queries per step (global batch a.batch x S, split id % S): per-GPU work is fixed
     gpus, rows = sharded_plan(S, ndev, a.batch * S, a.nbatches)
     phys = len(set(gpus))
+    # the in-flight streams of every slot, created first in the process through HIP (hip_streams): torch's stream
+    # pool can put two batches on one hardware queue (this leg read 3.07 M QPS on one slot of one GPU where the same
+    # layout measures 5.36 M on reserved streams, profiles/r04/layout_probe.jsonl)
+    per_dev: dict = {}
+    for s in range(S):
+        per_dev.setdefault(gpus[s], []).append(s)
+    slot_streams = {}
+    for d, slots_d in per_dev.items():
+        made = hip_streams(torch, max(1, a.inflight) * len(slots_d), d)
+        for j, s in enumerate(slots_d):
+            slot_streams[s] = made[j * max(1, a.inflight):(j + 1) * max(1, a.inflight)]
     dim, M, efc, ef, shards = 96, 16, 200, 128, 8
     # the index is built on GPU 0 by the GPU batch builder (10M records in seconds) and laid out over the slots as its
     # 8 memory-node dumps would be (shine_gpu_build_open_ex), without writing or parsing them
@@ -695,8 +706,7 @@ def run_sharded(a):
         ids.append([torch.empty((len(rows[b][s]), k), dtype=torch.int32, device=dev) for b in range(nb)])
         qs.append([torch.zeros((len(rows[b][s]), shine_amd.QS_WORDS), dtype=torch.int32, device=dev)
                    for b in range(nb)])
-        with torch.cuda.device(dev):
-            streams.append([torch.cuda.Stream(device=dev) for _ in range(max(1, a.inflight))])
+        streams.append(slot_streams[s])
 
     def step(i):
         b = i % nb
@@ -741,7 +751,8 @@ def run_sharded(a):
         hits, misses = int(st[:, 10:12].sum()), int(st[:, 8:10].sum())
         node_reads = int(st[:, 0].sum())  # every distance computation reads one record (rdma::read_node)
         qps = a.steps * B / el
-        one = one_gpu_rate(a, torch, shine_amd, gb, dim, M, ef, k, q, rows, mode) if mode_name == "fast" else None
+        one = (one_gpu_rate(a, torch, shine_amd, gb, dim, M, ef, k, q, rows, mode, slot_streams[per_dev[0][0]])
+               if mode_name == "fast" and 0 in per_dev else None)
         xgmi_in = 7 * 153e9
         line = {
             "metric": "QPS at recall@10, cfg4-shaped sharded index (DEEP-like 96-d L2, 8 memory-node dumps)",
@@ -776,14 +787,14 @@ def run_sharded(a):
     print(json.dumps(lines[0]), flush=True)
 
 
-def one_gpu_rate(a, torch, shine_amd, gb, dim, M, ef, k, q, rows, mode):
+def one_gpu_rate(a, torch, shine_amd, gb, dim, M, ef, k, q, rows, mode, streams):
     """The same index as a replica on GPU 0 (the build's own arrays), the same global batches (each slot's share one
-    launch, in flight on rotating streams): the one-GPU rate the sharded leg's speedup is quoted against."""
+    launch, in flight on rotating streams — GPU 0's first slot's reserved streams): the one-GPU rate the sharded leg's
+    speedup is quoted against."""
     nb, S = len(rows), len(rows[0])
     with gb.open_ex(1, gpus=[0]) as ix:
         ix.set_search_mode(mode)
         with torch.cuda.device(0):
-            streams = [torch.cuda.Stream() for _ in range(max(1, a.inflight))]
             qd = [[torch.from_numpy(np.ascontiguousarray(q[rows[b][s]])).cuda() for s in range(S)] for b in range(nb)]
             ids = [[torch.empty((len(rows[b][s]), k), dtype=torch.int32, device="cuda") for s in range(S)]
                    for b in range(nb)]
