@@ -706,19 +706,23 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
     uint32_t bits = 14;
     while (bits < 32 && (1ull << bits) < h->id_space) ++bits;
     bits = std::max<uint32_t>(bits, static_cast<uint32_t>(std::min<int64_t>(31, env_int("SHINE_DEBUG_VIS_BITS", 0))));
-    auto fit = [&](uint32_t vis_cap, uint32_t& vis16) {  // entry width and resident wavefronts for a table size
+    // entry width and resident wavefronts for a table size.  u16 entries: linear-probed buckets (VisitedLds<1>), or
+    // two-choice buckets (VisitedLds<2>) where the id space leaves no distance bits (two_choice).  The exact kernel's
+    // insert has no look-ahead plan, so two-choice pays the guess, a read of both buckets and the swap: on the table
+    // sized for the worst query it only lost (cfg 3: 8,192 entries, 0.89 M against 1.14 M QPS on u32), but on the
+    // mean-sized table (below) its halved bytes put a seventh wavefront on each CU and make room for next_candidates:
+    // 1.28 M against 1.14 M, and the hand-ons for next_candidates capacity drop from 6-13 to 0-1 per call
+    // (profiles/r04/env_scan_cfg3_exact.jsonl).  SHINE_EXACT_TWO_CHOICE = 0 / 1 turns it off / on for both sizes.
+    auto fit = [&](uint32_t vis_cap, uint32_t& vis16, bool two_choice) {
       auto waves = [&](uint64_t need) {
         return std::max<uint32_t>(1, std::min<uint32_t>(want, static_cast<uint32_t>(lds / need)));
       };
       const uint32_t w32 = waves(search_lds_bytes(ef, 4 * ef, vis_cap, 4));
       const uint32_t w16 = waves(search_lds_bytes(ef, 5 * ef, vis_cap, 2));
-      // u16 entries: linear-probed buckets (VisitedLds<1>); two-choice buckets (VisitedLds<2>) only on request
-      // (SHINE_EXACT_TWO_CHOICE=1) — the exact kernel's insert has no look-ahead plan, so it pays the guess, a read of
-      // both buckets and the swap, and at cfg 3 (24-bit ids) it ran at 0.90 M against 1.12 M QPS on u32 entries
-      // (profiles/r04/scale_10m_v9_exact_two_choice.jsonl)
-      const uint32_t kind = bits <= log2_ceil(vis_cap) + 10 ? 1u
-                            : bits <= log2_ceil(vis_cap) + 12 && env_int("SHINE_EXACT_TWO_CHOICE", 0) != 0 ? 2u
-                                                                                                            : 0u;
+      const int64_t tc = env_int("SHINE_EXACT_TWO_CHOICE", -1);
+      const uint32_t kind = bits <= log2_ceil(vis_cap) + 10                                        ? 1u
+                            : bits <= log2_ceil(vis_cap) + 12 && (tc == 1 || (tc < 0 && two_choice)) ? 2u
+                                                                                                   : 0u;
       const int64_t force16 = env_int("SHINE_DEBUG_VIS16", -1);
       const bool can16 = force16 != 0 && kind != 0;
       vis16 = can16 && (w16 > w32 || force16 >= 1) ? kind : 0;
@@ -730,10 +734,10 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
     // after a call that handed queries on)
     if (learned && (spill_enabled() || learned < sh.vis_cap || (handed != 0xFFFFFFFFu && handed > 0)))
       sh.vis_cap = learned;
-    wpc = fit(sh.vis_cap, sh.vis16);
+    wpc = fit(sh.vis_cap, sh.vis16, false);
     if (wpc < 4 && learned_mean && learned_mean < sh.vis_cap && spill_enabled()) {
       uint32_t v16 = 0;
-      const uint32_t w = fit(learned_mean, v16);
+      const uint32_t w = fit(learned_mean, v16, true);
       if (w > wpc) {
         sh.vis_cap = learned_mean;
         sh.vis16 = v16;
@@ -742,7 +746,7 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
     }
     if (const char* e = std::getenv("SHINE_DEBUG_VISCAP")) {  // test hook
       sh.vis_cap = static_cast<uint32_t>(std::atoll(e));
-      wpc = fit(sh.vis_cap, sh.vis16);
+      wpc = fit(sh.vis_cap, sh.vis16, false);
     }
     sh.vis_bits = std::max(bits, log2_ceil(sh.vis_cap) + 1);
     budget = (lds / wpc) & ~15u;
