@@ -2151,6 +2151,7 @@ hipError_t launch_search_acct(uint32_t grid, const SearchArgs& a, hipStream_t s)
   }
   if constexpr (!AC && D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
     if (a.prof && a.vis_cap > 0 && !a.vis16) return run(search_kernel<D, METRIC, E, 0, AC, 0, true>);
+    if (a.prof && a.vis_cap > 0 && a.vis16 == 1) return run(search_kernel<D, METRIC, E, 0, AC, 1, true>);
   }
   if (a.global_heaps) {  // both heaps in HBM: only the scratch ids / distances stay in LDS
     if (a.vis_cap != 0 || !a.heaps || a.heap_stride < align16(8ull * a.ef) / 8 + a.cap) return hipErrorInvalidValue;
