@@ -1392,7 +1392,10 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
         bool fresh = false, vovf = false;
         if (cand) {  // visited.contains / insert (:441-443)
           if (VIS == 0 && sslot < 0) {
-            fresh = vt.test_and_set(e, vovf);
+            // the home word / bucket read first (every candidate lane's read in flight together): a visited id is
+            // then answered in one LDS round trip and a fresh one swapped in two, where a blind swap assuming an
+            // empty home costs an extra failed round trip once the table has filled
+            fresh = vt.test_and_set(e, vovf, vt.probe(e));
           } else {  // the HBM bitmap: the fallback passes', or this query's spilled table
             u32* __restrict__ bm = VIS == 0 ? A.visited + static_cast<u64>(sslot) * A.words_per_slot : vis;
             const u32 bit = 1u << (e & 31);
