@@ -1164,10 +1164,15 @@ struct VisitedLds<2> {
     const uint4 w1 = bucket(b1), w2 = bucket(b2);
     const u32 e = rem << 1;
     if (VisitedLds<1>::has(w1, e) || VisitedLds<1>::has(w2, e | 1u)) return Plan2{kPresent, 0u, 0u};
-    const bool second = fill(w2) < fill(w1) && rem != 0x7FFFu;
-    int j;
-    u32 k, old;
-    VisitedLds<1>::first_empty(second ? w2 : w1, j, k, old);
+    // each bucket's first empty entry once: its position is the bucket's fill (entries fill in order)
+    int j1, j2;
+    u32 k1, k2, o1, o2;
+    VisitedLds<1>::first_empty(w1, j1, k1, o1);
+    VisitedLds<1>::first_empty(w2, j2, k2, o2);
+    const u32 f1 = j1 < 0 ? 8u : 2u * static_cast<u32>(j1) + k1, f2 = j2 < 0 ? 8u : 2u * static_cast<u32>(j2) + k2;
+    const bool second = f2 < f1 && rem != 0x7FFFu;
+    const int j = second ? j2 : j1;
+    const u32 k = second ? k2 : k1, old = second ? o2 : o1;
     if (j < 0) return Plan2{kFull, 0u, 0u};
     const u32 ent = second ? (e | 1u) : e;
     return Plan2{(second ? b2 : b1) * 4 + static_cast<u32>(j), old,
