@@ -573,12 +573,16 @@ uint32_t learned_mean_table(const Scratch& S) {
 }
 
 // The previous call's worst query with 1/8 to spare (large id spaces, see enqueue_search).
+// u32 tables (VisitedLds<0>) take any multiple of 64 entries: rounded up to 1,024, not to a power of two (100M ids at
+// ef = 128: 6,144 entries and 6 wavefronts per CU instead of 8,192 and 4; SHINE_FAST_TABLE_POW2=1 restores the
+// doubling for comparison).  u16 entries need a power of two (pick_fast_shape rounds them up).
 uint32_t learned_max_table(const Scratch& S) {
   if (!S.seen.p || !S.seen.p[3] || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
   const uint64_t vmax = S.seen.p[4];
   if (vmax == 0) return 0;
-  return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, pow2_at_least(static_cast<uint32_t>(
-                                                                                  std::min<uint64_t>(16384, vmax * 9 / 8)))}));
+  const uint32_t want = static_cast<uint32_t>(std::min<uint64_t>(16384, vmax * 9 / 8));
+  const uint32_t t = env_int("SHINE_FAST_TABLE_POW2", 0) ? pow2_at_least(want) : (want + 1023) / 1024 * 1024;
+  return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, t}));
 }
 
 // The exact pass's learned table, with the in-place spill: just the previous call's worst query (eighths/8 × its
@@ -642,7 +646,7 @@ LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds
   auto kind16 = [&](uint32_t t) -> uint32_t {
     return bits <= log2u(t) + 10 ? 1u : bits <= log2u(t) + 12 ? 2u : 0u;
   };
-  const uint32_t t32 = table_for(4), t16 = table_for(2);
+  const uint32_t t32 = table_for(4), t16 = pow2_at_least(table_for(2));  // (a learned size may not be a power of two)
   const int64_t force16 = env_int("SHINE_DEBUG_VIS16", -1);
   const bool can16 = force16 != 0 && kind16(t16) != 0 && (kind16(t16) == 1 || env_int("SHINE_TWO_CHOICE", 1) != 0);
   const uint64_t w32 = resident(t32, 4), w16 = can16 ? resident(t16, 2) : 0;
@@ -823,7 +827,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   // a learned table that handed queries on was too small — unless the pass spills its tables in place: then only the
   // exact pass hands queries on, for its next_candidates capacity, which a larger table would only shrink
   if (handed && S.last_learned && (S.last_fast || !spill_enabled()))
-    S.table_floor = std::max(S.table_floor, 2 * S.last_table);
+    S.table_floor = std::max(S.table_floor, pow2_at_least(2 * S.last_table));
   // Tuning hook (off by default): a learned fast table that sent more than SHINE_FAST_SPILL_PERMILLE / 1000 of its
   // call's queries to a spill bitmap is grown.  It cost 30 % at cfg 3 (10M ids, batch 4096), where residency matters
   // more than the spills (profiles/r04/scale_cfg3_cfg5_10m_v2_floor.jsonl), and did not help at 100M ids, where the
@@ -832,7 +836,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     const uint64_t spilled = S.seen.p[3] ? S.seen.p[7] : 0, seen_nq = S.seen.p[3] ? S.seen.p[6] : 0;
     const int64_t permille = env_int("SHINE_FAST_SPILL_PERMILLE", 0);
     if (permille > 0 && spilled && S.last_learned && S.last_fast && spilled * 1000 > seen_nq * static_cast<uint64_t>(permille))
-      S.table_floor = std::max(S.table_floor, 2 * S.last_table);
+      S.table_floor = std::max(S.table_floor, pow2_at_least(2 * S.last_table));
   }
   if (ef != S.last_ef) S.table_floor = 0;
   // the fast pass sizes its table for the mean query when it can spill in place; the exact pass keeps the maximum

@@ -892,46 +892,51 @@ struct PhaseClock<true> {  // lane i accumulates phase i: one compare and one 64
 template <int VT>
 struct VisitedLds;
 
+// VT = 0 tables hold any multiple of 64 entries: the home slot is the high word of hash x cap (v_mul_hi_u32), which for
+// a power of two is the hash's top bits, the same slot as a shift; probing wraps at cap.  Large id spaces use that to
+// size a table to its worst query without doubling it (100M ids at ef = 128: 6,144 entries, 6 wavefronts per CU,
+// where 8,192 allow 4; capi.cc learned_max_table).
 template <>
 struct VisitedLds<0> {
   u32* t;
-  u32 mask, shift;
-  __device__ __forceinline__ VisitedLds(void* base, const SearchArgs& A)
-      : t(static_cast<u32*>(base)), mask(A.vis_cap - 1), shift(32 - (31 - __clz(static_cast<int>(A.vis_cap)))) {}
+  u32 cap;
+  __device__ __forceinline__ VisitedLds(void* base, const SearchArgs& A) : t(static_cast<u32*>(base)), cap(A.vis_cap) {}
   static constexpr u32 kBytes = 4;
   using Hint = u32;  // the id's home word
   static __device__ __forceinline__ Hint unknown() { return INV; }
+  __device__ __forceinline__ u32 home(u32 x) const { return __umulhi(x * 0x9E3779B1u, cap); }
+  __device__ __forceinline__ u32 next(u32 h) const { return h + 1 == cap ? 0u : h + 1; }
   __device__ __forceinline__ void clear(const SearchArgs& A, int lane) {
     uint4* t4 = reinterpret_cast<uint4*>(t);
     for (u32 i = lane; i < A.vis_cap / 4; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
   }
-  __device__ __forceinline__ void insert_first(u32 x) { t[vhash(x, shift)] = x; }  // the table is empty
+  __device__ __forceinline__ void insert_first(u32 x) { t[home(x)] = x; }  // the table is empty
   // every id of the table into the HBM bitmap (the table's entries are the ids themselves)
   __device__ __forceinline__ void spill(u32* __restrict__ bits, const SearchArgs& A, int lane) const {
-    for (u32 i = lane; i <= mask; i += 64) {
+    for (u32 i = lane; i < cap; i += 64) {
       const u32 x = t[i];
       if (x < A.g.N) atomicOr(&bits[x >> 5], 1u << (x & 31));
     }
   }
   // the table's ids back out of the bitmap (whole words to zero: the bitmap goes back all zero)
   __device__ __forceinline__ void unspill(u32* __restrict__ bits, const SearchArgs& A, int lane) const {
-    for (u32 i = lane; i <= mask; i += 64) {
+    for (u32 i = lane; i < cap; i += 64) {
       const u32 x = t[i];
       if (x < A.g.N) bits[x >> 5] = 0u;
     }
   }
-  __device__ __forceinline__ bool at_home(u32 x) const { return t[vhash(x, shift)] == x; }
+  __device__ __forceinline__ bool at_home(u32 x) const { return t[home(x)] == x; }
   // the word at x's home slot (one read); home_match: x sits at home in that word
-  __device__ __forceinline__ u32 probe(u32 x) const { return t[vhash(x, shift)]; }
+  __device__ __forceinline__ u32 probe(u32 x) const { return t[home(x)]; }
   __device__ __forceinline__ bool home_match(u32 x, u32 w) const { return w == x; }
   // one exit from the probe loop (an early return per outcome compiles to a branchier loop and more live SGPRs).
   // hint: the home word as probe() read it since the last insert (INV: unknown), so a key found at home costs no
   // LDS operation and a home held by another key is skipped without a failed compare-and-swap
   __device__ __forceinline__ bool test_and_set(u32 x, bool& /*ovf*/, u32 hint = INV) {
-    u32 h = vhash(x, shift);
+    u32 h = home(x);
     bool fresh = false;
     if (hint == x) return false;
-    if (hint != INV) h = (h + 1) & mask;  // slots are never freed: home still holds that other key
+    if (hint != INV) h = next(h);  // slots are never freed: home still holds that other key
     for (;;) {
       const u32 old = atomicCAS(&t[h], INV, x);
       if (old == INV) {
@@ -939,7 +944,7 @@ struct VisitedLds<0> {
         break;
       }
       if (old == x) break;
-      h = (h + 1) & mask;
+      h = next(h);
     }
     return fresh;
   }

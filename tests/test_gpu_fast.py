@@ -247,6 +247,31 @@ def test_two_choice_tables_match_oracle(viscap, vis_bits, load, gpu_available, m
     np.testing.assert_array_equal(r.qstats[both][:, [0, 1, 2, 3, 4, 7]], w.qstats[both][:, [0, 1, 2, 3, 4, 7]])
 
 
+@pytest.mark.parametrize("viscap", ["1536", "320"])
+@pytest.mark.parametrize("mode", [L.MODE_FAST, L.MODE_EXACT])
+def test_u32_tables_of_any_multiple_of_64(viscap, mode, gpu_available, monkeypatch):
+    """u32 visited tables (VisitedLds<0>) of sizes that are not powers of two — the worst-query tables of large id
+    spaces (capi.cc learned_max_table: multiples of 1,024) — home slot hash x cap >> 32, probing wrapping at cap:
+    1,536 entries, and 320 (every query outgrows it and spills in place, the table decoded into the HBM bitmap).
+    Exact mode equals the oracle bit for bit, fast mode on every tie-free query."""
+    base = D.deep_like(6000, seed=331, d=96)
+    q = D.deep_like(200, seed=332, d=96)
+    dumps, _, _ = O.build(base, 16, 100, 0, 1, seed=6)
+    ref = O.OracleIndex(dumps, 96, 16, 0).knn(q, 10, 128, threads=8)
+    monkeypatch.setenv("SHINE_DEBUG_VISCAP", viscap)
+    monkeypatch.setenv("SHINE_DEBUG_VIS16", "0")
+    with shine_amd.Index.from_buffers(dumps, 96, 16, 0, gpus=[0]) as idx:
+        idx.set_search_mode(mode)
+        r = idx.knn(q, 10, 128)
+    if mode == L.MODE_EXACT:
+        assert (r.qstats[:, L.QS_STATUS] == 0).all()
+        np.testing.assert_array_equal(r.ids, ref[0])
+        np.testing.assert_array_equal(r.dists.view(np.uint32), ref[1].view(np.uint32))
+        np.testing.assert_array_equal(r.qstats[:, :5], ref[2][:, :5])
+    else:
+        _check_tie_free_exact(r, ref, 0.95)
+
+
 @pytest.mark.parametrize("mode", [L.MODE_FAST, L.MODE_EXACT])
 def test_learned_table_sizes_keep_results(mode, gpu_available):
     """The visited tables of a call are sized from the previous call's most-visited query on the same stream
