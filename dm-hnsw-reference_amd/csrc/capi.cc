@@ -580,8 +580,12 @@ uint32_t learned_max_table(const Scratch& S) {
   if (!S.seen.p || !S.seen.p[3] || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
   const uint64_t vmax = S.seen.p[4];
   if (vmax == 0) return 0;
-  const uint32_t want = static_cast<uint32_t>(std::min<uint64_t>(16384, vmax * 9 / 8));
-  const uint32_t t = env_int("SHINE_FAST_TABLE_POW2", 0) ? pow2_at_least(want) : (want + 1023) / 1024 * 1024;
+  // a multiple of 1,024 keeps 1/4 to spare, not 1/8: the worst query of the next call may visit more (TTI-shaped 50M
+  // at ef = 250, worst queries of 6.4K-8.0K from call to call: 9/8 rounded to 1,024 spilled often enough to cost 8 %,
+  // profiles/r04/scale_v6; 1/8 rounded to a power of two leaves more than 1/4)
+  const bool pow2 = env_int("SHINE_FAST_TABLE_POW2", 0) != 0;
+  const uint32_t want = static_cast<uint32_t>(std::min<uint64_t>(16384, pow2 ? vmax * 9 / 8 : vmax * 5 / 4));
+  const uint32_t t = pow2 ? pow2_at_least(want) : (want + 1023) / 1024 * 1024;
   return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, t}));
 }
 
