@@ -654,7 +654,13 @@ LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds
   const int64_t force16 = env_int("SHINE_DEBUG_VIS16", -1);
   const bool can16 = force16 != 0 && kind16(t16) != 0 && (kind16(t16) == 1 || env_int("SHINE_TWO_CHOICE", 1) != 0);
   const uint64_t w32 = resident(t32, 4), w16 = can16 ? resident(t16, 2) : 0;
-  sh.vis16 = can16 && (w16 > w32 || (w16 == w32 && t16 > t32)) ? kind16(t16) : 0;
+  // at equal residency the larger u16 table wins; in two-choice buckets only where it holds twice the u32 table's
+  // entries (the u32 one is then the spilling half-size table): a two-choice lookup reads two buckets and plans its
+  // insert, dearer than a u32 probe — TTI-shaped 50M: 16,384 two-choice entries ran at 1.35 M QPS against 8,192-9,216
+  // u32 entries (the worst query's size) at 1.55 M, both 4 wavefronts per CU (profiles/r04/scale_v7); at 10M 8,192
+  // two-choice entries against 4,096 u32 ones, 2.45 M against 2.14 M
+  const bool tie16 = w16 == w32 && t16 > t32 && (kind16(t16) == 1 || t16 >= 2 * t32);
+  sh.vis16 = can16 && (w16 > w32 || tie16) ? kind16(t16) : 0;
   if (force16 >= 1 && can16) sh.vis16 = kind16(t16);  // test hook: force the u16 entries
   sh.vis_cap = sh.vis16 ? t16 : t32;
   sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
