@@ -573,20 +573,24 @@ uint32_t learned_mean_table(const Scratch& S) {
 }
 
 // The previous call's worst query with 1/8 to spare (large id spaces, see enqueue_search).
-// u32 tables (VisitedLds<0>) take any multiple of 64 entries: rounded up to 1,024, not to a power of two (100M ids at
-// ef = 128: 6,144 entries and 6 wavefronts per CU instead of 8,192 and 4; SHINE_FAST_TABLE_POW2=1 restores the
-// doubling for comparison).  u16 entries need a power of two (pick_fast_shape rounds them up).
-uint32_t learned_max_table(const Scratch& S) {
+// The previous call's worst query with room to spare, for u32 tables (VisitedLds<0>), which take any multiple of 64
+// entries: 9/8 of it rounded up to a power of two, or — where that puts more wavefronts on a CU (one batch's worth,
+// `need`) — 5/4 of it rounded up to 1,024 entries.  100M ids at ef = 128: 6,144 entries and 6 wavefronts per CU
+// instead of 8,192 and 4, 3.97 M against 3.75 M QPS (profiles/r04/diag100m_nonpow2_tables.jsonl); 1/4 to spare, since
+// the next call's worst query may visit more.  Where the multiple of 1,024 gains no wavefront the power of two stays:
+// TTI-shaped 50M at ef = 250 (worst queries 6.4K-8.0K from call to call) ran at 1.35 M QPS on 9,216-10,240 entries
+// against 1.55 M on 8,192 (profiles/r04/scale_v6..v8).  SHINE_FAST_TABLE_POW2=1: always the power of two.
+uint32_t learned_max_table(const Scratch& S, uint32_t ef, uint32_t lds_per_cu) {
   if (!S.seen.p || !S.seen.p[3] || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
   const uint64_t vmax = S.seen.p[4];
   if (vmax == 0) return 0;
-  // a multiple of 1,024 keeps 1/4 to spare, not 1/8: the worst query of the next call may visit more (TTI-shaped 50M
-  // at ef = 250, worst queries of 6.4K-8.0K from call to call: 9/8 rounded to 1,024 spilled often enough to cost 8 %,
-  // profiles/r04/scale_v6; 1/8 rounded to a power of two leaves more than 1/4)
-  const bool pow2 = env_int("SHINE_FAST_TABLE_POW2", 0) != 0;
-  const uint32_t want = static_cast<uint32_t>(std::min<uint64_t>(16384, pow2 ? vmax * 9 / 8 : vmax * 5 / 4));
-  const uint32_t t = pow2 ? pow2_at_least(want) : (want + 1023) / 1024 * 1024;
-  return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, t}));
+  auto clampt = [&](uint32_t t) { return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, t})); };
+  const uint32_t p2 = clampt(pow2_at_least(static_cast<uint32_t>(std::min<uint64_t>(16384, vmax * 9 / 8))));
+  if (env_int("SHINE_FAST_TABLE_POW2", 0)) return p2;
+  const uint32_t want = static_cast<uint32_t>(std::min<uint64_t>(16384, vmax * 5 / 4));
+  const uint32_t np = clampt((want + 1023) / 1024 * 1024);
+  auto waves = [&](uint32_t t) { return lds_per_cu / search_fast_lds_bytes(t, ef, 4); };
+  return waves(np) > waves(p2) ? np : p2;
 }
 
 // The exact pass's learned table, with the in-place spill: just the previous call's worst query (eighths/8 × its
@@ -869,7 +873,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     if (!spill_enabled()) {
       learned_fast = learned;
     } else {
-      const uint32_t mean_t = learned_mean_table(S), max_t = learned_max_table(S);
+      const uint32_t mean_t = learned_mean_table(S), max_t = learned_max_table(S, ef, R.lds_per_cu);
       const uint64_t need = std::min<uint64_t>(16, (nq + R.cus - 1) / R.cus);
       const bool max_fits = max_t && R.lds_per_cu / search_fast_lds_bytes(max_t, ef, 4) >= need;
       const bool beyond_l2 = 4ull * h->words_per_slot > kXcdL2Bytes;
