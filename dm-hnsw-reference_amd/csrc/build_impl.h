@@ -13,6 +13,16 @@
 //     a row that would exceed m_max (2M at level 0, M above) is re-pruned with select_heuristic(m_max) over its old
 //     entries and all its new ones together (the reference prunes once per incoming edge, :191-221).
 // Distances are the search kernels' (dist_list: the reference's AVX2 accumulation order).
+//
+// Deliberate differences from the reference's insert (DESIGN §4 "GPU batch builder"), all by construction:
+//   * records of one batch do not see each other (a batch is <= 2 % of the graph built so far);
+//   * the level-0 beam of a record with upper levels starts from the greedy descent's node (the search kernel's
+//     descent with ef = 1 through every level), not from the closest node of its own level-1 beam as hnsw.hh:227-230
+//     leaves it: the level-0 searches of a whole batch run as one search-kernel launch before the upper beams, which
+//     only ~1/M of the records run.  Its level-0 beam starts from a node no closer than the reference's; the GPU-built graph's
+//     recall is within 1e-4 of the CPU builder's at 1M (profiles/r04/cmp1m_gpu_vs_cpu_build.jsonl);
+//   * a row receiving several new entries in one batch is re-pruned once over all of them (the reference prunes per
+//     incoming edge, :191-221).
 #pragma once
 
 #include "kernels_impl.h"

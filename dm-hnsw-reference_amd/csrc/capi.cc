@@ -108,6 +108,12 @@ void release_state(IndexState* h) {
     R.hd.release();
     R.hids.release();
     R.hqs.release();
+    for (hipStream_t s : R.hstreams) (void)hipStreamDestroy(s);
+    for (hipEvent_t e : R.hjoin) (void)hipEventDestroy(e);
+    if (R.hfork) (void)hipEventDestroy(R.hfork);
+    R.hstreams.clear();
+    R.hjoin.clear();
+    R.hfork = nullptr;
     if (R.ev0) (void)hipEventDestroy(R.ev0);
     if (R.ev1) (void)hipEventDestroy(R.ev1);
     if (R.stream) (void)hipStreamDestroy(R.stream);
@@ -135,8 +141,11 @@ hipMemAllocationProp device_prop(int device) {
 // over a view without holes (per-piece grants on views with holes were refused by the driver).
 int map_sharded(ShardedArray& A, uint64_t stride, size_t cached, const std::vector<int>& devs, size_t gran) {
   const size_t G = devs.size();
+  // the plan (views.cc, host-only and tested on CPU): which allocation backs every piece of every view, and the
+  // devices every view grants access to
+  const ViewPlan P = plan_views(devs, stride, cached);
   A.stride = stride;
-  A.cached = G > 1 ? std::min<size_t>(cached, stride) : 0;
+  A.cached = P.cached;
   A.hot.assign(G, 0);
   A.cold.assign(G, 0);
   A.copy.assign(G * G, 0);  // [o * G + q]: slot o's local copy of slot q's hot prefix
@@ -147,15 +156,6 @@ int map_sharded(ShardedArray& A, uint64_t stride, size_t cached, const std::vect
     for (size_t q = 0; q < G; ++q)
       if (A.cached && q != o) HIP_TRY(hipMemCreate(&A.copy[o * G + q], A.cached, &prop, 0));
   }
-  std::vector<int> uniq(devs);
-  std::sort(uniq.begin(), uniq.end());
-  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
-  std::vector<hipMemAccessDesc> acc(uniq.size());
-  for (size_t i = 0; i < uniq.size(); ++i) {
-    acc[i].location.type = hipMemLocationTypeDevice;
-    acc[i].location.id = uniq[i];
-    acc[i].flags = hipMemAccessFlagsProtReadWrite;
-  }
   A.view.resize(G);
   for (size_t o = 0; o < G; ++o) {
     StripedRange& V = A.view[o];
@@ -163,16 +163,20 @@ int map_sharded(ShardedArray& A, uint64_t stride, size_t cached, const std::vect
     void* va = nullptr;
     HIP_TRY(hipMemAddressReserve(&va, V.bytes, gran, nullptr, 0));
     V.va = static_cast<char*>(va);
-    for (size_t q = 0; q < G; ++q) {
-      const size_t base = q * stride;
-      if (A.cached) {  // hot prefix: the owner's memory in its own view, a local copy in every other view
-        HIP_TRY(hipMemMap(V.va + base, A.cached, 0, q == o ? A.hot[q] : A.copy[o * G + q], 0));
-        V.maps.emplace_back(base, A.cached);
-      }
-      if (A.cached < stride) {
-        HIP_TRY(hipMemMap(V.va + base + A.cached, stride - A.cached, 0, A.cold[q], 0));
-        V.maps.emplace_back(base + A.cached, stride - A.cached);
-      }
+    for (const ViewPiece& p : P.pieces[o]) {
+      // own stripe: this slot's hot / cold allocation; a copy: this slot's copy of the stripe's hot prefix; a peer
+      // piece: the owner's cold allocation (on the owner's GPU)
+      const hipMemGenericAllocationHandle_t backing = p.kind == 1 ? A.copy[o * G + p.stripe]
+                                                      : p.hot     ? A.hot[p.stripe]
+                                                                  : A.cold[p.stripe];
+      HIP_TRY(hipMemMap(V.va + p.offset, p.size, 0, backing, 0));
+      V.maps.emplace_back(p.offset, p.size);
+    }
+    std::vector<hipMemAccessDesc> acc(P.access[o].size());
+    for (size_t i = 0; i < acc.size(); ++i) {
+      acc[i].location.type = hipMemLocationTypeDevice;
+      acc[i].location.id = P.access[o][i];
+      acc[i].flags = hipMemAccessFlagsProtReadWrite;
     }
     const hipError_t e = hipMemSetAccess(V.va, V.bytes, acc.data(), acc.size());
     if (e != hipSuccess)
@@ -254,16 +258,14 @@ int make_index(HostGraph G, int elem, const int* gpu_ids, uint32_t n_gpus, int p
                                           "; the kernels are built for gfx950 (MI355X) only");
   }
   if (sharded) {  // every slot dereferences every other slot's stripe: each ordered pair needs a peer path (xGMI)
-    for (int a : devs)
-      for (int b : devs) {
-        if (a == b) continue;
-        int can = 0;
-        HIP_TRY(hipDeviceCanAccessPeer(&can, a, b));
-        if (!can)
-          return set_error(SHINE_ERR_HIP, "GPU " + std::to_string(a) + " cannot access GPU " + std::to_string(b) +
-                                              "'s memory (no peer path): the sharded placement needs all-to-all "
-                                              "peer access");
-      }
+    for (const auto& [a, b] : plan_views(devs, 1, 0).peer_pairs) {
+      int can = 0;
+      HIP_TRY(hipDeviceCanAccessPeer(&can, a, b));
+      if (!can)
+        return set_error(SHINE_ERR_HIP, "GPU " + std::to_string(a) + " cannot access GPU " + std::to_string(b) +
+                                            "'s memory (no peer path): the sharded placement needs all-to-all "
+                                            "peer access");
+    }
   }
 
   std::unique_ptr<shine_index> h(new shine_index);
@@ -562,11 +564,12 @@ uint32_t learned_table(const Scratch& S) {
 // config_lines_cfg3_10m_final.jsonl), and a table sized for the maximum holds half the wavefronts per CU.  Never below
 // the floor a call that exhausted the spill bitmaps set.
 uint32_t learned_mean_table(const Scratch& S) {
-  // (the visited sum is a u32 word of per-query counts capped at 16,384: calls of up to 2^18 queries cannot wrap it;
-  // seen[6] is the queries of the call that wrote the sum, which need not be the last one enqueued)
+  // (the visited sum is a u32 word of per-query counts capped at 16,384: calls of fewer than 2^18 queries cannot wrap
+  // it — 2^18 x 2^14 is 2^32; seen[6] is the queries of the call that wrote the sum, which need not be the last one
+  // enqueued)
   if (!S.seen.p || !S.seen.p[3] || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
   const uint32_t nq = S.seen.p[6];
-  if (nq == 0 || nq > (1u << 18)) return 0;
+  if (nq == 0 || nq >= (1u << 18)) return 0;
   const uint32_t mean = S.seen.p[5] / nq;
   if (mean == 0) return 0;
   return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, pow2_at_least(mean + mean / 4 + 64)}));
@@ -1287,6 +1290,29 @@ int apply_dynamic(shine_index* h, Replica& R, shine_stats* agg) {
   return 0;
 }
 
+// Queries per chunk of a large host-API call (the bench's batch) and the chunks in flight per slot: four, as the bench
+// keeps four batches in flight (2 -> 4 in flight: +27 % QPS, profiles/r02/inflight_scan_bucketed.jsonl).
+constexpr uint32_t kHostChunk = 1024;
+constexpr uint32_t kHostStreams = 4;
+
+// The slot's host streams and their events, created together on first use: streams created back to back take
+// consecutive hardware queues of HIP's round-robin, so four chunks in flight run on four queues (two batches sharing a
+// queue run back to back: DESIGN §4 "Hardware queues").
+int ensure_host_streams(Replica& R) {
+  if (!R.hstreams.empty()) return 0;
+  const uint32_t n = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_HOST_STREAMS", kHostStreams)));
+  for (uint32_t i = 0; i < n; ++i) {
+    hipStream_t s = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    R.hstreams.push_back(s);
+    hipEvent_t e = nullptr;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    R.hjoin.push_back(e);
+  }
+  HIP_TRY(hipEventCreateWithFlags(&R.hfork, hipEventDisableTiming));
+  return 0;
+}
+
 // shine_knn_batch with the handle locked.  access (nullable): per-slot device counters of record reads (warmup).
 int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k, uint32_t ef,
              uint32_t* out_ids, float* out_dists, uint32_t* qstats, shine_stats* stats,
@@ -1315,9 +1341,18 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
       if (part[r].empty()) continue;
       (void)hipSetDevice(h->reps[r].device);
       (void)hipStreamSynchronize(h->reps[r].stream);
+      for (hipStream_t hs : h->reps[r].hstreams) (void)hipStreamSynchronize(hs);
     }
     return rc;
   };
+  // Calls of more than `chunk` queries on a slot are split into chunks kept in flight (SHINE_HOST_CHUNK, default
+  // 1,024: the bench's batch; 0 = never split).  Not while the dynamic cache logs a call (its replay orders admissions
+  // by query within one launch) or a warmup counts reads.
+  const int64_t chunk_env = env_int("SHINE_HOST_CHUNK", kHostChunk);
+  const uint32_t chunk = (chunk_env <= 0 || access || h->cache_policy == SHINE_CACHE_DYNAMIC)
+                             ? 0xFFFFFFFFu
+                             : static_cast<uint32_t>(std::min<int64_t>(chunk_env, 0x7FFFFFFF));
+  std::vector<uint8_t> chunked(G, 0);
   // every slot's batch is staged through pinned host memory and enqueued before any wait
   for (uint32_t r = 0; r < G; ++r) {
     const uint32_t n = static_cast<uint32_t>(part[r].size());
@@ -1342,8 +1377,32 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     if (pe == hipSuccess) pe = hipHostGetDevicePointer(reinterpret_cast<void**>(&dd), R.hd.p, 0);
     if (pe == hipSuccess) pe = hipHostGetDevicePointer(reinterpret_cast<void**>(&dqs), R.hqs.p, 0);
     if (pe != hipSuccess) return drain(r, set_error(SHINE_ERR_HIP, std::string("hipHostGetDevicePointer: ") + hipGetErrorString(pe)));
-    if (int rc = enqueue_search(h, R, dq, n, k, ef, dids, dd, dqs, R.stream, true, access ? (*access)[r].p : nullptr))
-      return drain(r + 1, rc);
+    if (n <= chunk) {
+      if (int rc = enqueue_search(h, R, dq, n, k, ef, dids, dd, dqs, R.stream, true, access ? (*access)[r].p : nullptr))
+        return drain(r + 1, rc);
+      continue;
+    }
+    // A large call runs as chunks of `chunk` queries kept in flight on the slot's host streams, as a serving loop keeps
+    // batches in flight (the last, longest queries of one chunk overlap the next chunks' first ones): forked from the
+    // handle's stream (after anything enqueued there, e.g. dynamic-cache updates) and joined back into it, so the
+    // waits below and the event span see the whole call.
+    if (int rc = ensure_host_streams(R)) return drain(r, rc);
+    HIP_TRY(hipEventRecord(R.ev0, R.stream));
+    HIP_TRY(hipEventRecord(R.hfork, R.stream));
+    for (hipStream_t hs : R.hstreams) HIP_TRY(hipStreamWaitEvent(hs, R.hfork, 0));
+    for (uint32_t c = 0, off = 0; off < n; ++c, off += chunk) {
+      const uint32_t m = std::min(chunk, n - off);
+      hipStream_t hs = R.hstreams[c % R.hstreams.size()];
+      if (int rc = enqueue_search(h, R, dq + static_cast<size_t>(off) * d, m, k, ef, dids + static_cast<size_t>(off) * k,
+                                  dd + static_cast<size_t>(off) * k, dqs + static_cast<size_t>(off) * kQsWords, hs, false))
+        return drain(r + 1, rc);  // (the slot's host streams drain with the device below)
+    }
+    for (size_t i = 0; i < R.hstreams.size(); ++i) {
+      HIP_TRY(hipEventRecord(R.hjoin[i], R.hstreams[i]));
+      HIP_TRY(hipStreamWaitEvent(R.stream, R.hjoin[i], 0));
+    }
+    HIP_TRY(hipEventRecord(R.ev1, R.stream));
+    chunked[r] = 1;
   }
   double kernel_ms = 0;
   uint64_t retries = 0;
@@ -1357,8 +1416,15 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     HIP_TRY(hipEventElapsedTime(&ms, R.ev0, R.ev1));
     kernel_ms = std::max(kernel_ms, static_cast<double>(ms));
     if (r < h->slot_rate.size() && ms > 0) h->slot_rate[r] = n / static_cast<double>(ms);
-    const uint32_t* cnt = R.main.seen.p;  // written by the call's last pass (finish_call)
-    retries += cnt[0] + cnt[1] + cnt[2];  // queries handed on by each pass
+    if (!chunked[r]) {
+      const uint32_t* cnt = R.main.seen.p;  // written by the call's last pass (finish_call)
+      retries += cnt[0] + cnt[1] + cnt[2];  // queries handed on by each pass
+    } else {  // chunks: the last chunk of every host stream (its counter words hold its own call only)
+      for (hipStream_t hs : R.hstreams) {
+        const uint32_t* cnt = scratch_for(R, hs).seen.p;
+        if (cnt && cnt[3]) retries += cnt[0] + cnt[1] + cnt[2];
+      }
+    }
     if (env_int("SHINE_PHASE_PROFILE", 0) && R.prof.p) print_phase_profile(h, R);
   }
   int rc = SHINE_OK;

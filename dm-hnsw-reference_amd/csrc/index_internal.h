@@ -15,6 +15,7 @@
 #include "graph.h"
 #include "kernels.h"
 #include "placement.h"
+#include "views.h"
 
 #define HIP_TRY(expr)                                                                              \
   do {                                                                                             \
@@ -163,6 +164,11 @@ struct Replica {
   // staging for the host-pointer API: pinned, mapped into the GPU's address space (the kernels read and write it)
   HostBuf<float> hq, hd;
   HostBuf<uint32_t> hids, hqs;
+  // the host-pointer API's own in-flight streams: a call of more than one chunk (shine_knn_batch, kHostChunk queries)
+  // runs its chunks over them, forked from and joined back into `stream` by events
+  std::vector<hipStream_t> hstreams;
+  std::vector<hipEvent_t> hjoin;
+  hipEvent_t hfork = nullptr;
   DevBuf<unsigned long long> prof;  // SHINE_PHASE_PROFILE diagnostics
   // dynamic record cache (SHINE_CACHE_DYNAMIC): this GPU's arena, lookup table, logs and the host policy engine
   DevBuf<uint32_t> cslot, cool, rlog, logn, upd;

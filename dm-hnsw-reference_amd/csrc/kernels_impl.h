@@ -1168,7 +1168,9 @@ struct VisitedLds<2> {
     const u32 h = image(x), rem = h & rmask, b1 = h >> rbits, b2 = (b1 ^ alt(rem)) & bmask_b;
     const uint4 w1 = bucket(b1), w2 = bucket(b2);
     const u32 e = rem << 1;
-    if (VisitedLds<1>::has(w1, e) || VisitedLds<1>::has(w2, e | 1u)) return Plan2{kPresent, 0u, 0u};
+    // rem 0x7FFF never goes to b2 (its b2 entry would be the empty marker 0xFFFF, which any bucket with a free entry
+    // "holds"): only b1 is looked at for it
+    if (VisitedLds<1>::has(w1, e) | (VisitedLds<1>::has(w2, e | 1u) & (rem != 0x7FFFu))) return Plan2{kPresent, 0u, 0u};
     // each bucket's first empty entry once: its position is the bucket's fill (entries fill in order)
     int j1, j2;
     u32 k1, k2, o1, o2;

@@ -127,6 +127,19 @@ class GpuBuildStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class ViewPiece(C.Structure):
+    _fields_ = [
+        ("view_slot", C.c_uint32),
+        ("stripe", C.c_uint32),
+        ("offset", C.c_uint64),
+        ("size", C.c_uint64),
+        ("backing_device", C.c_int32),
+        ("kind", C.c_uint32),
+    ]
+
+
+VIEW_OWN, VIEW_COPY, VIEW_PEER = 0, 1, 2
+
 P = C.c_void_p
 U32, U64, I32 = C.c_uint32, C.c_uint64, C.c_int
 PU8 = C.POINTER(C.c_uint8)
@@ -153,6 +166,8 @@ PROTOTYPES = {
     "shine_distance_batch_device": (I32, [P, U32, P, U32, P, U32, P, P]),
     "shine_route": (I32, [P, P, U32, P]),
     "shine_plan_regions": (I32, [C.POINTER(PU8), C.POINTER(U64), U32, U32, U32, I32, U32, P, U64, P, P, P]),
+    "shine_plan_sharded_views": (I32, [C.POINTER(I32), U32, U64, U64, P, U64, C.POINTER(U64), P, P, P,
+                                       C.POINTER(U32)]),
     "shine_kmeans": (I32, [P, U64, U32, I32, U32, I32, P, P, P, P, P]),
     "shine_router_run": (I32, [P, P, U32, U32, U32, I32, P, U32, P, U32, I32, P, P]),
     "shine_set_search_mode": (I32, [P, I32]),

@@ -233,13 +233,16 @@ class GpuBuild:
         L.check(L.lib().shine_gpu_build_get_stats(self._h, C.byref(st)))
         return st.as_dict()
 
-    def dumps(self, n_shards: int = 1) -> list[np.ndarray]:
+    def dumps(self, n_shards: int = 1, copy: bool = True) -> list[np.ndarray]:
+        """The dump images of n_shards memory nodes.  copy=False: views of the build's own host buffers (no second
+        copy of a 60 GB index), valid until the next dumps() call or close()."""
         L.check(L.lib().shine_gpu_build_dumps(self._h, n_shards))
         out = []
         for s in range(n_shards):
             n = L.lib().shine_gpu_build_dump_size(self._h, s)
             p = L.lib().shine_gpu_build_dump_data(self._h, s)
-            out.append(np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(n,)).copy())
+            v = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(n,))
+            out.append(v.copy() if copy else v)
         return out
 
     def write(self, directory: str) -> None:
@@ -322,6 +325,27 @@ def router_run(centroids: np.ndarray, mapping: np.ndarray, k: int, queries: np.n
                                      None if qs is None else _ptr(qs), 0 if qs is None else qs.shape[0], int(adaptive),
                                      _ptr(out), _ptr(lim)))
     return out, lim
+
+
+def plan_sharded_views(gpus, stride_bytes: int, cached_bytes: int = 0) -> dict:
+    """Host-only view plan of SHINE_PLACE_SHARDED (shine_plan_sharded_views; the plan shine_open_ex maps).
+    Returns {"pieces": [dict per piece], "access": [[devices] per view], "peer_pairs": [(a, b), ...]}."""
+    g = (C.c_int * len(gpus))(*gpus)
+    G = len(gpus)
+    n = C.c_uint64()
+    L.check(L.lib().shine_plan_sharded_views(g, G, stride_bytes, cached_bytes, None, 0, C.byref(n), None, None, None,
+                                             None))
+    pieces = (L.ViewPiece * max(1, n.value))()
+    access = np.zeros(G * G, np.int32)
+    n_access = np.zeros(G, np.uint32)
+    pairs = np.zeros(2 * G * G, np.int32)
+    n_pairs = C.c_uint32()
+    L.check(L.lib().shine_plan_sharded_views(g, G, stride_bytes, cached_bytes, C.cast(pieces, C.c_void_p), n.value,
+                                             C.byref(n), _ptr(access), _ptr(n_access), _ptr(pairs), C.byref(n_pairs)))
+    out = [{k: getattr(pieces[i], k) for k, _ in L.ViewPiece._fields_} for i in range(n.value)]
+    acc = [access[o * G:o * G + int(n_access[o])].tolist() for o in range(G)]
+    pp = [(int(pairs[2 * i]), int(pairs[2 * i + 1])) for i in range(n_pairs.value)]
+    return {"pieces": out, "access": acc, "peer_pairs": pp}
 
 
 def graph_stats(dumps, dim: int, M: int) -> dict:

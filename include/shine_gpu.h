@@ -241,6 +241,30 @@ int shine_plan_regions(const uint8_t* const* dumps, const uint64_t* sizes, uint3
                        int metric, uint32_t k, uint32_t* region_of_uid, uint64_t uid_capacity, float* centroids,
                        uint32_t* mapping, uint32_t* n_centroids);
 
+/* Host-only view plan of SHINE_PLACE_SHARDED (no device needed; the same plan shine_open_ex maps): for n_slots GPU
+ * slots on gpu_ids (ids may repeat), a sharded array of stride_bytes per slot's stripe, whose leading cached_bytes every
+ * other slot keeps a local copy of.  Every slot's view maps the whole id space, G x stride_bytes: its own stripe
+ * (SHINE_VIEW_OWN), its local copies of the other stripes' hot prefixes (SHINE_VIEW_COPY) and the other stripes' cold
+ * rows backed by their owners' HBM (SHINE_VIEW_PEER: xGMI reads between distinct GPUs) — the reference's RemotePtr
+ * memory node (remote_pointer.hh:9-22) becomes the stripe, a remote read a peer load.  pieces (capacity cap_pieces;
+ * nullable to count): every view's pieces, view by view in offset order.  access (nullable, n_slots x n_slots):
+ * row o holds the n_access[o] devices granted access to view o.  peer_pairs (nullable, 2 x n_slots x n_slots): the
+ * ordered (accessor, owner) device pairs that need a peer path, n_peer_pairs of them. */
+#define SHINE_VIEW_OWN 0
+#define SHINE_VIEW_COPY 1
+#define SHINE_VIEW_PEER 2
+typedef struct shine_view_piece {
+  uint32_t view_slot;      /* the slot whose view holds the piece */
+  uint32_t stripe;         /* the slot whose rows the piece holds */
+  uint64_t offset;         /* in the view's virtual range */
+  uint64_t size;
+  int32_t backing_device;  /* the GPU whose allocation backs the piece */
+  uint32_t kind;           /* SHINE_VIEW_* */
+} shine_view_piece;
+int shine_plan_sharded_views(const int* gpu_ids, uint32_t n_slots, uint64_t stride_bytes, uint64_t cached_bytes,
+                             shine_view_piece* pieces, uint64_t cap_pieces, uint64_t* n_pieces, int* access,
+                             uint32_t* n_access, int* peer_pairs, uint32_t* n_peer_pairs);
+
 /* Kmeans<Distance> over n rows (kmeans.hh:10-378), host-only: balanced != 0 is run_and_optimize (balanced k-means,
  * c = 0.15, penalty factor 1.01, max size difference 1; odd k runs 2k clusters and merges the closest pairs),
  * balanced == 0 is run_kmeans with k clusters.  centroids: capacity 2k x dim; mapping: capacity 2k (centroid ->

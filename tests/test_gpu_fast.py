@@ -247,6 +247,37 @@ def test_two_choice_tables_match_oracle(viscap, vis_bits, load, gpu_available, m
     np.testing.assert_array_equal(r.qstats[both][:, [0, 1, 2, 3, 4, 7]], w.qstats[both][:, [0, 1, 2, 3, 4, 7]])
 
 
+@pytest.mark.parametrize("mode", [L.MODE_FAST, L.MODE_EXACT])
+def test_two_choice_remainder_0x7fff_is_visited(mode, gpu_available, monkeypatch):
+    """At 15-bit remainders (24-bit ids, 4,096 entries) the remainder 0x7FFF has no b2 entry: its b2 encoding is the
+    empty marker.  Ids whose permuted image ends in 0x7FFF (20655 + k * 32768 under the 0x9E3779B1 multiply) must
+    still be visited: queries placed on record 20655 of a 24K-record index find it first, bit for bit the oracle's
+    search (such ids were reported present by every bucket with a free entry, and never reached)."""
+    base = D.deep_like(24000, seed=97, d=96)
+    rng = np.random.default_rng(5)
+    bad = 20655
+    assert (bad * 0x9E3779B1) & 0x7FFF == 0x7FFF
+    q = np.concatenate([base[bad] + rng.normal(0, 1e-3, (32, 96)).astype(np.float32),
+                        D.deep_like(96, seed=98, d=96)]).astype(np.float32)
+    dumps, _, _ = O.build(base, 16, 100, 0, 1, seed=4)
+    ref = O.OracleIndex(dumps, 96, 16, 0).knn(q, 10, 128, threads=8)
+    assert (ref[0][:32] == bad).any(1).all()  # the oracle finds the record (uid == row for one shard)
+    monkeypatch.setenv("SHINE_DEBUG_VISCAP", "4096")
+    monkeypatch.setenv("SHINE_DEBUG_VIS_BITS", "24")
+    monkeypatch.setenv("SHINE_DEBUG_VIS16", "2")
+    monkeypatch.setenv("SHINE_EXACT_TWO_CHOICE", "1")
+    with shine_amd.Index.from_buffers(dumps, 96, 16, 0, gpus=[0]) as idx:
+        idx.set_search_mode(mode)
+        r = idx.knn(q, 10, 128)
+    assert (r.ids[:32] == bad).any(1).all()
+    if mode == L.MODE_EXACT:
+        np.testing.assert_array_equal(r.ids, ref[0])
+        np.testing.assert_array_equal(r.dists.view(np.uint32), ref[1].view(np.uint32))
+        np.testing.assert_array_equal(r.qstats[:, :5], ref[2][:, :5])
+    else:
+        _check_tie_free_exact(r, ref, 0.95)
+
+
 @pytest.mark.parametrize("viscap", ["1536", "320"])
 @pytest.mark.parametrize("mode", [L.MODE_FAST, L.MODE_EXACT])
 def test_u32_tables_of_any_multiple_of_64(viscap, mode, gpu_available, monkeypatch):
@@ -371,3 +402,30 @@ def test_byte_rows_spill_in_place_like_f32_rows(gpu_available, monkeypatch, vis1
     np.testing.assert_array_equal(b.dists.view(np.uint32), f.dists.view(np.uint32))
     np.testing.assert_array_equal(b.qstats[:, :8], f.qstats[:, :8])
     _check_tie_free_exact(b, ref, 0.25)
+
+
+@pytest.mark.parametrize("mode", [L.MODE_FAST, L.MODE_EXACT])
+def test_host_api_splits_large_calls_into_chunks_in_flight(mode, gpu_available, monkeypatch):
+    """shine_knn_batch with more queries than one chunk (capi.cc knn_host, 1,024 queries per chunk, four host streams
+    forked from and joined into the handle's stream) returns exactly what one launch over the whole call returns
+    (SHINE_HOST_CHUNK=0), query by query: ids, distances and counters; exact mode also equals the oracle."""
+    base = D.deep_like(5000, seed=401, d=96)
+    q = D.deep_like(4500, seed=402, d=96)  # four full chunks and a partial one
+    dumps, _, _ = O.build(base, 16, 80, 0, 1, seed=7)
+    out = {}
+    for chunk in ("0", "1024", "700"):
+        monkeypatch.setenv("SHINE_HOST_CHUNK", chunk)
+        with shine_amd.Index.from_buffers(dumps, 96, 16, 0, gpus=[0]) as idx:
+            idx.set_search_mode(mode)
+            out[chunk] = [idx.knn(q, 10, 64) for _ in range(2)]  # the second call runs on learned tables
+    want = out["0"][0]
+    assert (want.qstats[:, L.QS_STATUS] == 0).all()
+    for chunk, runs in out.items():
+        for r in runs:
+            np.testing.assert_array_equal(r.ids, want.ids)
+            np.testing.assert_array_equal(r.dists.view(np.uint32), want.dists.view(np.uint32))
+            np.testing.assert_array_equal(r.qstats[:, :5], want.qstats[:, :5])
+            assert r.stats["processed"] == q.shape[0] and r.stats["kernel_ms"] > 0
+    if mode == L.MODE_EXACT:
+        ref_ids, ref_d, _ = O.OracleIndex(dumps, 96, 16, 0).knn(q[:300], 10, 64, threads=8)
+        np.testing.assert_array_equal(want.ids[:300], ref_ids)

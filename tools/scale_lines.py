@@ -79,6 +79,8 @@ def run(name, a):
     gb, st = build_gpu(torch, shine_amd, base_t, M, efc, metric, a, name)
     del base_t
     torch.cuda.empty_cache()
+    orc = oracle_sample(shine_amd, gb, q, a.k, int((a.ef or str(ef)).split(",")[0]), dim, M, metric,
+                        8 if name == "cfg4" else 1, a.cmp_oracle_n) if a.cmp_oracle else None
     lines = []
     # slots > 1: the same graph as `slots` memory-node dumps under SHINE_PLACE_SHARDED over GPU slots that repeat this
     # box's device (the 8-slot emulation of configs[3]/[4]); every slot answers 1/slots of each batch.  The replica
@@ -92,10 +94,47 @@ def run(name, a):
             for line in run_measure(torch, idx, name, a, q, gt, batch, slots, ef, kind, n, dim, metric, M, efc,
                                     placement, alpha, nq, elem, st):
                 line["repeat"] = rep
+                if orc is not None:
+                    line["oracle"] = orc
+                    line["oracle_equals_exact_on_gpu_dump"] = orc["oracle_equals_exact_on_gpu_dump"]
                 lines.append(line)
         idx.close()
     gb.close()
     return lines
+
+
+def oracle_sample(shine_amd, gb, q, k, ef, dim, M, metric, shards, n_sample):
+    """The oracle's knn (checker; hnsw.hh:253-307) on the GPU-built index's dump images against exact mode on f32
+    rows of the same graph (the oracle's element type; fp16 workloads are measured on fp16 rows, this check runs on
+    f32 rows of the same dump), n_sample queries spread over the measured set: ids in heap order, distances bitwise,
+    counters."""
+    import oracle as O
+    L = shine_amd._lib
+    qn = q.cpu().numpy()
+    sel = np.linspace(0, qn.shape[0] - 1, n_sample).astype(np.int64)
+    qs = np.ascontiguousarray(qn[sel])
+    t0 = time.time()
+    with gb.open_ex(1, elem=L.ELEM_F32, gpus=[0]) as ix:
+        ix.set_search_mode(L.MODE_EXACT)
+        ex = ix.knn(qs, k, ef)
+    with Heartbeat(f"oracle sample: dump images of {shards} memory nodes"):
+        dumps = gb.dumps(shards, copy=False)
+    t1 = time.time()
+    with Heartbeat(f"oracle sample: {n_sample} queries"):
+        I = O.OracleIndex(dumps, dim, M, metric)
+        ref_ids, ref_d, ref_qs = I.knn(qs, k, ef, threads=host_threads())
+        I.close()
+    del dumps
+    same_ids = np.array_equal(ex.ids, ref_ids)
+    same_d = np.array_equal(ex.dists.view(np.uint32), ref_d.view(np.uint32))
+    same_qs = np.array_equal(ex.qstats[:, :5], ref_qs[:, :5])
+    out = {"oracle_equals_exact_on_gpu_dump": bool(same_ids and same_d and same_qs), "queries": int(n_sample),
+           "same_ids_heap_order": float((ex.ids == ref_ids).all(1).mean()),
+           "same_dists_bitwise": float((ex.dists.view(np.uint32) == ref_d.view(np.uint32)).all(1).mean()),
+           "same_counters": float((ex.qstats[:, :5] == ref_qs[:, :5]).all(1).mean()),
+           "exact_rows": "f32", "ef": ef, "memory_nodes": shards, "dumps_s": t1 - t0, "oracle_s": time.time() - t1}
+    log(f"oracle sample: {json.dumps(out)}")
+    return out
 
 
 def run_measure(torch, idx, name, a, q, gt, batch, slots, ef, kind, n, dim, metric, M, efc, placement, alpha, nq,
@@ -188,7 +227,9 @@ def main():
     p.add_argument("--cmp-kind", default="sift_like")
     p.add_argument("--cmp-dim", type=int, default=128)
     p.add_argument("--cmp-metric", type=int, default=0)
-    p.add_argument("--cmp-oracle", type=int, default=1)
+    p.add_argument("--cmp-oracle", type=int, default=1,
+                   help="cmp: the oracle on 512 queries of the GPU-built dump; cfg*: on --cmp-oracle-n queries")
+    p.add_argument("--cmp-oracle-n", type=int, default=64)
     p.add_argument("--cmp-fracs", default="0.02", help="cmp: GPU builds at these batch fractions")
     p.add_argument("--out", default=str(ROOT / "gpurun_out" / "scale_lines.jsonl"))
     a = p.parse_args()
