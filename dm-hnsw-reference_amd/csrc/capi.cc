@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -537,6 +538,23 @@ int64_t env_int(const char* name, int64_t dflt) {
 // to the light pass instead, the round-2 behaviour)
 bool spill_enabled() { return env_int("SHINE_DEBUG_NO_SPILL", 0) == 0; }
 
+// A spilled table goes to a hash table in its spill slot (kernels_impl.h SpillSet) where the id-space bitmap would
+// outgrow an XCD's L2 (> 32M ids); SHINE_SPILL_HASH = 0 / 1 forces the bitmap / the hash table (tests, A/B).
+constexpr uint32_t kSpillHashMax = 65536;  // entries (256 KB): 8 x the largest table it takes over, load <= 1/2
+bool spill_hashed(const shine_index* h) {
+  const int64_t f = env_int("SHINE_SPILL_HASH", -1);
+  return f == 1 || (f < 0 && 4ull * h->words_per_slot > kXcdL2Bytes);
+}
+// Hash entries for a main-pass table of vis_cap entries: 8 x, 16,384 to 65,536 (a spilled query hands itself on at
+// half of it, beyond any query seen at these sizes).
+uint32_t spill_hash_entries(uint32_t vis_cap) {
+  return std::min<uint32_t>(kSpillHashMax, std::max<uint32_t>(16384, pow2_at_least(8 * std::max<uint32_t>(vis_cap, 1))));
+}
+// Words per spill / fallback slot: the id-space bitmap, or at least the largest hash table.
+uint64_t slot_words(const shine_index* h) {
+  return spill_hashed(h) ? std::max<uint64_t>(h->words_per_slot, kSpillHashMax) : h->words_per_slot;
+}
+
 // Fast mode: the sorted list lives in VGPRs, LDS holds only the visited table.  The table holds between pow2(40·ef)
 // and pow2(48·ef) entries (a query visits ~5-20·ef nodes; one that fills 7/8 of it goes to the light pass).  The
 // shape aims at the wavefronts of two batches being resident together (the next batch in flight runs beside this
@@ -805,12 +823,14 @@ Scratch& scratch_for(Replica& R, hipStream_t s) {
 }
 
 int ensure_bitmaps(shine_index* h, Scratch& S, hipStream_t s, uint32_t slots) {
-  if (slots <= S.slots) return 0;
+  const uint64_t stride = slot_words(h);
+  if (slots <= S.slots && stride == S.stride) return 0;
   HIP_TRY(hipStreamSynchronize(s));  // earlier calls on this stream may still read the old bitmaps
   S.visited.release();
   S.vlog.release();
   S.slots = 0;
-  if (int rc = S.visited.grow(static_cast<size_t>(slots) * h->words_per_slot)) return rc;
+  S.stride = stride;
+  if (int rc = S.visited.grow(static_cast<size_t>(slots) * stride)) return rc;
   if (int rc = S.vlog.grow(static_cast<size_t>(slots) * kLogCap)) return rc;
   HIP_TRY(hipMemsetAsync(S.visited.p, 0, S.visited.n * sizeof(uint32_t), s));
   HIP_TRY(hipStreamSynchronize(s));
@@ -879,7 +899,8 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
       const uint32_t mean_t = learned_mean_table(S), max_t = learned_max_table(S, ef, R.lds_per_cu);
       const uint64_t need = std::min<uint64_t>(16, (nq + R.cus - 1) / R.cus);
       const bool max_fits = max_t && R.lds_per_cu / search_fast_lds_bytes(max_t, ef, 4) >= need;
-      const bool beyond_l2 = 4ull * h->words_per_slot > kXcdL2Bytes;
+      // (with the hash-table spill a spilled query stays in L2 at any id space, and the mean-sized table wins there)
+      const bool beyond_l2 = 4ull * h->words_per_slot > kXcdL2Bytes && !spill_hashed(h);
       const int64_t force = env_int("SHINE_FAST_TABLE_MAX", -1);
       learned_fast = (force == 1 || (force < 0 && max_fits && beyond_l2)) ? max_t : mean_t;
       learned_mean = mean_t;
@@ -906,9 +927,10 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
       S.last_learned = (learned_fast != 0 && sh.vis_cap == learned_fast) ||
                        (pass != PASS_FAST && learned != 0 && sh.vis_cap == learned);
       if (env_int("SHINE_DEBUG_SHAPE", 0))  // diagnostics: the main pass's shape and what it was learned from
-        std::fprintf(stderr, "shape: pass %d nq %u ef %u table %u vis16 %u grid %u learned %u vmax %u handed %u floor %u\n",
+        std::fprintf(stderr, "shape: pass %d nq %u ef %u table %u vis16 %u grid %u learned %u vmax %u handed %u floor %u "
+                     "spill_hash %u\n",
                      pass, nq, ef, sh.vis_cap, sh.vis16, sh.grid, learned, S.seen.p[3] ? S.seen.p[4] : 0u, handed,
-                     S.table_floor);
+                     S.table_floor, spill_hashed(h) ? spill_hash_entries(sh.vis_cap) : 0u);
     }
     SearchArgs a{};
     a.g = dev_graph(h, R);
@@ -948,7 +970,12 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     a.out_dists = d_dists;
     a.qstats = d_qs;
     a.visited = S.visited.p;
-    a.words_per_slot = h->words_per_slot;
+    a.words_per_slot = S.stride;
+    a.spill_hash = spill_hashed(h) ? spill_hash_entries(sh.vis_cap) : 0u;
+    if (a.spill_hash) {  // test hook: a smaller hash table (a power of two, >= 256 entries)
+      const int64_t hs = env_int("SHINE_DEBUG_SPILL_HASH", 0);
+      if (hs >= 256 && hs <= kSpillHashMax && (hs & (hs - 1)) == 0) a.spill_hash = static_cast<uint32_t>(hs);
+    }
     a.vlog = S.vlog.p;
     a.log_cap = kLogCap;
     a.counter = S.counter.p + i;
@@ -1471,10 +1498,12 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     // Device-API searches on other streams of a slot may still be reading the arena: the updates below rewrite its
     // rows and cslot, so every stream of the slot drains first (as shine_cache_update does).  Those calls' logged
     // misses are applied here too.
+    const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t r = 0; r < G; ++r) {
       HIP_TRY(hipSetDevice(h->reps[r].device));
       HIP_TRY(hipDeviceSynchronize());
     }
+    const auto t1 = std::chrono::steady_clock::now();
     for (uint32_t r = 0; r < G; ++r)
       th.emplace_back([&, r] {
         per[r] = shine_stats{};
@@ -1482,6 +1511,14 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
         if (rcs[r]) errs[r] = last_error();  // the message is thread-local
       });
     for (auto& t : th) t.join();
+    if (env_int("SHINE_DEBUG_CACHE_TIMING", 0)) {  // diagnostics: where the time between calls goes
+      const auto t2 = std::chrono::steady_clock::now();
+      auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+      uint64_t adm = 0;
+      for (const shine_stats& p : per) adm += p.cache_admitted;
+      std::fprintf(stderr, "cache timing: kernel %.3f ms, device sync %.3f ms, replay+update %.3f ms, admitted %llu\n",
+                   kernel_ms, ms(t0, t1), ms(t1, t2), static_cast<unsigned long long>(adm));
+    }
     for (uint32_t r = 0; r < G; ++r)
       if (rcs[r]) return set_error(rcs[r], errs[r]);
     for (const shine_stats& p : per) {

@@ -132,6 +132,7 @@ struct Scratch {
   uint32_t* seen_dev = nullptr;  // its device address
   bool counters_zero = false;    // the last call's last pass zeroed the counter words (finish_call)
   uint32_t slots = 0;
+  uint64_t stride = 0;           // words per slot of `visited` (capi.cc slot_words)
   uint32_t last_table = 0;       // visited-table entries of the last call's main pass, and whether they were learned
   bool last_learned = false;
   uint32_t table_floor = 0;      // a learned table that overflowed is never learned again below twice its size
@@ -145,6 +146,7 @@ struct Scratch {
     seen_dev = nullptr;
     counters_zero = false;
     slots = 0;
+    stride = 0;
   }
 };
 

@@ -95,6 +95,9 @@ struct SearchArgs {
   uint32_t spill_slots;
   uint32_t* spill_count;     // main pass (nullable): the call's counter word 9, queries that spilled (copied to
                              // host_counts[7]): a learned table that spills too often is grown (capi.cc)
+  uint32_t spill_hash;       // 0: a spilled table goes to its slot as a bitmap over the id space; else to a hash table
+                             // of spill_hash entries (a power of two <= words_per_slot) in the slot (kernels_impl.h
+                             // SpillSet), where the id-space bitmap would outgrow an XCD's L2
 };
 
 struct DistArgs {

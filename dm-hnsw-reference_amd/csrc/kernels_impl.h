@@ -911,18 +911,12 @@ struct VisitedLds<0> {
     for (u32 i = lane; i < A.vis_cap / 4; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
   }
   __device__ __forceinline__ void insert_first(u32 x) { t[home(x)] = x; }  // the table is empty
-  // every id of the table into the HBM bitmap (the table's entries are the ids themselves)
-  __device__ __forceinline__ void spill(u32* __restrict__ bits, const SearchArgs& A, int lane) const {
+  // f(x) for every id of the table (the entries are the ids themselves): the spill into HBM, and its release
+  template <class F>
+  __device__ __forceinline__ void for_each(F f, const SearchArgs& A, int lane) const {
     for (u32 i = lane; i < cap; i += 64) {
       const u32 x = t[i];
-      if (x < A.g.N) atomicOr(&bits[x >> 5], 1u << (x & 31));
-    }
-  }
-  // the table's ids back out of the bitmap (whole words to zero: the bitmap goes back all zero)
-  __device__ __forceinline__ void unspill(u32* __restrict__ bits, const SearchArgs& A, int lane) const {
-    for (u32 i = lane; i < cap; i += 64) {
-      const u32 x = t[i];
-      if (x < A.g.N) bits[x >> 5] = 0u;
+      if (x < A.g.N) f(x);
     }
   }
   __device__ __forceinline__ bool at_home(u32 x) const { return t[home(x)] == x; }
@@ -972,9 +966,10 @@ struct VisitedLds<1> {
     for (u32 i = lane; i < A.vis_cap / 8; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
   }
   __device__ __forceinline__ u32 image(u32 x) const { return (x * mul) & bmask; }
-  // every id of the table into the HBM bitmap: entry (bucket b, remainder, distance d) names the id whose image is
+  // f(x) for every id of the table: entry (bucket b, remainder, distance d) names the id whose image is
   // ((b - d) << rbits) | remainder, and the inverse multiply maps the image back
-  __device__ __forceinline__ void spill(u32* __restrict__ bits, const SearchArgs& A, int lane) const {
+  template <class F>
+  __device__ __forceinline__ void for_each(F f, const SearchArgs& A, int lane) const {
     const u32 nw = A.vis_cap >> 1;  // two entries per word
     for (u32 i = lane; i < nw; i += 64) {
       const u32 w = t[i], b = i >> 2;
@@ -984,21 +979,7 @@ struct VisitedLds<1> {
         if (v == 0xFFFFu) continue;
         const u32 home = (b - (v & ((1u << dbits) - 1u))) & bmask_b;
         const u32 x = (((home << rbits) | (v >> dbits)) * A.vis_mul_inv) & bmask;
-        if (x < A.g.N) atomicOr(&bits[x >> 5], 1u << (x & 31));
-      }
-    }
-  }
-  __device__ __forceinline__ void unspill(u32* __restrict__ bits, const SearchArgs& A, int lane) const {
-    const u32 nw = A.vis_cap >> 1;
-    for (u32 i = lane; i < nw; i += 64) {
-      const u32 w = t[i], b = i >> 2;
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const u32 v = half ? (w >> 16) : (w & 0xFFFFu);
-        if (v == 0xFFFFu) continue;
-        const u32 home = (b - (v & ((1u << dbits) - 1u))) & bmask_b;
-        const u32 x = (((home << rbits) | (v >> dbits)) * A.vis_mul_inv) & bmask;
-        if (x < A.g.N) bits[x >> 5] = 0u;
+        if (x < A.g.N) f(x);
       }
     }
   }
@@ -1124,7 +1105,8 @@ struct VisitedLds<2> {
     const u32 b1 = (v & 1u) ? (b ^ alt(rem)) & bmask_b : b;
     return (((b1 << rbits) | rem) * A.vis_mul_inv) & bmask;
   }
-  __device__ __forceinline__ void spill(u32* __restrict__ bits, const SearchArgs& A, int lane) const {
+  template <class F>
+  __device__ __forceinline__ void for_each(F f, const SearchArgs& A, int lane) const {
     const u32 nw = A.vis_cap >> 1;
     for (u32 i = lane; i < nw; i += 64) {
       const u32 w = t[i], b = i >> 2;
@@ -1133,20 +1115,7 @@ struct VisitedLds<2> {
         const u32 v = half ? (w >> 16) : (w & 0xFFFFu);
         if (v == 0xFFFFu) continue;
         const u32 x = decode(b, v, A);
-        if (x < A.g.N) atomicOr(&bits[x >> 5], 1u << (x & 31));
-      }
-    }
-  }
-  __device__ __forceinline__ void unspill(u32* __restrict__ bits, const SearchArgs& A, int lane) const {
-    const u32 nw = A.vis_cap >> 1;
-    for (u32 i = lane; i < nw; i += 64) {
-      const u32 w = t[i], b = i >> 2;
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const u32 v = half ? (w >> 16) : (w & 0xFFFFu);
-        if (v == 0xFFFFu) continue;
-        const u32 x = decode(b, v, A);
-        if (x < A.g.N) bits[x >> 5] = 0u;
+        if (x < A.g.N) f(x);
       }
     }
   }
@@ -1170,7 +1139,8 @@ struct VisitedLds<2> {
     const u32 e = rem << 1;
     // rem 0x7FFF never goes to b2 (its b2 entry would be the empty marker 0xFFFF, which any bucket with a free entry
     // "holds"): only b1 is looked at for it
-    if (VisitedLds<1>::has(w1, e) | (VisitedLds<1>::has(w2, e | 1u) & (rem != 0x7FFFu))) return Plan2{kPresent, 0u, 0u};
+    const bool in2 = rem != 0x7FFFu && VisitedLds<1>::has(w2, e | 1u);
+    if (VisitedLds<1>::has(w1, e) || in2) return Plan2{kPresent, 0u, 0u};
     // each bucket's first empty entry once: its position is the bucket's fill (entries fill in order)
     int j1, j2;
     u32 k1, k2, o1, o2;
@@ -1275,21 +1245,89 @@ __device__ __forceinline__ void spill_log(const SearchArgs& A, int sslot, u32& n
   n += static_cast<u32>(__popcll(m));
 }
 
-// Hand the spill bitmap back all zero, then drop its flag (every lane stores the same flag word: see the fast kernel).
+// The visited set of a query whose LDS table overflowed (in-place spill): slot `sslot` of the stream's spill storage
+// (SearchArgs::visited, words_per_slot words each, all zero between uses), used one of two ways.
+//   * a bitmap over the id space (spill_hash == 0): one atomicOr per visit.  Cheap while the bitmap stays in an XCD's
+//     L2 (1.25 MB at 10M ids); at 100M ids it is 12.5 MB, every visit of a spilled query missed to HBM, and the few
+//     queries that spilled (0.3 %) set their batches' times: 2.37 M against 3.41 M QPS with tables twice the size
+//     that never spill (profiles/r04/diag100m_tables_inflight.jsonl).
+//   * an open-addressing hash table of spill_hash entries (a power of two, load kept <= 1/2) in the slot's first words
+//     (spill_hash > 0): entry id + 1, 0 = empty (so the slot is all zero between uses, as the fallback passes' bitmaps
+//     must be), linear probing from the multiplicative hash's top bits, one compare-and-swap per probe.  128 KB at
+//     32,768 entries: it stays in L2 for the few queries that spill, whatever the id space.  The whole LDS table moves
+//     in at the spill and every later visit of the query goes there (a lookup walking the frozen LDS table first was
+//     40 % slower at cfg 3, profiles/r04/scale_cfg3_cfg5_10m_v3_hashspill_reverted.jsonl).
+struct SpillSet {
+  u32* p = nullptr;
+  u32 hmask = 0, hshift = 0;  // hash entries - 1 and 32 - log2(entries); hmask == 0: bitmap
+  __device__ __forceinline__ SpillSet() {}
+  __device__ __forceinline__ SpillSet(const SearchArgs& A, int sslot)
+      : p(A.visited + static_cast<u64>(sslot) * A.words_per_slot),
+        hmask(A.spill_hash ? A.spill_hash - 1u : 0u),
+        hshift(A.spill_hash ? static_cast<u32>(__clz(static_cast<int>(A.spill_hash))) + 1u : 0u) {}
+  __device__ __forceinline__ bool hashed() const { return hmask != 0u; }
+  // x recorded; true when it was not yet (ovf: a probe chain of 64, the query is handed on)
+  __device__ __forceinline__ bool test_and_set(u32 x, bool& ovf) const {
+    if (!hashed()) {
+      const u32 bit = 1u << (x & 31);
+      return (atomicOr(&p[x >> 5], bit) & bit) == 0u;
+    }
+    const u32 v = x + 1u;
+    u32 h = (x * 0x9E3779B1u) >> hshift;
+    bool fresh = false;
+    for (u32 n = 0;; ++n) {  // one loop exit (see the probe loops above)
+      const u32 old = atomicCAS(&p[h], 0u, v);
+      if (old == 0u) {
+        fresh = true;
+        break;
+      }
+      if (old == v) break;
+      if (n == 63) {
+        ovf = true;
+        break;
+      }
+      h = (h + 1u) & hmask;
+    }
+    return fresh;
+  }
+  __device__ __forceinline__ void set(u32 x) const {
+    bool ovf = false;
+    (void)test_and_set(x, ovf);
+  }
+};
+
+// Hand the spill slot back all zero, then drop its flag (every lane stores the same flag word: see the fast kernel).
+// Bitmap: the table's ids and the logged ones (spill_log); hash table: its words.
 template <class VTab>
 __device__ __forceinline__ void spill_release(const VTab& vt, const SearchArgs& A, int sslot, u32 n, int lane) {
-  u32* sb = A.visited + static_cast<u64>(sslot) * A.words_per_slot;
-  if (n > A.log_cap) {
+  const SpillSet ss(A, sslot);
+  u32* sb = ss.p;
+  if (ss.hashed()) {
+    uint4* s4 = reinterpret_cast<uint4*>(sb);
+    for (u32 i = lane; i <= (ss.hmask >> 2); i += 64) s4[i] = make_uint4(0u, 0u, 0u, 0u);
+  } else if (n > A.log_cap) {
     for (u64 w = lane; w < A.words_per_slot; w += 64) sb[w] = 0u;
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the log's stores, before its loads
-    vt.unspill(sb, A, lane);
+    vt.for_each([sb](u32 x) { sb[x >> 5] = 0u; }, A, lane);
     const u32* lg = A.vlog + static_cast<u64>(sslot) * A.log_cap;
     for (u32 i = lane; i < n; i += 64) sb[__hip_atomic_load(&lg[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 5] = 0u;
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __threadfence();
   __hip_atomic_store(&A.spill_flags[sslot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Move the LDS table into the spill slot (every id of it recorded there).
+template <class VTab>
+__device__ __forceinline__ void spill_table(const VTab& vt, const SpillSet& ss, const SearchArgs& A, int lane) {
+  if (ss.hashed()) {
+    const SpillSet s2 = ss;
+    vt.for_each([s2](u32 x) { s2.set(x); }, A, lane);
+  } else {
+    u32* sb = ss.p;
+    vt.for_each([sb](u32 x) { atomicOr(&sb[x >> 5], 1u << (x & 31)); }, A, lane);
+  }
 }
 
 template <int D, int METRIC, typename E, int VIS, int ACCT, int VT = 0, bool PROF = false>
@@ -1408,13 +1446,21 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
             // then answered in one LDS round trip and a fresh one swapped in two, where a blind swap assuming an
             // empty home costs an extra failed round trip once the table has filled
             fresh = vt.test_and_set(e, vovf, vt.probe(e));
-          } else {  // the HBM bitmap: the fallback passes', or this query's spilled table
-            u32* __restrict__ bm = VIS == 0 ? A.visited + static_cast<u64>(sslot) * A.words_per_slot : vis;
+          } else if (VIS == 0) {  // this query's spilled table: the HBM bitmap or hash table (SpillSet)
+            fresh = SpillSet(A, sslot).test_and_set(e, vovf);
+          } else {  // the fallback passes' HBM bitmap
             const u32 bit = 1u << (e & 31);
-            fresh = (atomicOr(&bm[e >> 5], bit) & bit) == 0;
+            fresh = (atomicOr(&vis[e >> 5], bit) & bit) == 0;
           }
         }
-        if (VIS == 0 && sslot >= 0) spill_log(A, sslot, slog, fresh, e, lane);
+        if (VIS == 0 && sslot >= 0) {
+          if (!SpillSet(A, sslot).hashed()) {
+            spill_log(A, sslot, slog, fresh, e, lane);
+          } else if (__ballot(vovf) || nvis + __popcll(__ballot(fresh)) > A.spill_hash / 2) {
+            status = ST_OVERFLOW;  // the hash table is half full: the query is handed on to the light pass
+            break;
+          }
+        }
         if constexpr (VIS == 0) {
           // In-place spill (as the fast kernel): the table is too full, or an id landed too far from its home
           // bucket — the table moves to an HBM bitmap and the query goes on there instead of being handed to the
@@ -1425,15 +1471,17 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
               status = ST_OVERFLOW;
               break;
             }
-            u32* sb = A.visited + static_cast<u64>(sslot) * A.words_per_slot;
+            const SpillSet ss(A, sslot);
             wave_sync();
-            vt.spill(sb, A, lane);
+            spill_table(vt, ss, A, lane);
             EVENT(3)
-            if (vovf) {
-              const u32 bit = 1u << (e & 31);
-              fresh = (atomicOr(&sb[e >> 5], bit) & bit) == 0u;
+            bool hovf = false;
+            if (vovf) fresh = ss.test_and_set(e, hovf);
+            if (!ss.hashed()) spill_log(A, sslot, slog, vovf, e, lane);
+            if (__ballot(hovf)) {
+              status = ST_OVERFLOW;
+              break;
             }
-            spill_log(A, sslot, slog, vovf, e, lane);
           }
         }
         const u64 fm = __ballot(fresh);
@@ -1764,13 +1812,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kFastWaves<D
       // ef = 128, profiles/r02/lib_probe_deferred_insert.jsonl)
       bool fresh = false, vovf = false;
       u32 pw = INV, pexp = 0, pold = 0;
-      if (sslot >= 0) {  // spilled: the HBM bitmap
-        if (cand) {
-          u32* sb = A.visited + static_cast<u64>(sslot) * A.words_per_slot;
-          const u32 bit = 1u << (e & 31);
-          fresh = (atomicOr(&sb[e >> 5], bit) & bit) == 0u;
+      if (sslot >= 0) {  // spilled: the HBM bitmap or hash table (SpillSet)
+        const SpillSet ss(A, sslot);
+        bool hovf = false;
+        if (cand) fresh = ss.test_and_set(e, hovf);
+        if (!ss.hashed()) {
+          spill_log(A, sslot, slog, fresh, e, lane);
+        } else if (__ballot(hovf) || nvis + __popcll(__ballot(fresh)) > A.spill_hash / 2) {
+          status = ST_OVERFLOW;  // the hash table is half full: the query is handed on to the light pass
+          break;
         }
-        spill_log(A, sslot, slog, fresh, e, lane);
       } else if constexpr (VT >= 1) {
         if (cand) {
           const int r = ehint_known ? vis.begin(e, ehint, pw, pexp, pold) : 2;
@@ -1789,17 +1840,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kFastWaves<D
           status = ST_OVERFLOW;
           break;
         }
-        u32* sb = A.visited + static_cast<u64>(sslot) * A.words_per_slot;
+        const SpillSet ss(A, sslot);
         wave_sync();
-        vis.spill(sb, A, lane);
+        spill_table(vis, ss, A, lane);
         EVENT(3)
-        if (lost) atomicOr(&sb[e >> 5], 1u << (e & 31));
+        if (lost) ss.set(e);
         pw = INV;
-        spill_log(A, sslot, slog, lost || vovf, e, lane);
+        if (!ss.hashed()) spill_log(A, sslot, slog, lost || vovf, e, lane);
+        bool hovf = false;
         if (vovf) {
-          const u32 bit = 1u << (e & 31);
-          fresh = (atomicOr(&sb[e >> 5], bit) & bit) == 0u;
+          fresh = ss.test_and_set(e, hovf);
           vovf = false;
+        }
+        if (__ballot(hovf)) {
+          status = ST_OVERFLOW;
+          break;
         }
       }
       const u64 fm = __ballot(fresh);
@@ -1836,12 +1891,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kFastWaves<D
             status = ST_OVERFLOW;
             break;
           }
-          u32* sb = A.visited + static_cast<u64>(sslot) * A.words_per_slot;
+          const SpillSet ss(A, sslot);
           wave_sync();
-          vis.spill(sb, A, lane);
+          spill_table(vis, ss, A, lane);
           EVENT(3)
-          if (vovf) atomicOr(&sb[e >> 5], 1u << (e & 31));
-          spill_log(A, sslot, slog, vovf, e, lane);
+          if (vovf) ss.set(e);
+          if (!ss.hashed()) spill_log(A, sslot, slog, vovf, e, lane);
         }
       }
 

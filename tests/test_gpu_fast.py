@@ -429,3 +429,64 @@ def test_host_api_splits_large_calls_into_chunks_in_flight(mode, gpu_available, 
     if mode == L.MODE_EXACT:
         ref_ids, ref_d, _ = O.OracleIndex(dumps, 96, 16, 0).knn(q[:300], 10, 64, threads=8)
         np.testing.assert_array_equal(want.ids[:300], ref_ids)
+
+
+@pytest.mark.parametrize("vis16,vis_bits", [("0", "0"), ("1", "0"), ("2", "20")], ids=["u32", "u16", "two_choice"])
+@pytest.mark.parametrize("mode", [L.MODE_FAST, L.MODE_EXACT])
+def test_hash_spill_matches_oracle(mode, vis16, vis_bits, gpu_available, monkeypatch, capfd):
+    """The hash-table spill target (kernels_impl.h SpillSet, SHINE_SPILL_HASH=1 forces it at any id space): 256-entry
+    LDS tables overflow in every query, each table moves into a 16,384-entry HBM hash table and the search goes on
+    there.  Every width of LDS table (u32, u16 quotient, two-choice at 20-bit ids) decodes into it; exact mode equals
+    the oracle bit for bit (ids in heap order, distances, counters), fast mode on every tie-free query; 48 queries,
+    fewer than the 64 spill slots, so none is handed on."""
+    base = D.deep_like(6000, seed=341, d=96)
+    q = D.deep_like(48, seed=342, d=96)
+    dumps, _, _ = O.build(base, 16, 100, 0, 1, seed=6)
+    ref = O.OracleIndex(dumps, 96, 16, 0).knn(q, 10, 128, threads=8)
+    monkeypatch.setenv("SHINE_SPILL_HASH", "1")
+    monkeypatch.setenv("SHINE_DEBUG_VISCAP", "256")
+    monkeypatch.setenv("SHINE_DEBUG_VIS16", vis16)
+    if vis_bits != "0":
+        monkeypatch.setenv("SHINE_DEBUG_VIS_BITS", vis_bits)
+        monkeypatch.setenv("SHINE_EXACT_TWO_CHOICE", "1")
+    monkeypatch.setenv("SHINE_DEBUG_SHAPE", "1")
+    with shine_amd.Index.from_buffers(dumps, 96, 16, 0, gpus=[0]) as idx:
+        idx.set_search_mode(mode)
+        capfd.readouterr()
+        runs = [idx.knn(q, 10, 128) for _ in range(2)]  # the second call: every spill slot was handed back zeroed
+        err = capfd.readouterr().err
+    assert f" table 256 vis16 {vis16} " in err, err
+    for r in runs:
+        assert r.stats["overflow_retries"] == 0
+        if mode == L.MODE_EXACT:
+            np.testing.assert_array_equal(r.ids, ref[0])
+            np.testing.assert_array_equal(r.dists.view(np.uint32), ref[1].view(np.uint32))
+            np.testing.assert_array_equal(r.qstats[:, :5], ref[2][:, :5])
+        else:
+            _check_tie_free_exact(r, ref, 0.95)
+
+
+def test_hash_spill_overflow_hands_queries_on(gpu_available, monkeypatch):
+    """A query whose spilled visited set passes half its hash table is handed on to the light pass (HBM bitmap) and
+    re-run there from scratch: 256-entry LDS tables and a 1,024-entry hash table (SHINE_DEBUG_SPILL_HASH) at ef = 128,
+    where queries visit ~2K nodes, so every query spills and then overflows.  Results equal the oracle bit for bit."""
+    base = D.deep_like(6000, seed=351, d=96)
+    q = D.deep_like(48, seed=352, d=96)
+    dumps, _, _ = O.build(base, 16, 100, 0, 1, seed=6)
+    ref = O.OracleIndex(dumps, 96, 16, 0).knn(q, 10, 128, threads=8)
+    monkeypatch.setenv("SHINE_SPILL_HASH", "1")
+    monkeypatch.setenv("SHINE_DEBUG_SPILL_HASH", "1024")
+    monkeypatch.setenv("SHINE_DEBUG_VISCAP", "256")
+    monkeypatch.setenv("SHINE_DEBUG_VIS16", "0")
+    for mode in (L.MODE_EXACT, L.MODE_FAST):
+        with shine_amd.Index.from_buffers(dumps, 96, 16, 0, gpus=[0]) as idx:
+            idx.set_search_mode(mode)
+            r = idx.knn(q, 10, 128)
+        assert r.stats["overflow_retries"] >= q.shape[0] // 2
+        assert (r.qstats[:, L.QS_STATUS] == 0).all()
+        if mode == L.MODE_EXACT:
+            np.testing.assert_array_equal(r.ids, ref[0])
+            np.testing.assert_array_equal(r.dists.view(np.uint32), ref[1].view(np.uint32))
+            np.testing.assert_array_equal(r.qstats[:, :5], ref[2][:, :5])
+        else:  # the light pass runs the exact heap kernel and writes ascending order
+            _check_tie_free_exact(r, ref, 0.95)

@@ -34,6 +34,9 @@ def main():
     p.add_argument("--envs", default=";SHINE_DEBUG_NO_SPILL=1;SHINE_DEBUG_VISCAP=8192")
     a = p.parse_args()
     import torch
+    torch.cuda.set_device(0)
+    from config_lines import reserve_streams
+    all_streams = reserve_streams(torch, 8)  # first streams of the process: distinct hardware queues
     import shine_amd
     from shine_amd import datasets as D
     L = shine_amd._lib
@@ -52,7 +55,6 @@ def main():
     B, nb = 1024, 8
     ids = torch.empty((nb, B, 10), dtype=torch.int32, device="cuda")
     qs = torch.zeros((nb, B, L.QS_WORDS), dtype=torch.int32, device="cuda")
-    all_streams = [torch.cuda.Stream() for _ in range(8)]
     streams = all_streams[:4]
 
     def run(steps, ef):

@@ -79,8 +79,15 @@ def run(name, a):
     gb, st = build_gpu(torch, shine_amd, base_t, M, efc, metric, a, name)
     del base_t
     torch.cuda.empty_cache()
-    orc = oracle_sample(shine_amd, gb, q, a.k, int((a.ef or str(ef)).split(",")[0]), dim, M, metric,
-                        8 if name == "cfg4" else 1, a.cmp_oracle_n) if a.cmp_oracle else None
+    L = shine_amd._lib
+    ef0 = int((a.ef or str(ef)).split(",")[0])
+    # the oracle's knn on the GPU-built dump (a checker sample, before the replica takes the build's arrays)
+    orc = oracle_ref(shine_amd, gb, q, a.k, ef0, dim, M, metric, 8 if name == "cfg4" else 1,
+                     a.cmp_oracle_n) if a.cmp_oracle else None
+    if orc is not None and elem != L.ELEM_F32:  # exact mode on f32 rows of the same graph (the oracle's element type)
+        with gb.open_ex(1, elem=L.ELEM_F32, gpus=[0]) as ix:
+            ix.set_search_mode(L.MODE_EXACT)
+            orc["exact"] = ix.knn(orc["q"], a.k, ef0)
     lines = []
     # slots > 1: the same graph as `slots` memory-node dumps under SHINE_PLACE_SHARDED over GPU slots that repeat this
     # box's device (the 8-slot emulation of configs[3]/[4]); every slot answers 1/slots of each batch.  The replica
@@ -90,49 +97,63 @@ def run(name, a):
             idx, placement = gb.open(elem), "replica"
         else:
             idx, placement = gb.open_ex(slots, elem=elem, gpus=[0] * slots, placement="sharded"), "sharded"
-        for rep in range(a.repeat):  # --repeat: the same measurement again on the same handle (warm-state check)
-            for line in run_measure(torch, idx, name, a, q, gt, batch, slots, ef, kind, n, dim, metric, M, efc,
-                                    placement, alpha, nq, elem, st):
-                line["repeat"] = rep
-                if orc is not None:
-                    line["oracle"] = orc
-                    line["oracle_equals_exact_on_gpu_dump"] = orc["oracle_equals_exact_on_gpu_dump"]
-                lines.append(line)
+        for env in a.envs.split(";"):  # --envs: the same measurement under library tuning hooks (A/B on one build)
+            kv = [x.partition("=") for x in env.split(",") if x]
+            for k_, _, v_ in kv:
+                os.environ[k_] = v_
+            for rep in range(a.repeat):  # --repeat: the same measurement again on the same handle (warm-state check)
+                for line in run_measure(torch, idx, name, a, q, gt, batch, slots, ef, kind, n, dim, metric, M, efc,
+                                        placement, alpha, nq, elem, st):
+                    line["repeat"] = rep
+                    line["env"] = env
+                    lines.append(line)
+            for k_, _, _ in kv:
+                del os.environ[k_]
+        if orc is not None and slots == 1 and "exact" not in orc:  # f32 rows: the measured replica itself
+            idx.set_search_mode(L.MODE_EXACT)
+            orc["exact"] = idx.knn(orc["q"], a.k, ef0)
         idx.close()
     gb.close()
+    if orc is not None:
+        res = oracle_compare(orc)
+        for line in lines:
+            line["oracle"] = res
+            line["oracle_equals_exact_on_gpu_dump"] = res["oracle_equals_exact_on_gpu_dump"]
     return lines
 
 
-def oracle_sample(shine_amd, gb, q, k, ef, dim, M, metric, shards, n_sample):
-    """The oracle's knn (checker; hnsw.hh:253-307) on the GPU-built index's dump images against exact mode on f32
-    rows of the same graph (the oracle's element type; fp16 workloads are measured on fp16 rows, this check runs on
-    f32 rows of the same dump), n_sample queries spread over the measured set: ids in heap order, distances bitwise,
-    counters."""
+def oracle_ref(shine_amd, gb, q, k, ef, dim, M, metric, shards, n_sample):
+    """The oracle's knn (the checker; hnsw.hh:253-307) on the GPU-built index's dump images, n_sample queries spread
+    over the measured set.  Exact mode on f32 rows of the same graph is compared with it (oracle_compare): ids in heap
+    order, distances bitwise, counters."""
     import oracle as O
-    L = shine_amd._lib
     qn = q.cpu().numpy()
     sel = np.linspace(0, qn.shape[0] - 1, n_sample).astype(np.int64)
     qs = np.ascontiguousarray(qn[sel])
     t0 = time.time()
-    with gb.open_ex(1, elem=L.ELEM_F32, gpus=[0]) as ix:
-        ix.set_search_mode(L.MODE_EXACT)
-        ex = ix.knn(qs, k, ef)
     with Heartbeat(f"oracle sample: dump images of {shards} memory nodes"):
         dumps = gb.dumps(shards, copy=False)
     t1 = time.time()
     with Heartbeat(f"oracle sample: {n_sample} queries"):
         I = O.OracleIndex(dumps, dim, M, metric)
-        ref_ids, ref_d, ref_qs = I.knn(qs, k, ef, threads=host_threads())
+        ref = I.knn(qs, k, ef, threads=host_threads())
         I.close()
     del dumps
+    return {"q": qs, "ref": ref, "ef": ef, "memory_nodes": shards, "dumps_s": t1 - t0, "oracle_s": time.time() - t1}
+
+
+def oracle_compare(orc):
+    ex = orc["exact"]
+    ref_ids, ref_d, ref_qs = orc["ref"]
     same_ids = np.array_equal(ex.ids, ref_ids)
     same_d = np.array_equal(ex.dists.view(np.uint32), ref_d.view(np.uint32))
     same_qs = np.array_equal(ex.qstats[:, :5], ref_qs[:, :5])
-    out = {"oracle_equals_exact_on_gpu_dump": bool(same_ids and same_d and same_qs), "queries": int(n_sample),
+    out = {"oracle_equals_exact_on_gpu_dump": bool(same_ids and same_d and same_qs), "queries": int(orc["q"].shape[0]),
            "same_ids_heap_order": float((ex.ids == ref_ids).all(1).mean()),
            "same_dists_bitwise": float((ex.dists.view(np.uint32) == ref_d.view(np.uint32)).all(1).mean()),
            "same_counters": float((ex.qstats[:, :5] == ref_qs[:, :5]).all(1).mean()),
-           "exact_rows": "f32", "ef": ef, "memory_nodes": shards, "dumps_s": t1 - t0, "oracle_s": time.time() - t1}
+           "exact_rows": "f32", "ef": orc["ef"], "memory_nodes": orc["memory_nodes"], "dumps_s": orc["dumps_s"],
+           "oracle_s": orc["oracle_s"]}
     log(f"oracle sample: {json.dumps(out)}")
     return out
 
@@ -220,6 +241,8 @@ def main():
     p.add_argument("--modes", default="fast,exact")
     p.add_argument("--inflight", type=int, default=4)
     p.add_argument("--repeat", type=int, default=1)
+    p.add_argument("--envs", default="", help="';'-separated variants of comma-separated KEY=VALUE library hooks, "
+                                              "measured one after the other on the same handle ('' = defaults)")
     p.add_argument("--slots", default="1", help="GPU slots per layout, e.g. 1,8: the same graph as a replica and "
                                                 "as 8 sharded memory-node dumps on this device")
     p.add_argument("--batch-fraction", type=float, default=0.0)

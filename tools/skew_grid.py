@@ -94,7 +94,7 @@ def main():
                 else:
                     idx.set_cache_policy(L.CACHE_DYNAMIC, ratio_percent=ratio, seed=1)
                 hits = reads = 0
-                res, t_meas, adm, qss, t_warm = [], 0.0, 0, [], 0.0
+                res, t_meas, adm, qss, t_warm, kms = [], 0.0, 0, [], 0.0, 0.0
                 for c in range(a.warm + a.calls):
                     qq = q[c * a.batch:(c + 1) * a.batch]
                     t1 = time.perf_counter()
@@ -109,6 +109,7 @@ def main():
                         reads += r.stats["node_reads"]
                         res.append(r.ids)
                         adm += r.stats["cache_admitted"]
+                        kms += r.stats["kernel_ms"]
                 got = np.concatenate(res)
                 want = gt_pool[src[a.warm * a.batch:per_cell]]
                 line = {"workload": "cfg5-skew-grid", "label": label, "alpha": alpha, "cache_ratio_percent": ratio,
@@ -119,6 +120,9 @@ def main():
                         "recall_at_10": D.recall_at_k(got, want, k),
                         "host_api_qps_including_cache_updates": a.calls * a.batch / t_meas,
                         "admitted_during_measured_calls": adm,
+                        # where a call's time goes: the searches' GPU span (events around every slot's pass chain, the
+                        # slowest slot) against the host call's wall time (staging, cache updates between calls)
+                        "kernel_ms_per_call": kms / a.calls, "wall_ms_per_call": t_meas * 1e3 / a.calls,
                         "config": {"n": a.n, "dim": dim, "metric": "IP", "elem": "f16", "M": M, "efc": efc,
                                    "ef": a.ef, "k": k, "batch": a.batch, "warmup_calls": a.warm,
                                    "measured_calls": a.calls, "pool": pool_n},
