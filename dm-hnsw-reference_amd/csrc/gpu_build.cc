@@ -38,6 +38,14 @@ int64_t env_int(const char* name, int64_t dflt) {
   return e ? std::atoll(e) : dflt;
 }
 
+// Host threads for host-side loops: OMP_NUM_THREADS when set (the GPU boxes grant 16 CPUs per GPU while the machine
+// shows 256), else the hardware's, at most 16.
+uint64_t host_threads() {
+  const int64_t omp = env_int("OMP_NUM_THREADS", 0);
+  if (omp > 0) return static_cast<uint64_t>(omp);
+  return std::max<uint64_t>(1, std::min<uint64_t>(16, std::thread::hardware_concurrency()));
+}
+
 template <class T>
 int upload_vec(DevBuf<T>& dst, const std::vector<T>& src, hipStream_t s) {
   if (int rc = dst.grow(std::max<size_t>(src.size(), 1))) return rc;
@@ -483,29 +491,37 @@ int shine_gpu_build_dumps(shine_gpu_build_t b, uint32_t n_shards) {
     std::memcpy(b->dumps[0].data() + 8, &ep_ptr, 8);  // rdma_reads.hh:74-99
     std::vector<uint32_t> perm(dim);
     for (uint32_t i = 0; i < dim; ++i) perm[i] = permuted_index(dim, i);
-    for (uint64_t i = 0; i < N; ++i) {
-      uint8_t* p = b->dumps[shard[i]].data() + off[i];
-      const uint64_t hdr = i == b->ep ? kEntryNode : 0;
-      const uint32_t id = static_cast<uint32_t>(i), lv = b->level[i];
-      std::memcpy(p, &hdr, 8);
-      std::memcpy(p + 8, &id, 4);
-      std::memcpy(p + 12, &lv, 4);
-      float* c = reinterpret_cast<float*>(p + 16);
-      const float* row = vec.data() + i * dim;
-      for (uint32_t k = 0; k < dim; ++k) std::memcpy(c + k, row + perm[k], 4);
-      for (uint32_t l = 0; l <= lv; ++l) {
-        uint8_t* lp = b->dumps[shard[i]].data() + L.list_offset(off[i], l);
-        const uint32_t* src = l == 0 ? &adj0[i * M0] : &adjU[(static_cast<uint64_t>(b->up_base[i]) + l - 1) * M];
-        const uint32_t cap = l == 0 ? M0 : M;
-        uint32_t cnt = 0;
-        while (cnt < cap && src[cnt] != kInvalid) {
-          const uint64_t rp = rptr(src[cnt]);
-          std::memcpy(lp + 4 + 8ull * cnt, &rp, 8);
-          ++cnt;
+    // records write disjoint byte ranges: the loop runs on the process's CPU share (16 per GPU on the pool's boxes;
+    // 100M records took a minute on one thread)
+    auto write_records = [&](uint64_t lo, uint64_t hi) {
+      for (uint64_t i = lo; i < hi; ++i) {
+        uint8_t* p = b->dumps[shard[i]].data() + off[i];
+        const uint64_t hdr = i == b->ep ? kEntryNode : 0;
+        const uint32_t id = static_cast<uint32_t>(i), lv = b->level[i];
+        std::memcpy(p, &hdr, 8);
+        std::memcpy(p + 8, &id, 4);
+        std::memcpy(p + 12, &lv, 4);
+        float* c = reinterpret_cast<float*>(p + 16);
+        const float* row = vec.data() + i * dim;
+        for (uint32_t k = 0; k < dim; ++k) std::memcpy(c + k, row + perm[k], 4);
+        for (uint32_t l = 0; l <= lv; ++l) {
+          uint8_t* lp = b->dumps[shard[i]].data() + L.list_offset(off[i], l);
+          const uint32_t* src = l == 0 ? &adj0[i * M0] : &adjU[(static_cast<uint64_t>(b->up_base[i]) + l - 1) * M];
+          const uint32_t cap = l == 0 ? M0 : M;
+          uint32_t cnt = 0;
+          while (cnt < cap && src[cnt] != kInvalid) {
+            const uint64_t rp = rptr(src[cnt]);
+            std::memcpy(lp + 4 + 8ull * cnt, &rp, 8);
+            ++cnt;
+          }
+          std::memcpy(lp, &cnt, 4);
         }
-        std::memcpy(lp, &cnt, 4);
       }
-    }
+    };
+    const uint64_t nt = std::max<uint64_t>(1, std::min<uint64_t>({host_threads(), 64, N / 65536 + 1}));
+    std::vector<std::thread> ts;
+    for (uint64_t t = 0; t < nt; ++t) ts.emplace_back(write_records, N * t / nt, N * (t + 1) / nt);
+    for (auto& t : ts) t.join();
   } catch (const std::bad_alloc&) {
     b->dumps.clear();
     return set_error(SHINE_ERR_NOMEM, "out of host memory for the dump images");

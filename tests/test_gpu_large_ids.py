@@ -2,7 +2,7 @@
 
 At more than 32M ids the spill target of an overflowing LDS visited table is the hash table in HBM (kernels_impl.h
 SpillSet; the id-space bitmap would be 8.5 MB, beyond an XCD's L2), chosen by the library itself (no override here).
-The records are 16-d (DEEP-shaped, GPU-generated) and the graph sparse (M = 8, efC = 32, the GPU batch builder) so the
+The records are 16-d (DEEP-shaped, GPU-generated) and the graph sparse (M = 8, efC = 24, the GPU batch builder) so the
 build and the dump images stay small; 64-entry LDS tables (SHINE_DEBUG_VISCAP) make every query spill.  Exact mode
 equals the oracle's knn on the dump bit for bit (ids in heap order, distances, counters); fast mode equals it on every
 tie-free query.
@@ -19,19 +19,34 @@ pytestmark = pytest.mark.gpu
 
 
 def test_spill_to_hash_at_27_bit_ids(gpu_available, monkeypatch, capfd):
+    import sys
+    import time
+
     import torch
-    n, dim, M, efc, ef, k = (1 << 26) + (1 << 20), 16, 8, 32, 64, 10
+    t0 = time.time()
+
+    def step(what):  # progress (visible with pytest -s): the phases' cost at this size
+        print(f"[large ids {time.time() - t0:6.1f}s] {what}", file=sys.stderr, flush=True)
+
+    n, dim, M, efc, ef, k = (1 << 26) + (1 << 16), 16, 8, 24, 64, 10
     base_t = D.generate_device("deep_like", n, seed=61, d=dim)
     q = D.generate_device("deep_like", 64, seed=62, d=dim).cpu().numpy()
+    step("rows generated")
     with shine_amd.GpuBuild(base_t.data_ptr(), M, efc, L.METRIC_L2, seed=7, n=n, dim=dim) as gb:
+        step("built")
         del base_t
         torch.cuda.empty_cache()
         assert gb.stats()["search_failures"] == 0
+        dumps = gb.dumps(1, copy=False)
+        step("dump images")
+        ref_ids, ref_d, ref_qs = O.OracleIndex(dumps, dim, M, L.METRIC_L2).knn(q, k, ef, threads=8)
+        del dumps
+        step("oracle")
         monkeypatch.setenv("SHINE_DEBUG_VISCAP", "64")
         monkeypatch.setenv("SHINE_DEBUG_VIS16", "0")
         monkeypatch.setenv("SHINE_DEBUG_SHAPE", "1")
         out = {}
-        with gb.open_ex(1, gpus=[0]) as idx:
+        with gb.open() as idx:  # the build's device arrays move into the handle
             assert idx.info()["id_space"] >= 1 << 26
             for mode in (L.MODE_EXACT, L.MODE_FAST):
                 idx.set_search_mode(mode)
@@ -39,9 +54,7 @@ def test_spill_to_hash_at_27_bit_ids(gpu_available, monkeypatch, capfd):
                 out[mode] = idx.knn(q, k, ef)
                 err = capfd.readouterr().err
                 assert " spill_hash 16384" in err, err  # the library chose the hash-table spill target
-        dumps = gb.dumps(1, copy=False)
-        ref_ids, ref_d, ref_qs = O.OracleIndex(dumps, dim, M, L.METRIC_L2).knn(q, k, ef, threads=8)
-        del dumps
+        step("searched")
     ex, fa = out[L.MODE_EXACT], out[L.MODE_FAST]
     assert ex.stats["overflow_retries"] == 0 and (ex.qstats[:, L.QS_STATUS] == 0).all()
     np.testing.assert_array_equal(ex.ids, ref_ids)
