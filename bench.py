@@ -2,7 +2,8 @@
 """bench.py — QPS at recall@10 >= 0.95 on a SIFT1M-shaped index (BASELINE.json configs[1]).
 
 Workload (one "step" = one batch): 1,024 queries through HNSW::knn (k=10, ef=128) against a 1M x 128-d L2 index
-built with M=16, efC=200 by the parallel restatement of HNSW::insert, in the reference's dump layout.  Data are
+built with M=16, efC=200 in-run by the GPU batch builder (--builder cpu: the parallel restatement of HNSW::insert),
+in the reference's dump layout.  Data are
 synthetic SIFT-shaped vectors (shine_amd.datasets.sift_like; no datasets can be fetched).  Queries and outputs
 are resident in HBM when the timed region starts; value = queries / wall time over exactly K steps.  Four batches
 are in flight per GPU (--inflight; step i is enqueued on HIP stream i % 4, each on a hardware queue of its own),
@@ -17,7 +18,8 @@ Also reported: `roofline` for the search kernel (algorithmic bytes of the K laun
 events vs 8 TB/s; `avg_launch_ms` is the per-launch event time, which rocprofv3's average duration matches),
 `value_host_to_host` (SURVEY §8d's query phase: queries and results in pinned host memory that the kernels read and
 write over PCIe, K steps, batches in flight as above; `value_host_to_host_copies` the same with copy-engine H2D / D2H;
-`value_host_api` is the synchronous C-ABI host call shine_knn_batch, one batch at a time)
+`value_host_api` is the drop-in C-ABI host call shine_knn_batch over the rank's whole query set per call, which the
+library runs as chunks in flight; `value_host_api_per_batch` the same call one batch at a time)
 and `cpu_baseline` (the CPU oracle — a C++ restatement of the reference's knn — built with the reference's flags on
 the host that runs it, on the host cores, bounded sample, rank 0 at N=1 only).
 
@@ -434,19 +436,30 @@ def main():
                "recall_at_10_host_to_host": D.recall_at_k(got, gt, a.k)}
         el, _ = timed(True)
         out["value_host_to_host_copies"] = a.steps * a.batch * world / el
-        # the synchronous host API (no batches in flight: it returns when the batch's results are on the host)
-        steps_api = max(1, min(a.steps, 20))
-        for i in range(2):
-            idx.knn(q[:a.batch], a.k, a.ef)
+        # the drop-in host API (shine_knn_batch: host arrays in, host arrays out, returns when the results are there),
+        # as the compute-node façade calls it: the rank's whole query set per call, which the library runs as 1,024-query
+        # chunks kept in flight on four streams (capi.cc knn_host; compute_node.cc:354-386 keeps T x C queries in
+        # flight), repeated to at least K batches' worth of queries
+        calls = max(1, -(-a.steps // a.nbatches))
+        api_ids = idx.knn(q, a.k, a.ef).ids
         if dist:
             dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(calls):
+            idx.knn(q, a.k, a.ef)
+        el = max_over_ranks(time.perf_counter() - t0, dist, "cuda")
+        out["value_host_api"] = calls * q.shape[0] * world / el
+        out["ms_per_step_host_api"] = el * 1e3 / (calls * a.nbatches)
+        out["host_api_calls"] = {"calls": calls, "queries_per_call": int(q.shape[0]),
+                                 "same_ids_as_device": bool(ref_ids is not None and (api_ids == ref_ids).all())}
+        # the same API one batch per call (nothing in flight between calls: the round-4 leg)
+        steps_api = max(1, min(a.steps, 20))
         t0 = time.perf_counter()
         for i in range(steps_api):
             b = i % a.nbatches
             idx.knn(q[b * a.batch:(b + 1) * a.batch], a.k, a.ef)
         el = max_over_ranks(time.perf_counter() - t0, dist, "cuda")
-        out["value_host_api"] = steps_api * a.batch * world / el
-        out["ms_per_step_host_api"] = el * 1e3 / steps_api
+        out["value_host_api_per_batch"] = steps_api * a.batch * world / el
         log(f"host legs: host-to-host zero copy {out['value_host_to_host'] / 1e6:.2f}M QPS (same ids as on HBM: "
             f"{out['host_to_host_same_ids_as_device']}), copy engine {out['value_host_to_host_copies'] / 1e6:.2f}M, "
             f"shine_knn_batch {out['value_host_api'] / 1e6:.2f}M QPS")
@@ -577,7 +590,12 @@ def main():
             "config": {"workload": "SIFT1M-shaped L2 knn, M=16 efC=200 ef=128 k=10", "n": a.n, "dim": a.dim,
                        "global_batch": a.batch * world, "batch_per_gpu": a.batch, "M": a.M, "efc": a.efc,
                        "ef": a.ef, "k": a.k, "shards": a.shards, "parallelism": f"replica{world}",
-                       "batches_in_flight": len(streams), "rows": rows},
+                       "batches_in_flight": len(streams), "rows": rows,
+                       # the GPU batch builder's graph is not the sequential insert's: at this size its recall@10 is
+                       # within 1e-4 of the CPU builder's (profiles/r04/cmp1m_gpu_vs_cpu_build.jsonl); --builder cpu
+                       # runs the restatement of HNSW::insert instead
+                       "builder": "gpu batch builder (shine_gpu_build)" if a.builder == "gpu" else
+                                  "CPU restatement of HNSW::insert (shine_build)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": (f"search_fast_kernel<128,L2,{rows},R=2,P=2>" if modes[0] == "fast"

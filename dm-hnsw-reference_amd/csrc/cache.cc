@@ -45,7 +45,7 @@ uint64_t cache_entries(uint64_t n, uint32_t M, uint32_t dim, double ratio_percen
   return cache_size / (16ull + 4ull * dim);  // compute_node.cc:40-54
 }
 
-RecordCache::RecordCache(uint32_t entries, uint64_t seed)
+RecordCache::RecordCache(uint32_t entries, uint64_t seed, uint32_t key_space)
     : C_(entries),
       B_(std::max<uint32_t>(1, entries)),
       CT_(std::max<uint32_t>(1, static_cast<uint32_t>(std::ceil(entries / static_cast<double>(kCoolingBucketEntries) *
@@ -56,7 +56,7 @@ RecordCache::RecordCache(uint32_t entries, uint64_t seed)
       key_of_(entries, kInv),
       dev_of_(entries, kInv),
       cooling_(entries, 0) {
-  slot_of_.reserve(entries);  // no rehash while the cache fills
+  slot_of_.assign(key_space, kInv);
 }
 
 bool RecordCache::size_ok(uint32_t entries) {
@@ -98,7 +98,7 @@ uint32_t RecordCache::evict() {  // cache.hh:232-311
     auto& b = buckets_[rand() % B_];
     if (b.empty()) continue;
     const uint32_t key = b[rand() % b.size()];
-    const uint32_t slot = slot_of_.at(key);
+    const uint32_t slot = slot_of_[key];
     uint32_t victim = kInv;
     bool has_victim = false;
     if (!cooling_[slot]) {  // hot -> cooling; the table may push its oldest key out
@@ -107,12 +107,11 @@ uint32_t RecordCache::evict() {  // cache.hh:232-311
       if (cool_on_) cool_on_->push_back(slot);
     }
     if (!has_victim) continue;
-    auto it = slot_of_.find(victim);
-    if (it == slot_of_.end() || !cooling_[it->second]) continue;  // rescued meanwhile: no eviction
-    const uint32_t vslot = it->second;
+    if (!contains(victim) || !cooling_[slot_of_[victim]]) continue;  // rescued meanwhile: no eviction
+    const uint32_t vslot = slot_of_[victim];
     auto& vb = buckets_[murmur64(victim) % B_];
     vb.erase(std::find(vb.begin(), vb.end(), victim));
-    slot_of_.erase(it);
+    slot_of_[victim] = kInv;
     cooling_[vslot] = 0;
     ++evicted;
     return vslot;
@@ -130,6 +129,43 @@ void RecordCache::insert(uint32_t key, uint32_t dev, std::vector<CacheUpdate>& u
   ++admitted;
 }
 
+// (query, key) order of the candidates: an LSD radix sort over the composite (query << 32 | key), 16-bit digits, only
+// the digits the largest composite needs (a comparison sort of the ~340K candidates one slot logs while its cache
+// fills took most of the time between calls)
+void sort_candidates(std::vector<CacheCandidate>& c) {
+  const size_t n = c.size();
+  if (n < 2) return;
+  std::vector<uint64_t> k(n), k2(n);
+  std::vector<uint32_t> ix(n), ix2(n);
+  uint64_t most = 0;
+  for (size_t i = 0; i < n; ++i) {
+    k[i] = (static_cast<uint64_t>(c[i].query) << 32) | c[i].key;
+    ix[i] = static_cast<uint32_t>(i);
+    most |= k[i];
+  }
+  std::vector<uint32_t> cnt(1u << 16);
+  for (int shift = 0; shift < 64 && (most >> shift) != 0; shift += 16) {
+    std::fill(cnt.begin(), cnt.end(), 0u);
+    for (size_t i = 0; i < n; ++i) ++cnt[(k[i] >> shift) & 0xFFFF];
+    uint32_t sum = 0;
+    for (uint32_t& x : cnt) {
+      const uint32_t t = x;
+      x = sum;
+      sum += t;
+    }
+    for (size_t i = 0; i < n; ++i) {
+      const uint32_t pos = cnt[(k[i] >> shift) & 0xFFFF]++;
+      k2[pos] = k[i];
+      ix2[pos] = ix[i];
+    }
+    k.swap(k2);
+    ix.swap(ix2);
+  }
+  std::vector<CacheCandidate> out(n);
+  for (size_t i = 0; i < n; ++i) out[i] = c[ix[i]];
+  c.swap(out);
+}
+
 void RecordCache::apply_call(std::vector<uint32_t> rescued_keys, std::vector<CacheCandidate> candidates,
                              std::vector<CacheUpdate>& updates, std::vector<uint32_t>& cool_on) {
   if (C_ == 0) return;
@@ -137,17 +173,14 @@ void RecordCache::apply_call(std::vector<uint32_t> rescued_keys, std::vector<Cac
   std::sort(rescued_keys.begin(), rescued_keys.end());
   rescued_keys.erase(std::unique(rescued_keys.begin(), rescued_keys.end()), rescued_keys.end());
   for (uint32_t key : rescued_keys) {  // cache.hh:128-132
-    auto it = slot_of_.find(key);
-    if (it != slot_of_.end() && cooling_[it->second] && ct_remove(key)) {
-      cooling_[it->second] = 0;
+    if (contains(key) && cooling_[slot_of_[key]] && ct_remove(key)) {
+      cooling_[slot_of_[key]] = 0;
       ++rescued;
     }
   }
-  std::stable_sort(candidates.begin(), candidates.end(), [](const CacheCandidate& a, const CacheCandidate& b) {
-    return a.query != b.query ? a.query < b.query : a.key < b.key;
-  });
+  sort_candidates(candidates);  // (query, key): a query offers a key once, so the order is total
   for (const CacheCandidate& c : candidates) {
-    if (contains(c.key)) continue;  // admitted by an earlier miss of this call (cache.hh:171-179)
+    if (c.key >= slot_of_.size() || contains(c.key)) continue;  // admitted by an earlier miss (cache.hh:171-179)
     if (c.always || !full() || c.coin) insert(c.key, c.dev_id, updates);
   }
   cool_on_ = nullptr;
@@ -155,8 +188,8 @@ void RecordCache::apply_call(std::vector<uint32_t> rescued_keys, std::vector<Cac
 
 std::vector<uint32_t> RecordCache::keys() const {
   std::vector<uint32_t> out;
-  out.reserve(slot_of_.size());
-  for (const auto& kv : slot_of_) out.push_back(kv.first);
+  for (uint32_t k : key_of_)
+    if (k != kInv && contains(k) && key_of_[slot_of_[k]] == k) out.push_back(k);
   std::sort(out.begin(), out.end());
   return out;
 }

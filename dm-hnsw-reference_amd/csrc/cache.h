@@ -11,7 +11,6 @@
 #pragma once
 
 #include <cstdint>
-#include <unordered_map>
 #include <vector>
 
 namespace shine {
@@ -31,14 +30,15 @@ struct CacheUpdate {
 class RecordCache {
  public:
   RecordCache() = default;
-  RecordCache(uint32_t entries, uint64_t seed);
+  // key_space: keys are below it (record uids; the key -> slot map is a flat array of that many entries)
+  RecordCache(uint32_t entries, uint64_t seed, uint32_t key_space);
 
   uint32_t capacity() const { return C_; }
   // evict() terminates only if the cache holds more entries than its cooling table (6 per bucket): otherwise every
   // entry can end up cooling with no bucket full, and the reference's loop never finds a victim (cache.hh:232-311)
   static bool size_ok(uint32_t entries);
   bool full() const { return next_idx_ >= C_; }  // cache.hh:205-216
-  bool contains(uint32_t key) const { return slot_of_.count(key) != 0; }
+  bool contains(uint32_t key) const { return key < slot_of_.size() && slot_of_[key] != 0xFFFFFFFFu; }
 
   // The policy over one call's logs.  rescued: keys of the cooling entries hit; candidates: the misses offered.
   // Appends the arena changes to `updates` and the slots whose cooling flag must be set to `cool_on`; slots whose
@@ -48,6 +48,7 @@ class RecordCache {
 
   std::vector<uint32_t> keys() const;
   uint32_t slot_key(uint32_t slot) const { return slot < key_of_.size() ? key_of_[slot] : 0xFFFFFFFFu; }
+  uint32_t slot_of(uint32_t key) const { return contains(key) ? slot_of_[key] : 0xFFFFFFFFu; }
   bool cooling(uint32_t slot) const { return slot < cooling_.size() && cooling_[slot] != 0; }
 
   uint64_t admitted = 0, evicted = 0, rescued = 0;
@@ -63,7 +64,7 @@ class RecordCache {
   uint64_t state_ = 0;
   std::vector<std::vector<uint32_t>> buckets_;  // keys per hash bucket, insertion order
   std::vector<std::vector<uint32_t>> ct_;       // cooling table, newest first
-  std::unordered_map<uint32_t, uint32_t> slot_of_;  // key -> arena slot
+  std::vector<uint32_t> slot_of_;                   // key -> arena slot (0xFFFFFFFF: not cached)
   std::vector<uint32_t> key_of_, dev_of_;           // slot -> key / device id
   std::vector<uint8_t> cooling_;                    // slot -> cooling
   std::vector<uint32_t>* cool_on_ = nullptr;

@@ -111,6 +111,8 @@ void release_state(IndexState* h) {
     R.hqs.release();
     for (hipStream_t s : R.hstreams) (void)hipStreamDestroy(s);
     for (hipEvent_t e : R.hjoin) (void)hipEventDestroy(e);
+    for (hipEvent_t e : R.hchunk) (void)hipEventDestroy(e);
+    R.hchunk.clear();
     if (R.hfork) (void)hipEventDestroy(R.hfork);
     R.hstreams.clear();
     R.hjoin.clear();
@@ -801,7 +803,9 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
   sh.cap = static_cast<uint32_t>(std::max<int64_t>(cap & ~1ll, 2));
   if (pass == PASS_LDS) sh.cap = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_DEBUG_CAP", sh.cap)));
   if (pass == PASS_LIGHT) sh.cap = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_DEBUG_LIGHT_CAP", sh.cap)));
-  sh.vis_limit = sh.vis_cap / 8 * 7;  // linear probing stays short; >= 64 free slots for one expansion
+  // linear probing stays short, and one expansion's fresh ids (up to M0) always find free slots: the u32 table's insert
+  // has no overflow exit (a 64-entry table, forced by the test hook at M0 = 16, filled up and probed forever)
+  sh.vis_limit = std::min<uint32_t>(sh.vis_cap / 8 * 7, sh.vis_cap > h->M0 ? sh.vis_cap - h->M0 : 0u);
   sh.grid = std::max<uint32_t>(1, std::min<uint32_t>(nq, cus * wpc));
   if (pass == PASS_LIGHT) {
     sh.grid = std::min(sh.grid, bitmap_slot_cap(h));
@@ -1227,6 +1231,7 @@ int shine_knn_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_qu
     if (int rc = S.qs.grow(static_cast<size_t>(nq) * kQsWords)) return rc;
     qs = S.qs.p;
   }
+  if (h->cache_policy == SHINE_CACHE_DYNAMIC) R.dev_api_dirty = true;  // it reads the arena and logs into its buffers
   return enqueue_search(h, R, d_queries, nq, k, ef, d_out_ids, d_out_dists, qs, s, false);
 }
 
@@ -1234,24 +1239,46 @@ int shine_knn_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_qu
 
 namespace {
 
-// The dynamic cache between calls (SHINE_CACHE_DYNAMIC): read slot R's logs of the last call(s), replay the
-// reference's policy on the host engine (cache.cc), and enqueue the arena updates on R's stream, ahead of its next call.
-int apply_dynamic(shine_index* h, Replica& R, shine_stats* agg) {
+// The dynamic cache between calls (SHINE_CACHE_DYNAMIC), in three steps per GPU slot:
+//   fetch_logs      after a call's searches are done: its miss and rescue logs to the host, the device counts zeroed;
+//   replay          host only (one thread per slot): the reference's policy (cache.cc) over the fetched logs, and the
+//                   arena updates it makes (rows to copy in, device ids to drop, cooling flags);
+//   enqueue_update  the updates uploaded and applied on the slot's stream, behind whatever is enqueued there.
+// Pipelined (default): a call's logs are replayed during the NEXT call's searches and its updates are applied behind
+// them, so the host's work hides behind the GPU's and a call's admissions serve from the call after next (the
+// reference admits while its queries run; here at call granularity, one call later).  SHINE_CACHE_LAG=0: the
+// updates of a call are applied before it returns (the round-3/4 behaviour: the host waits for the replay).
+bool cache_lagged() { return env_int("SHINE_CACHE_LAG", 1) != 0; }
+
+int fetch_logs(shine_index* h, Replica& R) {
   if (!R.logn.p) return 0;
   HIP_TRY(hipSetDevice(R.device));
   uint32_t cnt[2] = {0, 0};
   HIP_TRY(hipMemcpy(cnt, R.logn.p, sizeof(cnt), hipMemcpyDeviceToHost));
   const uint32_t n0 = std::min(cnt[0], R.clog_cap), n1 = std::min(cnt[1], R.rlog_cap);
-  std::vector<unsigned long long> cl(n0);
-  std::vector<uint32_t> rl(n1);
-  if (n0) HIP_TRY(hipMemcpy(cl.data(), R.clog.p, n0 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-  if (n1) HIP_TRY(hipMemcpy(rl.data(), R.rlog.p, n1 * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  std::vector<uint32_t> rescued_keys;
-  rescued_keys.reserve(n1);
-  for (uint32_t slot : rl) rescued_keys.push_back(R.cache.slot_key(slot));
-  std::vector<CacheCandidate> cand(n0);
-  for (uint32_t i = 0; i < n0; ++i) {
-    const unsigned long long e = cl[i];
+  const size_t b0 = R.pend_clog.size(), b1 = R.pend_rlog.size();
+  R.pend_clog.resize(b0 + n0);
+  R.pend_rlog.resize(b1 + n1);
+  if (n0) HIP_TRY(hipMemcpy(R.pend_clog.data() + b0, R.clog.p, n0 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  if (n1) HIP_TRY(hipMemcpy(R.pend_rlog.data() + b1, R.rlog.p, n1 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  R.pend_lost += (cnt[0] - n0) + (cnt[1] - n1);
+  HIP_TRY(hipMemsetAsync(R.logn.p, 0, 2 * sizeof(uint32_t), R.stream));  // before the slot's next search
+  return 0;
+}
+
+// Host only (no HIP call): safe on a thread per slot while the main thread waits.
+void replay(const shine_index* h, Replica& R, shine_stats* agg) {
+  if (R.pend_clog.empty() && R.pend_rlog.empty()) return;
+  std::vector<uint32_t> rescued_keys;  // hits on cooling entries, by device id
+  rescued_keys.reserve(R.pend_rlog.size());
+  for (uint32_t x : R.pend_rlog)
+    if (x < h->uid_of_dev.size()) rescued_keys.push_back(h->uid_of_dev[x]);
+  std::sort(rescued_keys.begin(), rescued_keys.end());
+  rescued_keys.erase(std::unique(rescued_keys.begin(), rescued_keys.end()), rescued_keys.end());
+  const std::vector<uint32_t> rescued_copy = rescued_keys;
+  std::vector<CacheCandidate> cand(R.pend_clog.size());
+  for (size_t i = 0; i < cand.size(); ++i) {
+    const unsigned long long e = R.pend_clog[i];
     CacheCandidate& c = cand[i];
     c.query = static_cast<uint32_t>(e >> 32) & 0x7FFFFFFFu;
     c.dev_id = static_cast<uint32_t>(e) & 0x7FFFFFFFu;
@@ -1263,58 +1290,94 @@ int apply_dynamic(shine_index* h, Replica& R, shine_stats* agg) {
   std::vector<CacheUpdate> ups;
   std::vector<uint32_t> cool_on;
   R.cache.apply_call(std::move(rescued_keys), std::move(cand), ups, cool_on);
-  // one change per slot: the occupant at the call's start leaves cslot, the last one admitted is copied in
+  // one change per slot: the occupant at the call's start leaves cslot, the last one admitted is copied in (ups are in
+  // slot-claim order; `at` maps a slot to its entry of `order`)
   std::vector<uint32_t> order, first_old, last_new;
-  std::unordered_map<uint32_t, uint32_t> at;
+  std::vector<uint32_t> at(R.cache.capacity(), kInvalid);
   for (const CacheUpdate& u : ups) {
-    auto it = at.find(u.slot);
-    if (it == at.end()) {
-      at.emplace(u.slot, static_cast<uint32_t>(order.size()));
+    if (at[u.slot] == kInvalid) {
+      at[u.slot] = static_cast<uint32_t>(order.size());
       order.push_back(u.slot);
       first_old.push_back(u.old_dev);
       last_new.push_back(u.new_dev);
     } else {
-      last_new[it->second] = u.new_dev;
+      last_new[at[u.slot]] = u.new_dev;
     }
   }
-  std::vector<uint32_t> upd;
+  // (every replay is uploaded before the next one: enqueue_update follows each replay_all)
+  std::vector<uint32_t>& upd = R.upd_vec;
+  std::vector<uint32_t> drop, fill;
   for (uint32_t i = 0; i < order.size(); ++i)
-    if (first_old[i] != kInvalid) upd.push_back(first_old[i]);
-  const uint32_t n_drop = static_cast<uint32_t>(upd.size());
+    if (first_old[i] != kInvalid) drop.push_back(first_old[i]);
   for (uint32_t i = 0; i < order.size(); ++i) {
-    upd.push_back(order[i]);
-    upd.push_back(last_new[i]);
+    fill.push_back(order[i]);
+    fill.push_back(last_new[i]);
   }
-  const uint32_t n_fill = static_cast<uint32_t>(order.size());
-  std::vector<uint32_t> touched(rl);
+  std::vector<uint32_t> touched;
+  for (uint32_t key : rescued_copy)  // the rescued entries still cached (their flags may have changed)
+    if (R.cache.slot_of(key) != kInvalid) touched.push_back(R.cache.slot_of(key));
   touched.insert(touched.end(), cool_on.begin(), cool_on.end());
   touched.insert(touched.end(), order.begin(), order.end());
   std::sort(touched.begin(), touched.end());
   touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
-  for (uint32_t slot : touched) {  // the engine's final cooling state of every slot this call changed
-    upd.push_back(slot);
-    upd.push_back(R.cache.cooling(slot) ? 1u : 0u);
+  std::vector<uint32_t> cool;
+  for (uint32_t slot : touched) {  // the engine's final cooling state of every slot this replay changed
+    cool.push_back(slot);
+    cool.push_back(R.cache.cooling(slot) ? 1u : 0u);
   }
-  const uint32_t n_cool = static_cast<uint32_t>(touched.size());
-  if (!upd.empty()) {
-    if (R.upd.n < upd.size()) HIP_TRY(hipStreamSynchronize(R.stream));
-    if (int rc = R.upd.grow(upd.size())) return rc;
-    HIP_TRY(hipMemcpyAsync(R.upd.p, upd.data(), upd.size() * sizeof(uint32_t), hipMemcpyHostToDevice, R.stream));
-    hipError_t e = launch_cache_apply(R.upd.p, n_drop, n_fill, n_cool, R.cslot.p, R.cvec.p, R.cool.p,
-                                      reinterpret_cast<const uint8_t*>(h->svec.view[R.slot].va),
-                                      row_bytes(h->dim, h->elem), R.stream);
-    if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("cache update: ") + hipGetErrorString(e));
-  }
-  HIP_TRY(hipMemsetAsync(R.logn.p, 0, 2 * sizeof(uint32_t), R.stream));
-  HIP_TRY(hipStreamSynchronize(R.stream));  // the upload reads a host vector that goes out of scope here
-  ++R.dyn_call;
+  upd.clear();
+  upd.insert(upd.end(), drop.begin(), drop.end());
+  upd.insert(upd.end(), fill.begin(), fill.end());
+  upd.insert(upd.end(), cool.begin(), cool.end());
+  R.upd_drop = static_cast<uint32_t>(drop.size());
+  R.upd_fill = static_cast<uint32_t>(fill.size() / 2);
+  R.upd_cool = static_cast<uint32_t>(cool.size() / 2);
   if (agg) {
     agg->cache_admitted += R.cache.admitted - a0;
     agg->cache_evicted += R.cache.evicted - e0;
     agg->cache_rescued += R.cache.rescued - r0;
-    agg->cache_log_dropped += (cnt[0] - n0) + (cnt[1] - n1);
+    agg->cache_log_dropped += R.pend_lost;
   }
+  R.pend_clog.clear();
+  R.pend_rlog.clear();
+  R.pend_lost = 0;
+}
+
+// The replayed updates onto the slot's stream (from pinned host memory: the stream is synchronized before the next
+// upload reuses it).  A device-API search on another stream of the slot may still read the arena: the device drains
+// first then.
+int enqueue_update(shine_index* h, Replica& R) {
+  if (R.upd_vec.empty()) return 0;
+  HIP_TRY(hipSetDevice(R.device));
+  if (R.dev_api_dirty) {
+    HIP_TRY(hipDeviceSynchronize());
+    R.dev_api_dirty = false;
+  }
+  const size_t n = R.upd_vec.size();
+  if (R.upd.n < n || R.upd_host.n < n) HIP_TRY(hipStreamSynchronize(R.stream));
+  if (int rc = R.upd.grow(n)) return rc;
+  if (int rc = R.upd_host.grow(n)) return rc;
+  std::memcpy(R.upd_host.p, R.upd_vec.data(), n * sizeof(uint32_t));
+  HIP_TRY(hipMemcpyAsync(R.upd.p, R.upd_host.p, n * sizeof(uint32_t), hipMemcpyHostToDevice, R.stream));
+  hipError_t e = launch_cache_apply(R.upd.p, R.upd_drop, R.upd_fill, R.upd_cool, R.cslot.p, R.cvec.p, R.cool.p,
+                                    reinterpret_cast<const uint8_t*>(h->svec.view[R.slot].va), row_bytes(h->dim, h->elem),
+                                    R.stream);
+  if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("cache update: ") + hipGetErrorString(e));
+  R.upd_vec.clear();
+  R.upd_drop = R.upd_fill = R.upd_cool = 0;
   return 0;
+}
+
+// replay on every slot with pending logs, one thread each (8 slots of a 10M-record index filling their caches took
+// ~0.3 s a call one after the other, profiles/r03/config_lines_cfg4_10m.jsonl)
+void replay_all(shine_index* h, std::vector<shine_stats>& per) {
+  const size_t G = h->reps.size();
+  per.assign(G, shine_stats{});
+  std::vector<std::thread> th;
+  for (size_t r = 0; r < G; ++r)
+    if (!h->reps[r].pend_clog.empty() || !h->reps[r].pend_rlog.empty())
+      th.emplace_back([h, r, &per] { replay(h, h->reps[r], &per[r]); });
+  for (auto& t : th) t.join();
 }
 
 // Queries per chunk of a large host-API call (the bench's batch) and the chunks in flight per slot: four, as the bench
@@ -1395,8 +1458,10 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     if (int rc = R.hids.grow(static_cast<size_t>(n) * k, kMapped)) return drain(r, rc);
     if (int rc = R.hd.grow(static_cast<size_t>(n) * k, kMapped)) return drain(r, rc);
     if (int rc = R.hqs.grow(static_cast<size_t>(n) * kQsWords + 8, kMapped)) return drain(r, rc);
-    for (uint32_t j = 0; j < n; ++j)
-      std::memcpy(R.hq.p + j * d, queries + static_cast<size_t>(part[r][j]) * d, d * sizeof(float));
+    auto stage = [&](uint32_t lo, uint32_t hi) {  // queries lo .. hi-1 of the slot into the staging
+      for (uint32_t j = lo; j < hi; ++j)
+        std::memcpy(R.hq.p + static_cast<size_t>(j) * d, queries + static_cast<size_t>(part[r][j]) * d, d * sizeof(float));
+    };
     float *dq = nullptr, *dd = nullptr;
     uint32_t *dids = nullptr, *dqs = nullptr;
     hipError_t pe = hipHostGetDevicePointer(reinterpret_cast<void**>(&dq), R.hq.p, 0);
@@ -1405,6 +1470,7 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     if (pe == hipSuccess) pe = hipHostGetDevicePointer(reinterpret_cast<void**>(&dqs), R.hqs.p, 0);
     if (pe != hipSuccess) return drain(r, set_error(SHINE_ERR_HIP, std::string("hipHostGetDevicePointer: ") + hipGetErrorString(pe)));
     if (n <= chunk) {
+      stage(0, n);
       if (int rc = enqueue_search(h, R, dq, n, k, ef, dids, dd, dqs, R.stream, true, access ? (*access)[r].p : nullptr))
         return drain(r + 1, rc);
       continue;
@@ -1417,12 +1483,22 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     HIP_TRY(hipEventRecord(R.ev0, R.stream));
     HIP_TRY(hipEventRecord(R.hfork, R.stream));
     for (hipStream_t hs : R.hstreams) HIP_TRY(hipStreamWaitEvent(hs, R.hfork, 0));
+    // each chunk is staged just before its launch (the first starts after one chunk's copy, not the whole call's) and
+    // signals an event, so its results are copied out while later chunks still run (below)
+    const uint32_t n_chunks = (n + chunk - 1) / chunk;
+    while (R.hchunk.size() < n_chunks) {
+      hipEvent_t ev = nullptr;
+      HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      R.hchunk.push_back(ev);
+    }
     for (uint32_t c = 0, off = 0; off < n; ++c, off += chunk) {
       const uint32_t m = std::min(chunk, n - off);
       hipStream_t hs = R.hstreams[c % R.hstreams.size()];
+      stage(off, off + m);
       if (int rc = enqueue_search(h, R, dq + static_cast<size_t>(off) * d, m, k, ef, dids + static_cast<size_t>(off) * k,
                                   dd + static_cast<size_t>(off) * k, dqs + static_cast<size_t>(off) * kQsWords, hs, false))
         return drain(r + 1, rc);  // (the slot's host streams drain with the device below)
+      HIP_TRY(hipEventRecord(R.hchunk[c], hs));
     }
     for (size_t i = 0; i < R.hstreams.size(); ++i) {
       HIP_TRY(hipEventRecord(R.hjoin[i], R.hstreams[i]));
@@ -1431,35 +1507,26 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     HIP_TRY(hipEventRecord(R.ev1, R.stream));
     chunked[r] = 1;
   }
-  double kernel_ms = 0;
-  uint64_t retries = 0;
-  for (uint32_t r = 0; r < G; ++r) {
-    const uint32_t n = static_cast<uint32_t>(part[r].size());
-    if (n == 0) continue;
-    Replica& R = h->reps[r];
-    HIP_TRY(hipSetDevice(R.device));
-    HIP_TRY(hipStreamSynchronize(R.stream));
-    float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, R.ev0, R.ev1));
-    kernel_ms = std::max(kernel_ms, static_cast<double>(ms));
-    if (r < h->slot_rate.size() && ms > 0) h->slot_rate[r] = n / static_cast<double>(ms);
-    if (!chunked[r]) {
-      const uint32_t* cnt = R.main.seen.p;  // written by the call's last pass (finish_call)
-      retries += cnt[0] + cnt[1] + cnt[2];  // queries handed on by each pass
-    } else {  // chunks: the last chunk of every host stream (its counter words hold its own call only)
-      for (hipStream_t hs : R.hstreams) {
-        const uint32_t* cnt = scratch_for(R, hs).seen.p;
-        if (cnt && cnt[3]) retries += cnt[0] + cnt[1] + cnt[2];
-      }
-    }
-    if (env_int("SHINE_PHASE_PROFILE", 0) && R.prof.p) print_phase_profile(h, R);
+  // Dynamic cache, pipelined: the previous call's logs are replayed while this call's searches run, and the updates
+  // go onto each slot's stream behind them (they serve from the next call on)
+  const bool dynamic = h->cache_policy == SHINE_CACHE_DYNAMIC && !access;
+  const bool lagged = dynamic && cache_lagged();
+  std::vector<shine_stats> per;
+  double replay_ms = 0;
+  if (lagged) {
+    const auto t0 = std::chrono::steady_clock::now();
+    replay_all(h, per);
+    replay_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    for (uint32_t r = 0; r < G; ++r)
+      if (int rc = enqueue_update(h, h->reps[r])) return drain(G, rc);
   }
   int rc = SHINE_OK;
   shine_stats agg{};
   const uint64_t e = elem_bytes(h->elem);
-  for (uint32_t r = 0; r < G; ++r) {
+  // results of the slot's queries lo .. hi-1 out of the staging into the caller's arrays, and their counters
+  auto collect = [&](uint32_t r, uint32_t lo, uint32_t hi) {
     const Replica& R = h->reps[r];
-    for (size_t j = 0; j < part[r].size(); ++j) {
+    for (size_t j = lo; j < hi; ++j) {
       const uint32_t qi = part[r][j];
       std::memcpy(out_ids + static_cast<size_t>(qi) * k, R.hids.p + j * k, k * 4);
       if (out_dists) std::memcpy(out_dists + static_cast<size_t>(qi) * k, R.hd.p + j * k, k * 4);
@@ -1483,49 +1550,71 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
       agg.node_reads += qs[SHINE_QS_DISTCOMPS] > 0 ? qs[SHINE_QS_DISTCOMPS] - 1 : 0;
       agg.node_cache_hits += qs[SHINE_QS_CACHED_VEC];
     }
+  };
+  double kernel_ms = 0;
+  uint64_t retries = 0;
+  for (uint32_t r = 0; r < G; ++r) {
+    const uint32_t n = static_cast<uint32_t>(part[r].size());
+    if (n == 0) continue;
+    Replica& R = h->reps[r];
+    HIP_TRY(hipSetDevice(R.device));
+    if (chunked[r]) {  // chunk by chunk, in order, while the later ones run
+      for (uint32_t c = 0, off = 0; off < n; ++c, off += chunk) {
+        HIP_TRY(hipEventSynchronize(R.hchunk[c]));
+        collect(r, off, std::min(n, off + chunk));
+      }
+    }
+    HIP_TRY(hipStreamSynchronize(R.stream));
+    if (!chunked[r]) collect(r, 0, n);
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, R.ev0, R.ev1));
+    kernel_ms = std::max(kernel_ms, static_cast<double>(ms));
+    if (r < h->slot_rate.size() && ms > 0) h->slot_rate[r] = n / static_cast<double>(ms);
+    if (!chunked[r]) {
+      const uint32_t* cnt = R.main.seen.p;  // written by the call's last pass (finish_call)
+      retries += cnt[0] + cnt[1] + cnt[2];  // queries handed on by each pass
+    } else {  // chunks: the last chunk of every host stream (its counter words hold its own call only)
+      for (hipStream_t hs : R.hstreams) {
+        const uint32_t* cnt = scratch_for(R, hs).seen.p;
+        if (cnt && cnt[3]) retries += cnt[0] + cnt[1] + cnt[2];
+      }
+    }
+    if (env_int("SHINE_PHASE_PROFILE", 0) && R.prof.p) print_phase_profile(h, R);
   }
   agg.overflow_retries = retries;
   agg.kernel_ms = kernel_ms;
-  if (h->cache_policy == SHINE_CACHE_DYNAMIC && !access) {
-    // admission / eviction between calls: the slots' caches are independent, so every slot's engine runs on a thread
-    // of its own (8 slots of a 10M-record index filling their caches took ~0.3 s a call one after the other,
-    // profiles/r03/config_lines_cfg4_10m.jsonl)
-    std::vector<shine_stats> per(G);
-    std::vector<int> rcs(G, 0);
-    std::vector<std::string> errs(G);
-    std::vector<std::thread> th;
-    th.reserve(G);
-    // Device-API searches on other streams of a slot may still be reading the arena: the updates below rewrite its
-    // rows and cslot, so every stream of the slot drains first (as shine_cache_update does).  Those calls' logged
-    // misses are applied here too.
+  if (dynamic) {
+    // this call's logs to the host (device-API searches on other streams of a slot log into the same buffers: the
+    // device drains first when one ran)
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t r = 0; r < G; ++r) {
-      HIP_TRY(hipSetDevice(h->reps[r].device));
-      HIP_TRY(hipDeviceSynchronize());
+      Replica& R = h->reps[r];
+      HIP_TRY(hipSetDevice(R.device));
+      if (!lagged || R.dev_api_dirty) {
+        HIP_TRY(hipDeviceSynchronize());
+        R.dev_api_dirty = false;
+      }
+      if (int e2 = fetch_logs(h, R)) return e2;
+      ++R.dyn_call;  // the coin's call counter: one per host call
     }
-    const auto t1 = std::chrono::steady_clock::now();
-    for (uint32_t r = 0; r < G; ++r)
-      th.emplace_back([&, r] {
-        per[r] = shine_stats{};
-        rcs[r] = apply_dynamic(h, h->reps[r], &per[r]);
-        if (rcs[r]) errs[r] = last_error();  // the message is thread-local
-      });
-    for (auto& t : th) t.join();
-    if (env_int("SHINE_DEBUG_CACHE_TIMING", 0)) {  // diagnostics: where the time between calls goes
-      const auto t2 = std::chrono::steady_clock::now();
-      auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-      uint64_t adm = 0;
-      for (const shine_stats& p : per) adm += p.cache_admitted;
-      std::fprintf(stderr, "cache timing: kernel %.3f ms, device sync %.3f ms, replay+update %.3f ms, admitted %llu\n",
-                   kernel_ms, ms(t0, t1), ms(t1, t2), static_cast<unsigned long long>(adm));
+    if (!lagged) {  // the updates before the call returns
+      replay_all(h, per);
+      for (uint32_t r = 0; r < G; ++r) {
+        if (int e2 = enqueue_update(h, h->reps[r])) return e2;
+        HIP_TRY(hipStreamSynchronize(h->reps[r].stream));
+      }
     }
-    for (uint32_t r = 0; r < G; ++r)
-      if (rcs[r]) return set_error(rcs[r], errs[r]);
     for (const shine_stats& p : per) {
       agg.cache_admitted += p.cache_admitted;
       agg.cache_evicted += p.cache_evicted;
       agg.cache_rescued += p.cache_rescued;
       agg.cache_log_dropped += p.cache_log_dropped;
+    }
+    if (env_int("SHINE_DEBUG_CACHE_TIMING", 0)) {  // diagnostics: where the time between calls goes
+      const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      std::fprintf(stderr, "cache timing: kernel %.3f ms, replay during the searches %.3f ms, after them %.3f ms, "
+                   "admitted %llu (%s)\n", kernel_ms, replay_ms, ms, static_cast<unsigned long long>(agg.cache_admitted),
+                   lagged ? "pipelined" : "synchronous");
     }
   }
   if (stats) *stats = agg;
@@ -1803,10 +1892,10 @@ int shine_set_cache_policy(shine_index_t h, int policy, double ratio_percent, ui
     HIP_TRY(hipDeviceSynchronize());
     R.release_dynamic();
     R.clog_cap = 1u << 22;
-    R.rlog_cap = static_cast<uint32_t>(entries);
+    R.rlog_cap = 1u << 22;  // every hit on a cooling entry is logged (duplicates too)
     int rc = 0;
     if ((rc = R.cslot.grow(h->id_space)) || (rc = R.cvec.grow(entries * vrow)) || (rc = R.cool.grow(entries)) ||
-        (rc = R.clog.grow(R.clog_cap)) || (rc = R.rlog.grow(entries)) || (rc = R.logn.grow(2))) {
+        (rc = R.clog.grow(R.clog_cap)) || (rc = R.rlog.grow(R.rlog_cap)) || (rc = R.logn.grow(2))) {
       R.release_dynamic();
       return rc;
     }
@@ -1814,7 +1903,7 @@ int shine_set_cache_policy(shine_index_t h, int policy, double ratio_percent, ui
     HIP_TRY(hipMemsetAsync(R.cool.p, 0, entries * sizeof(uint32_t), R.stream));
     HIP_TRY(hipMemsetAsync(R.logn.p, 0, 2 * sizeof(uint32_t), R.stream));
     HIP_TRY(hipStreamSynchronize(R.stream));
-    R.cache = RecordCache(static_cast<uint32_t>(entries), seed + R.slot);
+    R.cache = RecordCache(static_cast<uint32_t>(entries), seed + R.slot, h->inv_size);  // keys: uids < inv_size
   }
   h->cache_policy = SHINE_CACHE_DYNAMIC;
   h->cache_seed = seed;
@@ -1829,7 +1918,14 @@ int shine_cache_update(shine_index_t h) {
   for (auto& R : h->reps) {  // every stream of the slot may have searched: wait for the device
     HIP_TRY(hipSetDevice(R.device));
     HIP_TRY(hipDeviceSynchronize());
-    if (int rc = apply_dynamic(h, R, nullptr)) return rc;
+    R.dev_api_dirty = false;
+    if (int rc = fetch_logs(h, R)) return rc;
+  }
+  std::vector<shine_stats> per;
+  replay_all(h, per);  // every log not replayed yet (a pipelined call's, device-API searches')
+  for (auto& R : h->reps) {
+    if (int rc = enqueue_update(h, R)) return rc;
+    HIP_TRY(hipStreamSynchronize(R.stream));
   }
   return SHINE_OK;
 }
@@ -1856,7 +1952,10 @@ int shine_selftest_cache(uint32_t entries, uint64_t seed, uint32_t n_calls, cons
                          uint64_t cap, uint64_t* n, uint64_t* counts) {
   if (!cand_off || !resc_off || !n || !counts) return set_error(SHINE_ERR_ARG, "NULL argument");
   if (!RecordCache::size_ok(entries)) return set_error(SHINE_ERR_ARG, "cache no larger than its cooling table");
-  RecordCache c(entries, seed);
+  uint32_t key_space = 1;  // keys below the largest named + 1
+  for (uint32_t i = cand_off[0]; i < cand_off[n_calls]; ++i) key_space = std::max(key_space, cand[3ull * i + 1] + 1);
+  for (uint32_t i = resc_off[0]; i < resc_off[n_calls]; ++i) key_space = std::max(key_space, resc[i] + 1);
+  RecordCache c(entries, seed, key_space);
   for (uint32_t call = 0; call < n_calls; ++call) {
     std::vector<uint32_t> rk(resc + resc_off[call], resc + resc_off[call + 1]);
     std::vector<CacheCandidate> cv;

@@ -170,6 +170,7 @@ struct Replica {
   // runs its chunks over them, forked from and joined back into `stream` by events
   std::vector<hipStream_t> hstreams;
   std::vector<hipEvent_t> hjoin;
+  std::vector<hipEvent_t> hchunk;  // one per chunk of the current call: its results are in the staging
   hipEvent_t hfork = nullptr;
   DevBuf<unsigned long long> prof;  // SHINE_PHASE_PROFILE diagnostics
   // dynamic record cache (SHINE_CACHE_DYNAMIC): this GPU's arena, lookup table, logs and the host policy engine
@@ -178,12 +179,28 @@ struct Replica {
   DevBuf<unsigned long long> clog;
   uint32_t clog_cap = 0, rlog_cap = 0, dyn_call = 0;
   RecordCache cache;
+  // the policy's pipeline (capi.cc): logs of past calls copied to the host and not replayed yet; the arena updates a
+  // replay made, not uploaded yet; a device-API search ran on another stream since the last update
+  std::vector<unsigned long long> pend_clog;
+  std::vector<uint32_t> pend_rlog;
+  uint64_t pend_lost = 0;  // log entries past the device logs' capacity
+  std::vector<uint32_t> upd_vec;
+  uint32_t upd_drop = 0, upd_fill = 0, upd_cool = 0;
+  HostBuf<uint32_t> upd_host;
+  bool dev_api_dirty = false;
   void release_dynamic() {
     for (auto* b : {&cslot, &cool, &rlog, &logn, &upd}) b->release();
     cvec.release();
     clog.release();
+    upd_host.release();
     clog_cap = rlog_cap = dyn_call = 0;
     cache = RecordCache();
+    pend_clog.clear();
+    pend_rlog.clear();
+    pend_lost = 0;
+    upd_vec.clear();
+    upd_drop = upd_fill = upd_cool = 0;
+    dev_api_dirty = false;
   }
 };
 

@@ -27,16 +27,16 @@ struct DevGraph {
   // Dynamic record cache (SHINE_CACHE_DYNAMIC, the reference's cache::Cache, cache.hh:102-311): this GPU's arena of
   // record vectors, fixed during a call and updated between calls by the host's admission / eviction engine.
   // Kernels built with ACCT = 2 look every off-stripe vector read up in cslot: a hit reads the local arena row and
-  // rescues a cooling entry (cache.hh:128-132: its slot goes to rlog), a miss reads over xGMI and is offered for
-  // admission through clog (entry point and upper levels always, level-0 reads while the cache is not full or when
-  // their coin passes, hnsw.hh:447-448).
+  // offers a cooling entry its second chance (cache.hh:128-132: the device id goes to rlog), a miss reads over xGMI
+  // and is offered for admission through clog (entry point and upper levels always, level-0 reads while the cache is
+  // not full or when their coin passes, hnsw.hh:447-448).
   const uint32_t* cslot;      // [id space]: arena slot of device id x, or 0xFFFFFFFF
   const void* cvec;           // [arena slots][row]: cached vectors, device row layout
   uint32_t* cool;             // [arena slots]: 1 while the entry is cooling
   unsigned long long* clog;   // admission candidates: (query << 32) | x | always << 31 | coin << 63
   uint32_t* clog_n;           // [0] candidates logged (may exceed clog_cap: the overflow is counted, not stored);
-                              // [1] rescued slots logged
-  uint32_t* rlog;             // rescued arena slots
+                              // [1] hits on cooling entries logged
+  uint32_t* rlog;             // device ids of the hits on cooling entries
   uint32_t clog_cap, rlog_cap;
   uint32_t dyn_full;          // the cache was full when the call started: level-0 misses draw the coin
   uint32_t dyn_call;          // call counter (coin input)

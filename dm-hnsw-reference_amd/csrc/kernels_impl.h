@@ -709,9 +709,12 @@ __device__ __forceinline__ void count_vec_reads(const SearchArgs& A, ReadCount& 
         const u32 slot = A.g.cslot[x];
         if (slot != INV) {
           c = 1u;
-          if (A.g.cool[slot] && atomicExch(&A.g.cool[slot], 0u)) {  // a hit on a cooling entry: second chance
+          // a hit on a cooling entry: its second chance (cache.hh:128-132) is the host's to give, so every such hit is
+          // logged by device id and the flag is left as the host engine set it: the flags on the device always equal
+          // the engine's after its last update, which is what lets the updates trail the calls (capi.cc replay)
+          if (A.g.cool[slot]) {
             const u32 i = atomicAdd(&A.g.clog_n[1], 1u);
-            if (i < A.g.rlog_cap) A.g.rlog[i] = slot;
+            if (i < A.g.rlog_cap) A.g.rlog[i] = x;
           }
         } else {
           const bool coin = admission_coin(A.g.dyn_seed, A.g.dyn_call, qi, x);

@@ -2,7 +2,8 @@
 
 The reference's compute-node cache (cache.hh:24-311, cooling_table.hh:52-98, hnsw.hh:447-448, 524-548) admits a node
 record on a miss — upper levels always, level 0 while not full and then with probability 0.01 — evicts by random
-cooling through the cooling table and rescues a cooling entry that is hit.  The GPU applies it between calls.  In exact
+cooling through the cooling table and rescues a cooling entry that is hit.  The GPU applies it between calls, by
+default one call later (the host replays a call's logs while the next call runs).  In exact
 mode a query reads exactly the records the oracle reads (oracle_knn_trace), so from the same starting state the
 restatement predicts, call after call, every query's cache hits (qstats word SHINE_QS_CACHED_VEC) and each GPU's cache
 contents after the call.  Results never change.
@@ -19,9 +20,12 @@ from shine_amd import datasets as D
 pytestmark = pytest.mark.gpu
 
 
-def _stream(idx, trace_index, batches, slots, seed, k, ef, capacity):
-    """Run every batch through the GPU handle and the restatement side by side; returns per-call hit rates."""
+def _stream(idx, trace_index, batches, slots, seed, k, ef, capacity, lag=False):
+    """Run every batch through the GPU handle and the restatement side by side; returns per-call hit rates.
+    lag: the pipelined policy (capi.cc replay): call n's logs are replayed during call n + 1, so call n searches the
+    cache as calls <= n - 2 left it, and the engine holds calls <= n - 1 when call n returns."""
     caches = [CR.RefCache(capacity, seed + s) for s in range(slots)]
+    pending = None
     rates = []
     for call, (q, ids) in enumerate(batches):
         r = idx.knn(q, k, ef, query_ids=ids)
@@ -53,14 +57,18 @@ def _stream(idx, trace_index, batches, slots, seed, k, ef, capacity):
                     cands[s].append((int(local[i]), u, bool(always[j]),
                                      CR.admission_coin(seed + s, call, int(local[i]), int(dev[j]))))
         np.testing.assert_array_equal(r.qstats[:, L.QS_CACHED_VEC].astype(np.int64), hits)
+        apply, pending = (pending, (rescued, cands)) if lag else ((rescued, cands), None)
         for s in range(slots):
-            caches[s].apply_call(rescued[s], cands[s])
+            if apply is not None:
+                caches[s].apply_call(apply[0][s], apply[1][s])
             np.testing.assert_array_equal(idx.cache_keys(s), np.array(sorted(caches[s].keys()), np.uint32))
         rates.append(r.stats["node_cache_hits"] / max(1, r.stats["node_reads"]))
     return rates, caches
 
 
-def test_dynamic_cache_matches_the_restatement_call_by_call(gpu_available):
+@pytest.mark.parametrize("lag", [True, False], ids=["pipelined", "synchronous"])
+def test_dynamic_cache_matches_the_restatement_call_by_call(lag, gpu_available, monkeypatch):
+    monkeypatch.setenv("SHINE_CACHE_LAG", "1" if lag else "0")
     base = D.deep_like(6000, seed=401, d=96)
     pool = D.deep_like(400, seed=402, d=96)
     dumps, _, _ = O.build(base, 12, 64, 0, 4, seed=5)
@@ -70,7 +78,7 @@ def test_dynamic_cache_matches_the_restatement_call_by_call(gpu_available):
     oi = O.OracleIndex(dumps, 96, 12, 0)
     with shine_amd.Index.from_buffers(dumps, 96, 12, 0, gpus=[0] * slots, placement="sharded") as idx:
         idx.set_cache_policy(L.CACHE_DYNAMIC, ratio_percent=5.0, seed=seed)
-        rates, caches = _stream(idx, oi, batches, slots, seed, k, ef, CR.capacity(6000, 12, 96, 5.0))
+        rates, caches = _stream(idx, oi, batches, slots, seed, k, ef, CR.capacity(6000, 12, 96, 5.0), lag)
     assert caches[0].is_full() and caches[1].is_full()  # the stream went past the fill phase
     assert sum(c.evicted for c in caches) > 0 and rates[-1] > rates[0]
 
