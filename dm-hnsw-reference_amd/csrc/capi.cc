@@ -1269,6 +1269,7 @@ int fetch_logs(shine_index* h, Replica& R) {
 // Host only (no HIP call): safe on a thread per slot while the main thread waits.
 void replay(const shine_index* h, Replica& R, shine_stats* agg) {
   if (R.pend_clog.empty() && R.pend_rlog.empty()) return;
+  const auto t0 = std::chrono::steady_clock::now();
   std::vector<uint32_t> rescued_keys;  // hits on cooling entries, by device id
   rescued_keys.reserve(R.pend_rlog.size());
   for (uint32_t x : R.pend_rlog)
@@ -1289,7 +1290,10 @@ void replay(const shine_index* h, Replica& R, shine_stats* agg) {
   const uint64_t a0 = R.cache.admitted, e0 = R.cache.evicted, r0 = R.cache.rescued;
   std::vector<CacheUpdate> ups;
   std::vector<uint32_t> cool_on;
+  const size_t n_cand = cand.size(), n_resc = rescued_keys.size();
+  const auto t1 = std::chrono::steady_clock::now();
   R.cache.apply_call(std::move(rescued_keys), std::move(cand), ups, cool_on);
+  const auto t2 = std::chrono::steady_clock::now();
   // one change per slot: the occupant at the call's start leaves cslot, the last one admitted is copied in (ups are in
   // slot-claim order; `at` maps a slot to its entry of `order`)
   std::vector<uint32_t> order, first_old, last_new;
@@ -1332,6 +1336,12 @@ void replay(const shine_index* h, Replica& R, shine_stats* agg) {
   R.upd_drop = static_cast<uint32_t>(drop.size());
   R.upd_fill = static_cast<uint32_t>(fill.size() / 2);
   R.upd_cool = static_cast<uint32_t>(cool.size() / 2);
+  if (env_int("SHINE_DEBUG_CACHE_TIMING", 0) > 1) {  // diagnostics: the replay's parts on this slot
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    std::fprintf(stderr, "replay slot %u: %zu candidates, %zu rescued keys, %zu updates: logs %.3f policy %.3f "
+                 "updates %.3f ms\n", R.slot, n_cand, n_resc, ups.size(), ms(t0, t1), ms(t1, t2),
+                 ms(t2, std::chrono::steady_clock::now()));
+  }
   if (agg) {
     agg->cache_admitted += R.cache.admitted - a0;
     agg->cache_evicted += R.cache.evicted - e0;

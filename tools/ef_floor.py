@@ -29,6 +29,7 @@ def main():
     p.add_argument("--efs", default="16,24,32,48,64,128")
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--envs", default=";SHINE_DEBUG_MAIN_ONLY=1", help="';'-separated variants (KEY=VALUE[,KEY=VALUE])")
     p.add_argument("--out", default=str(ROOT / "gpurun_out" / "ef_floor.jsonl"))
     a = p.parse_args()
     import torch
@@ -54,9 +55,9 @@ def main():
                        stream=streams[i % 4].cuda_stream)
 
     lines = []
-    for env in ("", "SHINE_DEBUG_MAIN_ONLY=1"):
-        if env:
-            k_, _, v_ = env.partition("=")
+    for env in a.envs.split(";"):
+        kv = [x.partition("=") for x in env.split(",") if x]
+        for k_, _, v_ in kv:
             os.environ[k_] = v_
         for ef in [int(x) for x in a.efs.split(",")]:
             for i in range(nb + a.warmup):
@@ -75,8 +76,8 @@ def main():
                  "mean_distcomps": float(st[:, 0].mean()), "mean_lists_l0": float(st[:, 4].mean())}
             log(json.dumps(d))
             lines.append(d)
-        if env:
-            del os.environ[env.partition("=")[0]]
+        for k_, _, _ in kv:
+            del os.environ[k_]
     idx.close()
     Path(a.out).parent.mkdir(parents=True, exist_ok=True)
     with open(a.out, "a") as f:
