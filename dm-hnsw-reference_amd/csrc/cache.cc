@@ -51,8 +51,8 @@ RecordCache::RecordCache(uint32_t entries, uint64_t seed, uint32_t key_space)
       CT_(std::max<uint32_t>(1, static_cast<uint32_t>(std::ceil(entries / static_cast<double>(kCoolingBucketEntries) *
                                                                 kCoolingRatio)))),
       state_(seed),
-      buckets_(B_),
-      ct_(CT_),
+      bk_(static_cast<size_t>(B_) * kBW, 0),
+      ct_(static_cast<size_t>(CT_) * kBW, 0),
       key_of_(entries, kInv),
       dev_of_(entries, kInv),
       cooling_(entries, 0) {
@@ -73,31 +73,71 @@ uint64_t RecordCache::rand() {
   return z ^ (z >> 31);
 }
 
+uint32_t RecordCache::bget(uint32_t b, uint32_t i) const {
+  if (i < kInPlace) return bk_[static_cast<size_t>(b) * kBW + 1 + i];
+  return bover_.at(b)[i - kInPlace];
+}
+
+void RecordCache::bpush(uint32_t b, uint32_t key) {
+  uint32_t* r = &bk_[static_cast<size_t>(b) * kBW];
+  if (r[0] < kInPlace) r[1 + r[0]] = key;
+  else bover_[b].push_back(key);
+  ++r[0];
+}
+
+// remove key from bucket b, keeping the others in order (vector::erase in the reference's Bucket)
+void RecordCache::berase(uint32_t b, uint32_t key) {
+  uint32_t* r = &bk_[static_cast<size_t>(b) * kBW];
+  const uint32_t n = r[0];
+  const uint32_t in = n < kInPlace ? n : kInPlace;
+  uint32_t i = 0;
+  while (i < in && r[1 + i] != key) ++i;
+  if (i < in) {
+    for (uint32_t j = i; j + 1 < in; ++j) r[1 + j] = r[2 + j];
+    if (n > kInPlace) {  // the first entry past the in-place ones moves in
+      auto it = bover_.find(b);
+      r[kInPlace] = it->second.front();
+      it->second.erase(it->second.begin());
+      if (it->second.empty()) bover_.erase(it);
+    }
+  } else {
+    auto it = bover_.find(b);
+    it->second.erase(std::find(it->second.begin(), it->second.end(), key));
+    if (it->second.empty()) bover_.erase(it);
+  }
+  r[0] = n - 1;
+}
+
 bool RecordCache::ct_remove(uint32_t key) {  // cooling_table.hh:52-75
-  auto& b = ct_[splitmix(key) % CT_];
-  auto it = std::find(b.begin(), b.end(), key);
-  if (it == b.end()) return false;
-  b.erase(it);
+  uint32_t* r = &ct_[static_cast<size_t>(splitmix(key) % CT_) * kBW];
+  uint32_t i = 0;
+  while (i < r[0] && r[1 + i] != key) ++i;
+  if (i == r[0]) return false;
+  for (uint32_t j = i; j + 1 < r[0]; ++j) r[1 + j] = r[2 + j];
+  --r[0];
   return true;
 }
 
 bool RecordCache::ct_insert(uint32_t key, uint32_t& victim) {  // cooling_table.hh:81-98
-  auto& b = ct_[splitmix(key) % CT_];
+  uint32_t* r = &ct_[static_cast<size_t>(splitmix(key) % CT_) * kBW];
   bool pushed = false;
-  if (b.size() == kCoolingBucketEntries) {
-    victim = b.back();
-    b.pop_back();
+  if (r[0] == kCoolingBucketEntries) {  // the oldest (last) key leaves
+    victim = r[kCoolingBucketEntries];
+    --r[0];
     pushed = true;
   }
-  b.insert(b.begin(), key);
+  for (uint32_t j = r[0]; j > 0; --j) r[1 + j] = r[j];  // newest first
+  r[1] = key;
+  ++r[0];
   return pushed;
 }
 
 uint32_t RecordCache::evict() {  // cache.hh:232-311
   for (;;) {
-    auto& b = buckets_[rand() % B_];
-    if (b.empty()) continue;
-    const uint32_t key = b[rand() % b.size()];
+    const uint32_t b = static_cast<uint32_t>(rand() % B_);
+    const uint32_t n = bsize(b);
+    if (n == 0) continue;
+    const uint32_t key = bget(b, static_cast<uint32_t>(rand() % n));
     const uint32_t slot = slot_of_[key];
     uint32_t victim = kInv;
     bool has_victim = false;
@@ -109,8 +149,7 @@ uint32_t RecordCache::evict() {  // cache.hh:232-311
     if (!has_victim) continue;
     if (!contains(victim) || !cooling_[slot_of_[victim]]) continue;  // rescued meanwhile: no eviction
     const uint32_t vslot = slot_of_[victim];
-    auto& vb = buckets_[murmur64(victim) % B_];
-    vb.erase(std::find(vb.begin(), vb.end(), victim));
+    berase(static_cast<uint32_t>(murmur64(victim) % B_), victim);
     slot_of_[victim] = kInv;
     cooling_[vslot] = 0;
     ++evicted;
@@ -121,7 +160,7 @@ uint32_t RecordCache::evict() {  // cache.hh:232-311
 void RecordCache::insert(uint32_t key, uint32_t dev, std::vector<CacheUpdate>& updates) {  // cache.hh:147-203
   const uint32_t slot = next_idx_ < C_ ? next_idx_++ : evict();
   updates.push_back({slot, dev, dev_of_[slot]});
-  buckets_[murmur64(key) % B_].push_back(key);
+  bpush(static_cast<uint32_t>(murmur64(key) % B_), key);
   slot_of_[key] = slot;
   key_of_[slot] = key;
   dev_of_[slot] = dev;

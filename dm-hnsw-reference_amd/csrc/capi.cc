@@ -686,7 +686,9 @@ LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds
   // insert, dearer than a u32 probe — TTI-shaped 50M: 16,384 two-choice entries ran at 1.35 M QPS against 8,192-9,216
   // u32 entries (the worst query's size) at 1.55 M, both 4 wavefronts per CU (profiles/r04/scale_v7); at 10M 8,192
   // two-choice entries against 4,096 u32 ones, 2.45 M against 2.14 M
-  const bool tie16 = w16 == w32 && t16 > t32 && (kind16(t16) == 1 || t16 >= 2 * t32);
+  // (linear-probed u16 buckets win every tie: at ef <= 32 the round-1 rule took u32 tables on a tie, and u16 ran
+  // 1.21-1.33x faster there — ef = 16 / 32: 18.5 M / 15.1 M QPS against 13.9 M / 12.5 M, profiles/r05/ef_floor.jsonl)
+  const bool tie16 = w16 == w32 && (kind16(t16) == 1 ? t16 >= t32 : t16 >= 2 * t32);
   sh.vis16 = can16 && (w16 > w32 || tie16) ? kind16(t16) : 0;
   if (force16 >= 1 && can16) sh.vis16 = kind16(t16);  // test hook: force the u16 entries
   sh.vis_cap = sh.vis16 ? t16 : t32;
@@ -903,8 +905,10 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
       const uint32_t mean_t = learned_mean_table(S), max_t = learned_max_table(S, ef, R.lds_per_cu);
       const uint64_t need = std::min<uint64_t>(16, (nq + R.cus - 1) / R.cus);
       const bool max_fits = max_t && R.lds_per_cu / search_fast_lds_bytes(max_t, ef, 4) >= need;
-      // (with the hash-table spill a spilled query stays in L2 at any id space, and the mean-sized table wins there)
-      const bool beyond_l2 = 4ull * h->words_per_slot > kXcdL2Bytes && !spill_hashed(h);
+      // (the hash-table spill keeps a spilled query in L2 at any id space, but even so the longest queries spill and set
+      // their batches' times: cfg 4 at 100M ran at 3.39 M QPS mean-sized with hash spills against 4.00 M max-sized,
+      // profiles/r05/scale_cfg4_100m_hash_vs_bitmap.jsonl — the max-sized table stays where the bitmap outgrows L2)
+      const bool beyond_l2 = 4ull * h->words_per_slot > kXcdL2Bytes;
       const int64_t force = env_int("SHINE_FAST_TABLE_MAX", -1);
       learned_fast = (force == 1 || (force < 0 && max_fits && beyond_l2)) ? max_t : mean_t;
       learned_mean = mean_t;
