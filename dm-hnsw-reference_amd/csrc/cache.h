@@ -56,6 +56,7 @@ class RecordCache {
 
  private:
   uint64_t rand();
+  uint64_t peek(uint32_t i) const;
   uint32_t evict();  // cache.hh:232-311: frees one slot
   void insert(uint32_t key, uint32_t dev, std::vector<CacheUpdate>& updates);
   bool ct_remove(uint32_t key);

@@ -1654,6 +1654,29 @@ int shine_knn_batch_ex(shine_index_t h, const float* queries, const uint32_t* qu
   return knn_host(h, queries, query_ids, nq, k, ef, out_ids, out_dists, qstats, stats, nullptr);
 }
 
+int shine_prepare(shine_index_t h, uint32_t nq, uint32_t k, uint32_t ef) {
+  if (int rc = check_knn_args(h, k, ef)) return rc;
+  if (nq == 0) return SHINE_OK;
+  std::lock_guard<std::mutex> lk(h->mu);
+  const size_t n = nq;
+  std::vector<float> q(n * h->dim, 0.f);
+  std::vector<uint32_t> ids(n * k);
+  const bool dynamic = h->cache_policy == SHINE_CACHE_DYNAMIC;
+  std::vector<uint32_t> calls;
+  for (const Replica& R : h->reps) calls.push_back(R.dyn_call);
+  if (int rc = knn_host(h, q.data(), nullptr, nq, k, ef, ids.data(), nullptr, nullptr, nullptr, nullptr)) return rc;
+  if (dynamic) {  // the setup searches leave the cache as it was: their logs dropped, the coin's call count restored
+    for (size_t r = 0; r < h->reps.size(); ++r) {
+      Replica& R = h->reps[r];
+      R.pend_clog.clear();
+      R.pend_rlog.clear();
+      R.pend_lost = 0;
+      R.dyn_call = calls[r];
+    }
+  }
+  return SHINE_OK;
+}
+
 int shine_cache_warmup(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
                        uint32_t ef) {
   if (int rc = check_knn_args(h, k, ef)) return rc;

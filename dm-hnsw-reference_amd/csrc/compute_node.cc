@@ -7,7 +7,8 @@
 //   build or load      --store-index / --load-index / neither (compute_node.cc:79-101, memory_node.hh:130-209):
 //                      shine_build (+ shine_build_write) or the dumps under <data-path>/dump
 //   warmup             with --cache: the warmup queries run first and feed the cache admission (compute_node.cc:116-131)
-//   run_queries        batches through shine_knn_batch with the queries' ids; query_results[q_id] is filled from
+//   run_queries        shine_prepare (setup, untimed), then the whole query set through shine_knn_batch (chunks in
+//                      flight inside the library) with the queries' ids; query_results[q_id] is filled from
 //                      out_ids (compute_thread.hh:77), the wall time of the whole phase is the query time
 //   recall             compute_local_recall (compute_node.cc:579-600)
 //   statistics         one JSON document on stdout under the reference's names (statistics.hh:122-130,
@@ -462,6 +463,11 @@ int run(const Config& c) {
     t_warm.stop();
   }
 
+  // the compute threads' setup, outside the query timer (compute_node.cc:354-380): streams, scratch and staging for
+  // the query phase's calls and the kernels' code, by a call over all-zero queries
+  check(shine_prepare(h, std::max<uint32_t>(1, c.batch ? std::min(c.batch, queries.num_read()) : queries.num_read()),
+                      c.k, c.ef_search),
+        "shine_prepare");
   status("run queries");
   ComputeThread th;
   t_query.start();

@@ -153,6 +153,10 @@ class Index:
                                         C.byref(st)))
         return KnnResult(ids, dists, qs, st.as_dict())
 
+    def prepare(self, nq: int, k: int, ef: int) -> None:
+        """shine_prepare: one-time setup (streams, scratch, staging, kernel code) for calls of up to nq queries."""
+        L.check(L.lib().shine_prepare(self._h, nq, k, ef))
+
     def cache_warmup(self, queries: np.ndarray, k: int, ef: int, query_ids: np.ndarray | None = None) -> None:
         """shine_cache_warmup: run the warmup split and re-rank every stripe's cached prefix by its reads."""
         q = np.ascontiguousarray(queries, dtype=np.float32)

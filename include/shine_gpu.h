@@ -159,9 +159,18 @@ int shine_open_buffers_ex(const uint8_t* const* dumps, const uint64_t* sizes, ui
  * out_dists (nullable): nq × k.  stats (nullable): aggregates.  The signature is SURVEY.md §8b's.
  * Requires ef >= k (hnsw.hh:36).  Synchronous: every slot's batch is staged in pinned host memory mapped into the
  * GPU's address space (the kernels read the queries and write the results over PCIe themselves, no copy engine) and
- * enqueued before the call waits. */
+ * enqueued before the call waits.  A slot's share beyond 1,024 queries (SHINE_HOST_CHUNK) runs as 1,024-query chunks
+ * kept in flight on four streams of the slot, each staged just before its launch and copied out as soon as it is
+ * done — the T threads x C coroutines of queries the reference keeps in flight (scheduler.hh:42-96,
+ * compute_node.cc:354-386); not under the dynamic cache policy, whose logs are per launch. */
 int shine_knn_batch(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
                     uint32_t ef, uint32_t* out_ids, float* out_dists, shine_stats* stats);
+
+/* One-time setup before a measured query phase (the GPU side of the reference's compute-thread setup, outside its
+ * query timer, compute_node.cc:354-380): on every slot the host streams, per-stream scratch and pinned staging for
+ * calls of up to nq queries, and the search kernels' code loaded, by searching nq all-zero queries (results
+ * discarded; the dynamic cache's logs of them are dropped). */
+int shine_prepare(shine_index_t h, uint32_t nq, uint32_t k, uint32_t ef);
 
 /* shine_knn_batch with the per-query counters as well: qstats (nullable) nq × SHINE_QS_WORDS, query i's row. */
 int shine_knn_batch_ex(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
