@@ -2,8 +2,14 @@
 // call granularity.  See cache.h.
 #include "cache.h"
 
+#include <sys/mman.h>
+
 #include <algorithm>
 #include <cmath>
+#include <new>
+#ifndef SHINE_CACHE_PF
+#define SHINE_CACHE_PF 4
+#endif
 
 namespace shine {
 
@@ -45,18 +51,44 @@ uint64_t cache_entries(uint64_t n, uint32_t M, uint32_t dim, double ratio_percen
   return cache_size / (16ull + 4ull * dim);  // compute_node.cc:40-54
 }
 
+template <typename T>
+HugeArray<T>::HugeArray(size_t n) : n_(n) {
+  if (n == 0) return;
+  constexpr size_t kHuge = 2u << 20;
+  bytes_ = (n * sizeof(T) + kHuge - 1) / kHuge * kHuge;
+  void* p = mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) throw std::bad_alloc();
+  madvise(p, bytes_, MADV_HUGEPAGE);  // a hint: without huge pages the array still works (zero-filled by mmap)
+  p_ = static_cast<T*>(p);
+}
+
+template <typename T>
+void HugeArray<T>::release() {
+  if (p_) munmap(p_, bytes_);
+  p_ = nullptr;
+  n_ = bytes_ = 0;
+}
+
+template class HugeArray<uint32_t>;
+template class HugeArray<uint8_t>;
+
 RecordCache::RecordCache(uint32_t entries, uint64_t seed, uint32_t key_space)
     : C_(entries),
       B_(std::max<uint32_t>(1, entries)),
       CT_(std::max<uint32_t>(1, static_cast<uint32_t>(std::ceil(entries / static_cast<double>(kCoolingBucketEntries) *
                                                                 kCoolingRatio)))),
+      key_space_(key_space),
       state_(seed),
-      bk_(static_cast<size_t>(B_) * kBW, 0),
-      ct_(static_cast<size_t>(CT_) * kBW, 0),
-      key_of_(entries, kInv),
-      dev_of_(entries, kInv),
-      cooling_(entries, 0) {
-  slot_of_.assign(key_space, kInv);
+      bk_(static_cast<size_t>(B_) * kBW),
+      ct_(static_cast<size_t>(CT_) * kCW),
+      key_of_(entries),
+      dev_of_(entries),
+      cooling_(entries) {
+  modB_ = FastMod(B_);
+  modCT_ = FastMod(CT_);
+  for (uint32_t n = 1; n <= kInPlace; ++n) mod_n_[n] = FastMod(n);
+  std::fill(key_of_.data(), key_of_.data() + entries, kInv);
+  std::fill(dev_of_.data(), dev_of_.data() + entries, kInv);
 }
 
 bool RecordCache::size_ok(uint32_t entries) {
@@ -73,43 +105,83 @@ uint64_t RecordCache::rand() {
   return z ^ (z >> 31);
 }
 
-uint32_t RecordCache::bget(uint32_t b, uint32_t i) const {
-  if (i < kInPlace) return bk_[static_cast<size_t>(b) * kBW + 1 + i];
-  return bover_.at(b)[i - kInPlace];
+uint32_t RecordCache::bucket_of(uint32_t key) const { return static_cast<uint32_t>(modB_(murmur64(key))); }
+uint32_t RecordCache::cool_of(uint32_t key) const { return static_cast<uint32_t>(modCT_(splitmix(key))); }
+
+uint32_t RecordCache::bfind(uint32_t b, uint32_t key) const {
+  const uint32_t* r = brec(b);
+  const uint32_t in = r[0] < kInPlace ? r[0] : kInPlace;
+  for (uint32_t i = 0; i < in; ++i)
+    if (r[1 + 2 * i] == key) return r[2 + 2 * i];
+  if (r[0] > kInPlace) {
+    const std::vector<uint32_t>& o = bover_.at(b);
+    for (size_t i = 0; i < o.size(); i += 2)
+      if (o[i] == key) return o[i + 1];
+  }
+  return kInv;
 }
 
-void RecordCache::bpush(uint32_t b, uint32_t key) {
-  uint32_t* r = &bk_[static_cast<size_t>(b) * kBW];
-  if (r[0] < kInPlace) r[1 + r[0]] = key;
-  else bover_[b].push_back(key);
+uint32_t RecordCache::slot_of(uint32_t key) const {
+  if (C_ == 0 || key >= key_space_) return kInv;
+  return bfind(bucket_of(key), key);
+}
+
+void RecordCache::bget(uint32_t b, uint32_t i, uint32_t& key, uint32_t& slot) const {
+  if (i < kInPlace) {
+    key = brec(b)[1 + 2 * i];
+    slot = brec(b)[2 + 2 * i];
+    return;
+  }
+  const std::vector<uint32_t>& o = bover_.at(b);
+  key = o[2 * (i - kInPlace)];
+  slot = o[2 * (i - kInPlace) + 1];
+}
+
+void RecordCache::bpush(uint32_t b, uint32_t key, uint32_t slot) {
+  uint32_t* r = brec(b);
+  if (r[0] < kInPlace) {
+    r[1 + 2 * r[0]] = key;
+    r[2 + 2 * r[0]] = slot;
+  } else {
+    auto& o = bover_[b];
+    o.push_back(key);
+    o.push_back(slot);
+  }
   ++r[0];
 }
 
 // remove key from bucket b, keeping the others in order (vector::erase in the reference's Bucket)
 void RecordCache::berase(uint32_t b, uint32_t key) {
-  uint32_t* r = &bk_[static_cast<size_t>(b) * kBW];
+  uint32_t* r = brec(b);
   const uint32_t n = r[0];
   const uint32_t in = n < kInPlace ? n : kInPlace;
   uint32_t i = 0;
-  while (i < in && r[1 + i] != key) ++i;
+  while (i < in && r[1 + 2 * i] != key) ++i;
   if (i < in) {
-    for (uint32_t j = i; j + 1 < in; ++j) r[1 + j] = r[2 + j];
+    for (uint32_t j = i; j + 1 < in; ++j) {
+      r[1 + 2 * j] = r[3 + 2 * j];
+      r[2 + 2 * j] = r[4 + 2 * j];
+    }
     if (n > kInPlace) {  // the first entry past the in-place ones moves in
       auto it = bover_.find(b);
-      r[kInPlace] = it->second.front();
-      it->second.erase(it->second.begin());
+      r[1 + 2 * (kInPlace - 1)] = it->second[0];
+      r[2 + 2 * (kInPlace - 1)] = it->second[1];
+      it->second.erase(it->second.begin(), it->second.begin() + 2);
       if (it->second.empty()) bover_.erase(it);
     }
   } else {
     auto it = bover_.find(b);
-    it->second.erase(std::find(it->second.begin(), it->second.end(), key));
-    if (it->second.empty()) bover_.erase(it);
+    auto& o = it->second;
+    size_t k = 0;
+    while (o[k] != key) k += 2;
+    o.erase(o.begin() + k, o.begin() + k + 2);
+    if (o.empty()) bover_.erase(it);
   }
   r[0] = n - 1;
 }
 
 bool RecordCache::ct_remove(uint32_t key) {  // cooling_table.hh:52-75
-  uint32_t* r = &ct_[static_cast<size_t>(splitmix(key) % CT_) * kBW];
+  uint32_t* r = &ct_[static_cast<size_t>(cool_of(key)) * kCW];
   uint32_t i = 0;
   while (i < r[0] && r[1 + i] != key) ++i;
   if (i == r[0]) return false;
@@ -119,7 +191,7 @@ bool RecordCache::ct_remove(uint32_t key) {  // cooling_table.hh:52-75
 }
 
 bool RecordCache::ct_insert(uint32_t key, uint32_t& victim) {  // cooling_table.hh:81-98
-  uint32_t* r = &ct_[static_cast<size_t>(splitmix(key) % CT_) * kBW];
+  uint32_t* r = &ct_[static_cast<size_t>(cool_of(key)) * kCW];
   bool pushed = false;
   if (r[0] == kCoolingBucketEntries) {  // the oldest (last) key leaves
     victim = r[kCoolingBucketEntries];
@@ -140,29 +212,44 @@ uint64_t RecordCache::peek(uint32_t i) const {
   return z ^ (z >> 31);
 }
 
+// The next pick of the eviction scan, read ahead (its bucket's line was requested SHINE_CACHE_PF draws earlier): the
+// lines its step will touch — the entry's cooling flag, its cooling-table bucket and, when that bucket is full, the
+// hash bucket of the key it would push out — are requested now, so that the victim lookup, the scan's one dependent
+// miss, overlaps this step's.  A hint only: the step itself re-reads everything.
+void RecordCache::lookahead() const {
+  const uint32_t* r = brec(static_cast<uint32_t>(modB_(peek(1))));
+  const uint32_t n = r[0];
+  if (n == 0 || n > kInPlace) return;
+  const uint32_t i = static_cast<uint32_t>(mod_n_[n](peek(2)));
+  const uint32_t key = r[1 + 2 * i];
+  __builtin_prefetch(&cooling_[r[2 + 2 * i]]);
+  const uint32_t* c = &ct_[static_cast<size_t>(cool_of(key)) * kCW];
+  if (c[0] == kCoolingBucketEntries) __builtin_prefetch(brec(bucket_of(c[kCoolingBucketEntries])));
+}
+
 uint32_t RecordCache::evict() {  // cache.hh:232-311
   for (;;) {
-    const uint32_t b = static_cast<uint32_t>(rand() % B_);
+    const uint32_t b = static_cast<uint32_t>(modB_(rand()));
     // the next pick's bucket is one or two draws ahead (an empty bucket takes no entry draw): both requested now, so
-    // the loop's dependent misses overlap (an admission into a full cache took ~1 us of misses)
-    __builtin_prefetch(&bk_[static_cast<size_t>(peek(1) % B_) * kBW]);
-    __builtin_prefetch(&bk_[static_cast<size_t>(peek(2) % B_) * kBW]);
-    const uint32_t n = bsize(b);
+    // the loop's dependent misses overlap
+    for (uint32_t a = 1; a <= SHINE_CACHE_PF; ++a) __builtin_prefetch(brec(static_cast<uint32_t>(modB_(peek(a)))));
+    const uint32_t n = brec(b)[0];
     if (n == 0) continue;
-    const uint32_t key = bget(b, static_cast<uint32_t>(rand() % n));
-    const uint32_t slot = slot_of_[key];
+    uint32_t key, slot;
+    bget(b, static_cast<uint32_t>(n <= kInPlace ? mod_n_[n](rand()) : rand() % n), key, slot);
+    lookahead();
     uint32_t victim = kInv;
     bool has_victim = false;
     if (!cooling_[slot]) {  // hot -> cooling; the table may push its oldest key out
       has_victim = ct_insert(key, victim);
       cooling_[slot] = 1;
-      if (cool_on_) cool_on_->push_back(slot);
+      if (flagged_) flagged_->push_back(slot);
     }
     if (!has_victim) continue;
-    if (!contains(victim) || !cooling_[slot_of_[victim]]) continue;  // rescued meanwhile: no eviction
-    const uint32_t vslot = slot_of_[victim];
-    berase(static_cast<uint32_t>(murmur64(victim) % B_), victim);
-    slot_of_[victim] = kInv;
+    const uint32_t vb = bucket_of(victim);
+    const uint32_t vslot = bfind(vb, victim);
+    if (vslot == kInv || !cooling_[vslot]) continue;  // rescued meanwhile: no eviction
+    berase(vb, victim);
     cooling_[vslot] = 0;
     ++evicted;
     return vslot;
@@ -172,15 +259,14 @@ uint32_t RecordCache::evict() {  // cache.hh:232-311
 void RecordCache::insert(uint32_t key, uint32_t dev, std::vector<CacheUpdate>& updates) {  // cache.hh:147-203
   const uint32_t slot = next_idx_ < C_ ? next_idx_++ : evict();
   updates.push_back({slot, dev, dev_of_[slot]});
-  bpush(static_cast<uint32_t>(murmur64(key) % B_), key);
-  slot_of_[key] = slot;
+  bpush(bucket_of(key), key, slot);
   key_of_[slot] = key;
   dev_of_[slot] = dev;
   cooling_[slot] = 0;
   ++admitted;
 }
 
-// (query, key) order of the candidates: an LSD radix sort over the composite (query << 32 | key), 16-bit digits, only
+// (query, key) order of the candidates: an LSD radix sort over the composite (query << 32 | key), 11-bit digits, only
 // the digits the largest composite needs (a comparison sort of the ~340K candidates one slot logs while its cache
 // fills took most of the time between calls)
 void sort_candidates(std::vector<CacheCandidate>& c) {
@@ -194,10 +280,11 @@ void sort_candidates(std::vector<CacheCandidate>& c) {
     ix[i] = static_cast<uint32_t>(i);
     most |= k[i];
   }
-  std::vector<uint32_t> cnt(1u << 16);
-  for (int shift = 0; shift < 64 && (most >> shift) != 0; shift += 16) {
+  constexpr int kDigit = 11;  // 2K counters a pass: a call's few thousand candidates take 4 cheap passes
+  std::vector<uint32_t> cnt(1u << kDigit);
+  for (int shift = 0; shift < 64 && (most >> shift) != 0; shift += kDigit) {
     std::fill(cnt.begin(), cnt.end(), 0u);
-    for (size_t i = 0; i < n; ++i) ++cnt[(k[i] >> shift) & 0xFFFF];
+    for (size_t i = 0; i < n; ++i) ++cnt[(k[i] >> shift) & ((1u << kDigit) - 1)];
     uint32_t sum = 0;
     for (uint32_t& x : cnt) {
       const uint32_t t = x;
@@ -205,7 +292,7 @@ void sort_candidates(std::vector<CacheCandidate>& c) {
       sum += t;
     }
     for (size_t i = 0; i < n; ++i) {
-      const uint32_t pos = cnt[(k[i] >> shift) & 0xFFFF]++;
+      const uint32_t pos = cnt[(k[i] >> shift) & ((1u << kDigit) - 1)]++;
       k2[pos] = k[i];
       ix2[pos] = ix[i];
     }
@@ -218,29 +305,43 @@ void sort_candidates(std::vector<CacheCandidate>& c) {
 }
 
 void RecordCache::apply_call(std::vector<uint32_t> rescued_keys, std::vector<CacheCandidate> candidates,
-                             std::vector<CacheUpdate>& updates, std::vector<uint32_t>& cool_on) {
+                             std::vector<CacheUpdate>& updates, std::vector<uint32_t>& flagged) {
   if (C_ == 0) return;
-  cool_on_ = &cool_on;
+  flagged_ = &flagged;
   std::sort(rescued_keys.begin(), rescued_keys.end());
   rescued_keys.erase(std::unique(rescued_keys.begin(), rescued_keys.end()), rescued_keys.end());
-  for (uint32_t key : rescued_keys) {  // cache.hh:128-132
-    if (contains(key) && cooling_[slot_of_[key]] && ct_remove(key)) {
-      cooling_[slot_of_[key]] = 0;
+  constexpr size_t kAhead = 8;  // lookups requested this many keys ahead (each one a likely miss)
+  const size_t nr = rescued_keys.size();
+  for (size_t i = 0; i < nr; ++i) {  // cache.hh:128-132
+    if (i + kAhead < nr && rescued_keys[i + kAhead] < key_space_) {
+      const uint32_t k = rescued_keys[i + kAhead];
+      __builtin_prefetch(brec(bucket_of(k)));
+      __builtin_prefetch(&ct_[static_cast<size_t>(cool_of(k)) * kCW]);
+    }
+    const uint32_t key = rescued_keys[i];
+    const uint32_t slot = slot_of(key);
+    if (slot != kInv && cooling_[slot] && ct_remove(key)) {
+      cooling_[slot] = 0;
+      flagged.push_back(slot);
       ++rescued;
     }
   }
   sort_candidates(candidates);  // (query, key): a query offers a key once, so the order is total
-  for (const CacheCandidate& c : candidates) {
-    if (c.key >= slot_of_.size() || contains(c.key)) continue;  // admitted by an earlier miss (cache.hh:171-179)
+  const size_t nc = candidates.size();
+  for (size_t i = 0; i < nc; ++i) {
+    if (i + kAhead < nc && candidates[i + kAhead].key < key_space_)
+      __builtin_prefetch(brec(bucket_of(candidates[i + kAhead].key)));
+    const CacheCandidate& c = candidates[i];
+    if (c.key >= key_space_ || contains(c.key)) continue;  // admitted by an earlier miss (cache.hh:171-179)
     if (c.always || !full() || c.coin) insert(c.key, c.dev_id, updates);
   }
-  cool_on_ = nullptr;
+  flagged_ = nullptr;
 }
 
 std::vector<uint32_t> RecordCache::keys() const {
   std::vector<uint32_t> out;
-  for (uint32_t k : key_of_)
-    if (k != kInv && contains(k) && key_of_[slot_of_[k]] == k) out.push_back(k);
+  for (size_t s = 0; s < key_of_.size(); ++s)
+    if (const uint32_t k = key_of_[s]; k != kInv && slot_of(k) == s) out.push_back(k);
   std::sort(out.begin(), out.end());
   return out;
 }

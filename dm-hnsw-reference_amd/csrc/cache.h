@@ -16,6 +16,53 @@
 
 namespace shine {
 
+// A zero-filled array in its own mapping, backed by 2 MiB pages where the kernel allows (madvise): the policy's random
+// picks over tens of MiB of bucket records otherwise pay a TLB miss and a page walk on top of each cache miss.
+template <typename T>
+class HugeArray {
+ public:
+  HugeArray() = default;
+  explicit HugeArray(size_t n);
+  HugeArray(HugeArray&& o) noexcept : p_(o.p_), n_(o.n_), bytes_(o.bytes_) { o.p_ = nullptr; o.n_ = o.bytes_ = 0; }
+  HugeArray& operator=(HugeArray&& o) noexcept {
+    if (this != &o) {
+      release();
+      p_ = o.p_; n_ = o.n_; bytes_ = o.bytes_;
+      o.p_ = nullptr; o.n_ = o.bytes_ = 0;
+    }
+    return *this;
+  }
+  HugeArray(const HugeArray&) = delete;
+  HugeArray& operator=(const HugeArray&) = delete;
+  ~HugeArray() { release(); }
+  T* data() { return p_; }
+  const T* data() const { return p_; }
+  size_t size() const { return n_; }
+  T& operator[](size_t i) { return p_[i]; }
+  const T& operator[](size_t i) const { return p_[i]; }
+
+ private:
+  void release();
+  T* p_ = nullptr;
+  size_t n_ = 0, bytes_ = 0;
+};
+
+// x % d for a fixed d by multiplication (Lemire, Kaser, Kurz, "Faster remainder by direct computation", 2019: a
+// 128-bit reciprocal, exact for every 64-bit x and d): the policy takes several remainders per step (bucket of a key,
+// cooling bucket, random pick), and a 64-bit divide costs tens of cycles each.
+struct FastMod {
+  unsigned __int128 m = 0;
+  uint64_t d = 1;
+  FastMod() = default;
+  explicit FastMod(uint64_t div) : m(~static_cast<unsigned __int128>(0) / div + 1), d(div) {}
+  uint64_t operator()(uint64_t x) const {
+    const unsigned __int128 low = m * x;
+    const unsigned __int128 bottom = (static_cast<unsigned __int128>(static_cast<uint64_t>(low)) * d) >> 64;
+    const unsigned __int128 top = static_cast<unsigned __int128>(static_cast<uint64_t>(low >> 64)) * d;
+    return static_cast<uint64_t>((bottom + top) >> 64);
+  }
+};
+
 struct CacheCandidate {
   uint32_t query, key;  // query index of the call, record uid
   uint32_t dev_id;      // the record's device id
@@ -31,7 +78,7 @@ struct CacheUpdate {
 class RecordCache {
  public:
   RecordCache() = default;
-  // key_space: keys are below it (record uids; the key -> slot map is a flat array of that many entries)
+  // key_space: keys are below it (record uids)
   RecordCache(uint32_t entries, uint64_t seed, uint32_t key_space);
 
   uint32_t capacity() const { return C_; }
@@ -39,17 +86,18 @@ class RecordCache {
   // entry can end up cooling with no bucket full, and the reference's loop never finds a victim (cache.hh:232-311)
   static bool size_ok(uint32_t entries);
   bool full() const { return next_idx_ >= C_; }  // cache.hh:205-216
-  bool contains(uint32_t key) const { return key < slot_of_.size() && slot_of_[key] != 0xFFFFFFFFu; }
+  bool contains(uint32_t key) const { return slot_of(key) != 0xFFFFFFFFu; }
 
   // The policy over one call's logs.  rescued: keys of the cooling entries hit; candidates: the misses offered.
-  // Appends the arena changes to `updates` and the slots whose cooling flag must be set to `cool_on`; slots whose
-  // entry left the cache are reported in updates (their flag is cleared with the copy).
+  // Appends the arena changes to `updates` and to `flagged` the slots whose cooling flag changed (set by the eviction
+  // scan, cleared by a second chance); slots whose entry left the cache are reported in updates (their flag is cleared
+  // with the copy).
   void apply_call(std::vector<uint32_t> rescued, std::vector<CacheCandidate> candidates,
-                  std::vector<CacheUpdate>& updates, std::vector<uint32_t>& cool_on);
+                  std::vector<CacheUpdate>& updates, std::vector<uint32_t>& flagged);
 
   std::vector<uint32_t> keys() const;
   uint32_t slot_key(uint32_t slot) const { return slot < key_of_.size() ? key_of_[slot] : 0xFFFFFFFFu; }
-  uint32_t slot_of(uint32_t key) const { return contains(key) ? slot_of_[key] : 0xFFFFFFFFu; }
+  uint32_t slot_of(uint32_t key) const;
   bool cooling(uint32_t slot) const { return slot < cooling_.size() && cooling_[slot] != 0; }
 
   uint64_t admitted = 0, evicted = 0, rescued = 0;
@@ -58,29 +106,36 @@ class RecordCache {
   uint64_t rand();
   uint64_t peek(uint32_t i) const;
   uint32_t evict();  // cache.hh:232-311: frees one slot
+  void lookahead() const;
   void insert(uint32_t key, uint32_t dev, std::vector<CacheUpdate>& updates);
   bool ct_remove(uint32_t key);
   bool ct_insert(uint32_t key, uint32_t& victim);
 
-  // Hash buckets (keys in insertion order) and cooling-table buckets (newest first) as flat arrays of 8-word records:
-  // [count, entries...] — the policy's random picks land on a bucket in one cache line instead of a vector header and
-  // its heap block (two misses; the replay of a full cache spent ~1.5 us per admission there).  A hash bucket holds 7
-  // entries in place and the rare rest (Poisson(1) occupancy: ~1e-5 of the buckets) in `bover_`, in order.
-  static constexpr uint32_t kBW = 8, kInPlace = 7;
-  uint32_t bsize(uint32_t b) const { return bk_[static_cast<size_t>(b) * kBW]; }
-  uint32_t bget(uint32_t b, uint32_t i) const;
-  void bpush(uint32_t b, uint32_t key);
+  // Hash buckets (keys in insertion order, each with its arena slot) as flat 64-byte records, one cache line each:
+  // [count, key0, slot0, ..., key6, slot6, -].  A lookup, the eviction scan's random pick and an erase each touch one
+  // line: the key -> slot map needs no array of its own (a key-space array was a second random miss per step; the
+  // policy is a chain of dependent misses, ~1 us per admission into a full cache).  A bucket holds 7 entries in place
+  // and the rare rest (Poisson(1) occupancy: ~1e-5 of the buckets) in `bover_`, in order.  Cooling-table buckets:
+  // 8-word records [count, up to 6 keys newest first].
+  static constexpr uint32_t kBW = 16, kInPlace = 7, kCW = 8;
+  uint32_t* brec(uint32_t b) { return bk_.data() + static_cast<size_t>(b) * kBW; }
+  const uint32_t* brec(uint32_t b) const { return bk_.data() + static_cast<size_t>(b) * kBW; }
+  uint32_t bucket_of(uint32_t key) const;
+  uint32_t cool_of(uint32_t key) const;  // the key's cooling-table bucket
+  uint32_t bfind(uint32_t b, uint32_t key) const;  // the key's slot, or 0xFFFFFFFF
+  void bget(uint32_t b, uint32_t i, uint32_t& key, uint32_t& slot) const;
+  void bpush(uint32_t b, uint32_t key, uint32_t slot);
   void berase(uint32_t b, uint32_t key);
 
-  uint32_t C_ = 0, B_ = 1, CT_ = 1, next_idx_ = 0;
+  uint32_t C_ = 0, B_ = 1, CT_ = 1, next_idx_ = 0, key_space_ = 0;
+  FastMod modB_, modCT_, mod_n_[kInPlace + 1];  // % B_, % CT_, % n for in-place bucket sizes n
   uint64_t state_ = 0;
-  std::vector<uint32_t> bk_;                                   // [B_][kBW]
-  std::unordered_map<uint32_t, std::vector<uint32_t>> bover_;  // bucket -> entries past kInPlace
-  std::vector<uint32_t> ct_;                                   // [CT_][kBW]: count, up to 6 keys newest first
-  std::vector<uint32_t> slot_of_;                   // key -> arena slot (0xFFFFFFFF: not cached)
-  std::vector<uint32_t> key_of_, dev_of_;           // slot -> key / device id
-  std::vector<uint8_t> cooling_;                    // slot -> cooling
-  std::vector<uint32_t>* cool_on_ = nullptr;
+  HugeArray<uint32_t> bk_;  // [B_][kBW] (page-aligned: records on cache-line boundaries)
+  std::unordered_map<uint32_t, std::vector<uint32_t>> bover_;  // bucket -> (key, slot) pairs past kInPlace
+  HugeArray<uint32_t> ct_;                                     // [CT_][kCW]
+  HugeArray<uint32_t> key_of_, dev_of_;                        // slot -> key / device id
+  HugeArray<uint8_t> cooling_;                                 // slot -> cooling
+  std::vector<uint32_t>* flagged_ = nullptr;
 };
 
 // entries of a compute node's cache: ratio % of estimate_index_size(n) over the record prefix size 16 + 4d

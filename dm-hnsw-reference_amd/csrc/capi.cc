@@ -1280,7 +1280,6 @@ void replay(const shine_index* h, Replica& R, shine_stats* agg) {
     if (x < h->uid_of_dev.size()) rescued_keys.push_back(h->uid_of_dev[x]);
   std::sort(rescued_keys.begin(), rescued_keys.end());
   rescued_keys.erase(std::unique(rescued_keys.begin(), rescued_keys.end()), rescued_keys.end());
-  const std::vector<uint32_t> rescued_copy = rescued_keys;
   std::vector<CacheCandidate> cand(R.pend_clog.size());
   for (size_t i = 0; i < cand.size(); ++i) {
     const unsigned long long e = R.pend_clog[i];
@@ -1293,15 +1292,16 @@ void replay(const shine_index* h, Replica& R, shine_stats* agg) {
   }
   const uint64_t a0 = R.cache.admitted, e0 = R.cache.evicted, r0 = R.cache.rescued;
   std::vector<CacheUpdate> ups;
-  std::vector<uint32_t> cool_on;
+  std::vector<uint32_t> flagged;  // slots whose cooling flag the policy changed
   const size_t n_cand = cand.size(), n_resc = rescued_keys.size();
   const auto t1 = std::chrono::steady_clock::now();
-  R.cache.apply_call(std::move(rescued_keys), std::move(cand), ups, cool_on);
+  R.cache.apply_call(std::move(rescued_keys), std::move(cand), ups, flagged);
   const auto t2 = std::chrono::steady_clock::now();
   // one change per slot: the occupant at the call's start leaves cslot, the last one admitted is copied in (ups are in
   // slot-claim order; `at` maps a slot to its entry of `order`)
   std::vector<uint32_t> order, first_old, last_new;
-  std::vector<uint32_t> at(R.cache.capacity(), kInvalid);
+  std::vector<uint32_t>& at = R.upd_at;  // all kInvalid between replays
+  if (at.size() != R.cache.capacity()) at.assign(R.cache.capacity(), kInvalid);
   for (const CacheUpdate& u : ups) {
     if (at[u.slot] == kInvalid) {
       at[u.slot] = static_cast<uint32_t>(order.size());
@@ -1321,10 +1321,8 @@ void replay(const shine_index* h, Replica& R, shine_stats* agg) {
     fill.push_back(order[i]);
     fill.push_back(last_new[i]);
   }
-  std::vector<uint32_t> touched;
-  for (uint32_t key : rescued_copy)  // the rescued entries still cached (their flags may have changed)
-    if (R.cache.slot_of(key) != kInvalid) touched.push_back(R.cache.slot_of(key));
-  touched.insert(touched.end(), cool_on.begin(), cool_on.end());
+  for (uint32_t slot : order) at[slot] = kInvalid;
+  std::vector<uint32_t> touched = std::move(flagged);
   touched.insert(touched.end(), order.begin(), order.end());
   std::sort(touched.begin(), touched.end());
   touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
@@ -2001,8 +1999,8 @@ int shine_selftest_cache(uint32_t entries, uint64_t seed, uint32_t n_calls, cons
       cv.push_back({t[0], t[1], t[1], (t[2] & 1u) != 0, (t[2] & 2u) != 0});
     }
     std::vector<CacheUpdate> ups;
-    std::vector<uint32_t> cool_on;
-    c.apply_call(std::move(rk), std::move(cv), ups, cool_on);
+    std::vector<uint32_t> flagged;
+    c.apply_call(std::move(rk), std::move(cv), ups, flagged);
   }
   const std::vector<uint32_t> k = c.keys();
   *n = k.size();
