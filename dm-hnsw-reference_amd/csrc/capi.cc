@@ -617,11 +617,14 @@ uint32_t learned_max_table(const Scratch& S, uint32_t ef, uint32_t lds_per_cu) {
 }
 
 // The exact pass's learned table, with the in-place spill: just the previous call's worst query (eighths/8 × its
-// visited count, SHINE_EXACT_LEARN_EIGHTHS, default 9), never below 2,048 entries (SHINE_EXACT_LEARN_MIN), which then
+// visited count, SHINE_EXACT_LEARN_EIGHTHS, default 8), never below 2,048 entries (SHINE_EXACT_LEARN_MIN), which then
 // replaces the fixed size in either direction — a query beyond it spills in place instead of being re-run.  At
 // ef = 128 on the bench's index that is 4,096 entries and 11 wavefronts per CU instead of 8,192 and 7: 3.51 M against
 // 2.38 M QPS (profiles/r03/exact_learned_scan.jsonl); at ef = 32 a 1,024-entry table spilled too often (9.7 M against
-// 10.6 M), hence the floor.  Without the spill: learned_table (1.625 ×).
+// 10.6 M), hence the floor.  No margin above the worst query: with 9/8 (rounds 3-4) a batch whose worst query visits
+// 3,851 nodes put the next call on its stream on 8,192 entries, and that one slow launch set the time of a 20-step run
+// (warmup 5: 3.19 M against 3.64 M QPS with 8/8; 200 steps: 3.74 M against 3.96 M, profiles/r05/k20_exact_eighths.jsonl)
+// — the few queries past the table's 7/8 load spill in place.  Without the spill: learned_table (1.625 ×).
 uint32_t learned_exact_table(const Scratch& S, uint32_t ef) {
   if (!spill_enabled()) return learned_table(S);
   if (!S.seen.p || !S.seen.p[3] || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
@@ -630,7 +633,7 @@ uint32_t learned_exact_table(const Scratch& S, uint32_t ef) {
   // at ef <= 32 the tables are small and a half-empty one probed faster than a fuller one (10.6 M against 9.7 M QPS
   // at ef = 32, profiles/r03/exact_learned_scan_floor.jsonl): the round-2 margin there
   const uint64_t eighths =
-      static_cast<uint64_t>(std::max<int64_t>(8, env_int("SHINE_EXACT_LEARN_EIGHTHS", ef <= 32 ? 13 : 9)));
+      static_cast<uint64_t>(std::max<int64_t>(6, env_int("SHINE_EXACT_LEARN_EIGHTHS", ef <= 32 ? 13 : 8)));
   const uint64_t want = std::min<uint64_t>(16384, vmax * eighths / 8);
   const uint32_t lo = static_cast<uint32_t>(std::max<int64_t>(1024, env_int("SHINE_EXACT_LEARN_MIN", 2048)));
   return std::min<uint32_t>(16384, std::max<uint32_t>({lo, S.table_floor, pow2_at_least(static_cast<uint32_t>(want))}));
