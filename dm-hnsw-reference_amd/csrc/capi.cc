@@ -1301,18 +1301,22 @@ void replay(const shine_index* h, Replica& R, shine_stats* agg) {
   R.cache.apply_call(std::move(rescued_keys), std::move(cand), ups, flagged);
   const auto t2 = std::chrono::steady_clock::now();
   // one change per slot: the occupant at the call's start leaves cslot, the last one admitted is copied in (ups are in
-  // slot-claim order; `at` maps a slot to its entry of `order`)
+  // slot-claim order; `at` maps a slot to its entry of `order`, open-addressed over twice the updates: a few KiB that
+  // stay in cache, where an array over the arena's slots took a miss per update)
   std::vector<uint32_t> order, first_old, last_new;
-  std::vector<uint32_t>& at = R.upd_at;  // all kInvalid between replays
-  if (at.size() != R.cache.capacity()) at.assign(R.cache.capacity(), kInvalid);
+  uint32_t amask = 63;
+  while (amask + 1 < 2 * ups.size()) amask = 2 * amask + 1;
+  std::vector<uint64_t> at(amask + 1, ~0ull);  // (slot << 32) | index
   for (const CacheUpdate& u : ups) {
-    if (at[u.slot] == kInvalid) {
-      at[u.slot] = static_cast<uint32_t>(order.size());
+    uint32_t p = (u.slot * 0x9E3779B1u) & amask;
+    while (at[p] != ~0ull && static_cast<uint32_t>(at[p] >> 32) != u.slot) p = (p + 1) & amask;
+    if (at[p] == ~0ull) {
+      at[p] = (static_cast<uint64_t>(u.slot) << 32) | order.size();
       order.push_back(u.slot);
       first_old.push_back(u.old_dev);
       last_new.push_back(u.new_dev);
     } else {
-      last_new[at[u.slot]] = u.new_dev;
+      last_new[static_cast<uint32_t>(at[p])] = u.new_dev;
     }
   }
   // (every replay is uploaded before the next one: enqueue_update follows each replay_all)
@@ -1324,7 +1328,6 @@ void replay(const shine_index* h, Replica& R, shine_stats* agg) {
     fill.push_back(order[i]);
     fill.push_back(last_new[i]);
   }
-  for (uint32_t slot : order) at[slot] = kInvalid;
   std::vector<uint32_t> touched = std::move(flagged);
   touched.insert(touched.end(), order.begin(), order.end());
   std::sort(touched.begin(), touched.end());

@@ -185,7 +185,6 @@ struct Replica {
   std::vector<uint32_t> pend_rlog;
   uint64_t pend_lost = 0;  // log entries past the device logs' capacity
   std::vector<uint32_t> upd_vec;
-  std::vector<uint32_t> upd_at;  // replay scratch: arena slot -> its entry of the call's update order
   uint32_t upd_drop = 0, upd_fill = 0, upd_cool = 0;
   HostBuf<uint32_t> upd_host;
   bool dev_api_dirty = false;
