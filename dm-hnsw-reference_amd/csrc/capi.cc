@@ -595,25 +595,37 @@ uint32_t learned_mean_table(const Scratch& S) {
   return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, pow2_at_least(mean + mean / 4 + 64)}));
 }
 
-// The previous call's worst query with 1/8 to spare (large id spaces, see enqueue_search).
-// The previous call's worst query with room to spare, for u32 tables (VisitedLds<0>), which take any multiple of 64
-// entries: 9/8 of it rounded up to a power of two, or — where that puts more wavefronts on a CU (one batch's worth,
-// `need`) — 5/4 of it rounded up to 1,024 entries.  100M ids at ef = 128: 6,144 entries and 6 wavefronts per CU
-// instead of 8,192 and 4, 3.97 M against 3.75 M QPS (profiles/r04/diag100m_nonpow2_tables.jsonl); 1/4 to spare, since
-// the next call's worst query may visit more.  Where the multiple of 1,024 gains no wavefront the power of two stays:
-// TTI-shaped 50M at ef = 250 (worst queries 6.4K-8.0K from call to call) ran at 1.35 M QPS on 9,216-10,240 entries
-// against 1.55 M on 8,192 (profiles/r04/scale_v6..v8).  SHINE_FAST_TABLE_POW2=1: always the power of two.
+// The fast table where the spill target is HBM beyond L2 (large id spaces, see enqueue_search): u32 entries
+// (VisitedLds<0>, any multiple of 64), sized for a load of 0.45 at the stream's mean query and then grown to the
+// largest table that keeps the same wavefronts per CU.  A linear-probed table's probe chains, walked in lockstep by the
+// wave's 32 list slots, lengthen with the load faster than residency pays for it: on the 100M-record index at ef = 128
+// (mean 2,524 visits) 6,144 entries at 6 wavefronts per CU (load 0.41) ran at 4.75-4.83 M QPS, against 4.18 M for
+// 5,120 at 7 (0.49, no query spilling in the timed batches), 3.35 M for 4,096 at 8 (0.62), 4.33 M for 7,168 at 5 and
+// 3.79 M for 8,192 at 4; at d = 200, ef = 250 on 50M ids (mean 4,200) 9,536 entries at 4 per CU (0.44) ran at 1.45 M
+// against 1.38 M for 7,488 at 5, 1.39 M for 8,192 at 4 and 1.21-1.24 M at 3 (profiles/r05/scale_cfg4_viscap*.jsonl,
+// scale_cfg5_viscap*.jsonl).  The few queries that outgrow the table spill in place to the L2 hash set.
+// SHINE_FAST_TABLE_POW2=1: the round-4 rule (the power of two 9/8 above the last call's worst query).
 uint32_t learned_max_table(const Scratch& S, uint32_t ef, uint32_t lds_per_cu) {
   if (!S.seen.p || !S.seen.p[3] || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
-  const uint64_t vmax = S.seen.p[4];
-  if (vmax == 0) return 0;
-  auto clampt = [&](uint32_t t) { return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, t})); };
-  const uint32_t p2 = clampt(pow2_at_least(static_cast<uint32_t>(std::min<uint64_t>(16384, vmax * 9 / 8))));
-  if (env_int("SHINE_FAST_TABLE_POW2", 0)) return p2;
-  const uint32_t want = static_cast<uint32_t>(std::min<uint64_t>(16384, vmax * 5 / 4));
-  const uint32_t np = clampt((want + 1023) / 1024 * 1024);
-  auto waves = [&](uint32_t t) { return lds_per_cu / search_fast_lds_bytes(t, ef, 4); };
-  return waves(np) > waves(p2) ? np : p2;
+  auto clampt = [&](uint64_t t) {
+    return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, static_cast<uint32_t>(std::min<uint64_t>(t, 16384))}));
+  };
+  if (env_int("SHINE_FAST_TABLE_POW2", 0)) {
+    const uint64_t vmax = S.seen.p[4];
+    return vmax ? clampt(pow2_at_least(static_cast<uint32_t>(std::min<uint64_t>(16384, vmax * 9 / 8)))) : 0;
+  }
+  const uint32_t nq = S.seen.p[6];  // (the mean as learned_mean_table reads it)
+  if (nq == 0 || nq >= (1u << 18) || S.seen.p[5] == 0) return 0;
+  const uint64_t mean = S.seen.p[5] / nq;
+  const uint64_t overhead = search_fast_lds_bytes(0, ef, 4);
+  auto waves = [&](uint64_t t) { return lds_per_cu / lds_alloc_bytes(search_fast_lds_bytes(static_cast<uint32_t>(t), ef, 4)); };
+  auto largest_at = [&](uint64_t w) -> uint64_t {  // the largest multiple of 64 entries holding w wavefronts per CU
+    const uint64_t per = lds_per_cu / w / 1024 * 1024;
+    return per > overhead + 256 ? (per - overhead) / 4 / 64 * 64 : 0;
+  };
+  const uint64_t want = (mean * 20 / 9 + 63) / 64 * 64;  // load 0.45 at the mean query
+  const uint64_t w = std::max<uint64_t>(1, waves(want));
+  return clampt(std::max(want, largest_at(w)));
 }
 
 // The exact pass's learned table, with the in-place spill: just the previous call's worst query (eighths/8 × its
@@ -624,11 +636,14 @@ uint32_t learned_max_table(const Scratch& S, uint32_t ef, uint32_t lds_per_cu) {
 // 10.6 M), hence the floor.  No margin above the worst query: with 9/8 (rounds 3-4) a batch whose worst query visits
 // 3,851 nodes put the next call on its stream on 8,192 entries, and that one slow launch set the time of a 20-step run
 // (warmup 5: 3.19 M against 3.64 M QPS with 8/8; 200 steps: 3.74 M against 3.96 M, profiles/r05/k20_exact_eighths.jsonl)
-// — the few queries past the table's 7/8 load spill in place.  Without the spill: learned_table (1.625 ×).
-uint32_t learned_exact_table(const Scratch& S, uint32_t ef) {
+// — the few queries past the table's 7/8 load spill in place.  The worst query of the slot's recent calls on all its
+// streams (Replica::vmax_recent), as the fast table: one stream's last call flipped the 100M-record index's table
+// between 4,096 and 8,192 entries (exact 1.29 M against 1.46 M QPS, profiles/r05/scale_cfg4_rule.jsonl).  Without the
+// spill: learned_table (1.625 ×).
+uint32_t learned_exact_table(const Scratch& S, uint32_t ef, uint32_t recent_vmax) {
   if (!spill_enabled()) return learned_table(S);
   if (!S.seen.p || !S.seen.p[3] || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
-  const uint64_t vmax = S.seen.p[4];
+  const uint64_t vmax = std::max(S.seen.p[4], recent_vmax);
   if (vmax == 0) return 0;
   // at ef <= 32 the tables are small and a half-empty one probed faster than a fuller one (10.6 M against 9.7 M QPS
   // at ef = 32, profiles/r03/exact_learned_scan_floor.jsonl): the round-2 margin there
@@ -670,7 +685,7 @@ LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds
     return std::max(lo, std::min(hi, fit));
   };
   auto resident = [&](uint32_t t, uint32_t entry_bytes) {
-    return std::min<uint64_t>(target, lds_per_cu / search_fast_lds_bytes(t, ef, entry_bytes));
+    return std::min<uint64_t>(target, lds_per_cu / lds_alloc_bytes(search_fast_lds_bytes(t, ef, entry_bytes)));
   };
   // test hook: the id space the u16 entries are sized for, widened (SHINE_DEBUG_VIS_BITS=24 puts a small index's ids
   // through the full 15-bit remainders of 4,096-entry two-choice tables)
@@ -696,10 +711,11 @@ LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds
   if (force16 >= 1 && can16) sh.vis16 = kind16(t16);  // test hook: force the u16 entries
   sh.vis_cap = sh.vis16 ? t16 : t32;
   sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
-  if (sh.vis16) sh.vis16 = kind16(sh.vis_cap);  // a forced table size: the entries it allows (0: back to u32)
+  // a forced table size: the entries it allows (0: back to u32; u16 buckets need a power of two)
+  if (sh.vis16) sh.vis16 = (sh.vis_cap & (sh.vis_cap - 1)) == 0 ? kind16(sh.vis_cap) : 0u;
   if (force16 == 2 && bits <= log2u(sh.vis_cap) + 12) sh.vis16 = 2;  // test hook: two-choice
   sh.vis_bits = std::max(bits, log2u(sh.vis_cap) + 1);
-  const uint64_t need = search_fast_lds_bytes(sh.vis_cap, ef, sh.vis16 ? 2 : 4);
+  const uint64_t need = lds_alloc_bytes(search_fast_lds_bytes(sh.vis_cap, ef, sh.vis16 ? 2 : 4));
   const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(lds_per_cu / need));
   const uint32_t wpc = std::max<uint32_t>(1, std::min<uint32_t>({(nq + cus - 1) / cus, 16u, fit}));
   sh.cap = 0;
@@ -885,21 +901,21 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
       S.table_floor = std::max(S.table_floor, pow2_at_least(2 * S.last_table));
   }
   if (ef != S.last_ef) S.table_floor = 0;
+  if (ef != R.vmax_ef) {
+    for (uint32_t& v : R.vmax_recent) v = 0;
+    R.vmax_ef = ef;
+  }
+  if (ef == S.last_ef && S.seen.p && S.seen.p[3])  // the worst query of the stream's latest finished call
+    R.vmax_recent[R.vmax_pos++ % 32] = S.seen.p[4];
   // the fast pass sizes its table for the mean query when it can spill in place; the exact pass keeps the maximum
   // (its tables sized from the mean ran slower, profiles/r03/ab1_merge_spill_tables.jsonl)
-  const uint32_t learned = ef != S.last_ef ? 0 : learned_exact_table(S, ef);
-  // The fast table: sized for the previous call's mean query (mean-sized, spilling the rest) or its worst one
-  // (max-sized, 9/8 of it).  A spilled query's later visits are atomics on its HBM bitmap, and the spilled queries are
-  // the longest ones, which set their batch's time: where the max-sized table still holds the wavefronts one batch
-  // puts on a CU it is taken — on the 100M-record index at ef = 128, 8,192 entries ran at 3.41 M QPS against 2.36 M
-  // mean-sized (1.98 M against 1.26 M with one batch in flight, same residency; profiles/r04/
-  // diag100m_tables_inflight.jsonl) — else residency wins and the table is mean-sized: DEEP-shaped 10M at ef = 256 and
-  // batch 4,096 (16 wavefronts per CU wanted) ran at 3.0 M QPS mean-sized against 2.1 M with larger tables (profiles/
-  // r04/scale_cfg3_cfg5_10m_v2_floor.jsonl).  Bucketed u32 tables and HBM hash tables as the spill target were tried and
-  // were slower at both sizes (profiles/r04/*_reverted.jsonl).  SHINE_FAST_TABLE_MAX=0 / 1 forces either (tuning).
-  //   Only where a spill bitmap outgrows an XCD's 4 MiB L2: at 10M ids (1.25 MB bitmaps) the spills stay cheap and the
-  // mean-sized table's residency wins even with one batch (cfg5-shaped 10M at ef = 250: 1.82 M mean-sized against
-  // 1.59 M max-sized, profiles/r04/scale_cfg3_cfg5_10m_v6_maxtable.jsonl).
+  const uint32_t learned = ef != S.last_ef ? 0 : learned_exact_table(S, ef, R.recent_vmax());
+  // The fast table: sized for the previous call's mean query — the smallest power of two above 1.25x it (mean-sized,
+  // spilling the rest, where the spill bitmap stays in an XCD's 4 MiB L2: at 10M ids the mean-sized table's residency
+  // wins, cfg5-shaped 10M at ef = 250: 1.82 M against 1.59 M with the worst query's table, profiles/r04/
+  // scale_cfg3_cfg5_10m_v6_maxtable.jsonl) or, beyond L2, the u32 table of learned_max_table (load 0.45 at the mean,
+  // grown to its residency level), where it holds the wavefronts one batch puts on a CU.  SHINE_FAST_TABLE_MAX=0 / 1
+  // forces either (tuning).
   uint32_t learned_fast = 0, learned_mean = 0;
   if (ef == S.last_ef) {
     if (!spill_enabled()) {
@@ -907,10 +923,9 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     } else {
       const uint32_t mean_t = learned_mean_table(S), max_t = learned_max_table(S, ef, R.lds_per_cu);
       const uint64_t need = std::min<uint64_t>(16, (nq + R.cus - 1) / R.cus);
-      const bool max_fits = max_t && R.lds_per_cu / search_fast_lds_bytes(max_t, ef, 4) >= need;
-      // (the hash-table spill keeps a spilled query in L2 at any id space, but even so the longest queries spill and set
-      // their batches' times: cfg 4 at 100M ran at 3.39 M QPS mean-sized with hash spills against 4.00 M max-sized,
-      // profiles/r05/scale_cfg4_100m_hash_vs_bitmap.jsonl — the max-sized table stays where the bitmap outgrows L2)
+      const bool max_fits = max_t && R.lds_per_cu / lds_alloc_bytes(search_fast_lds_bytes(max_t, ef, 4)) >= need;
+      // (the mean-sized power of two at 100M ids: 4,096 entries, load 0.62 at the mean, 3.39 M QPS, profiles/r05/
+      // scale_cfg4_100m_hash_vs_bitmap.jsonl)
       const bool beyond_l2 = 4ull * h->words_per_slot > kXcdL2Bytes;
       const int64_t force = env_int("SHINE_FAST_TABLE_MAX", -1);
       learned_fast = (force == 1 || (force < 0 && max_fits && beyond_l2)) ? max_t : mean_t;

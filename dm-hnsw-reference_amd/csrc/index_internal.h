@@ -156,6 +156,15 @@ struct Replica {
   uint32_t cus = 256;                 // compute units of the device (hipDeviceProp_t, queried at open)
   uint32_t lds_per_cu = 160 * 1024;   // LDS bytes per CU
   uint32_t pad_node = 0;  // a node of this slot's own stripe (sharded) for the unconditional loads of empty slots
+  // the worst query's visits of the latest finished call on a stream, as seen at the slot's last 32 enqueues at
+  // `vmax_ef` on any of its streams: the learned tables size for the recent batches, not one stream's last
+  uint32_t vmax_recent[32] = {};
+  uint32_t vmax_pos = 0, vmax_ef = 0;
+  uint32_t recent_vmax() const {
+    uint32_t m = 0;
+    for (uint32_t v : vmax_recent) m = v > m ? v : m;
+    return m;
+  }
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   DevBuf<uint8_t> vec;

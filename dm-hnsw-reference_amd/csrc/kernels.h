@@ -161,6 +161,12 @@ inline uint32_t fast_list_regs(uint32_t ef) { return ef <= 64 ? 1 : ef <= 128 ? 
 inline size_t search_fast_lds_bytes(uint32_t vis_cap, uint32_t ef, uint32_t entry_bytes = 4) {
   return align16(static_cast<size_t>(entry_bytes) * vis_cap) + 64 * 4 * 2 + 8ull * (64 * fast_list_regs(ef) + 2);
 }
+// LDS a workgroup holds, for residency estimates: whole 1 KiB granules.  HIP's occupancy calculator rounds to 128 B,
+// but the measured rates follow granules of at least 512 B: on the 100M-record index at ef = 128, 6,400 u32 entries
+// (27,152 B: 6 wavefronts per CU by 128-byte rounding, 5 by 512) ran at 4.29 M QPS against 4.75-4.83 M for 6,144
+// (26,128 B, 6 either way) and 4.33 M for 7,168 (5 either way) (profiles/r05/scale_cfg4_viscap*.jsonl,
+// lds_occupancy.jsonl); 1 KiB keeps the sizing clear of the boundary either way.
+inline size_t lds_alloc_bytes(size_t bytes) { return (bytes + 1023) / 1024 * 1024; }
 
 // Device row layout of the vectors.  The reference's AVX2 kernels keep 8 accumulators: accumulator a sums the
 // elements i ≡ a (mod 8) of the 16-aligned prefix in increasing i (distance.hh:11-76).  A distance kernel lane
