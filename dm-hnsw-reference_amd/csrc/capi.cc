@@ -605,7 +605,7 @@ uint32_t learned_mean_table(const Scratch& S) {
 // against 1.38 M for 7,488 at 5, 1.39 M for 8,192 at 4 and 1.21-1.24 M at 3 (profiles/r05/scale_cfg4_viscap*.jsonl,
 // scale_cfg5_viscap*.jsonl).  The few queries that outgrow the table spill in place to the L2 hash set.
 // SHINE_FAST_TABLE_POW2=1: the round-4 rule (the power of two 9/8 above the last call's worst query).
-uint32_t learned_max_table(const Scratch& S, uint32_t ef, uint32_t lds_per_cu) {
+uint32_t learned_max_table(const Scratch& S, uint32_t ef, uint32_t lds_per_cu, uint32_t waves_wanted) {
   if (!S.seen.p || !S.seen.p[3] || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
   auto clampt = [&](uint64_t t) {
     return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, static_cast<uint32_t>(std::min<uint64_t>(t, 16384))}));
@@ -624,7 +624,8 @@ uint32_t learned_max_table(const Scratch& S, uint32_t ef, uint32_t lds_per_cu) {
     return per > overhead + 256 ? (per - overhead) / 4 / 64 * 64 : 0;
   };
   const uint64_t want = (mean * 20 / 9 + 63) / 64 * 64;  // load 0.45 at the mean query
-  const uint64_t w = std::max<uint64_t>(1, waves(want));
+  // (no more wavefronts per CU than two batches of this call's size put there: a small call takes a larger table)
+  const uint64_t w = std::max<uint64_t>(1, std::min<uint64_t>(waves(want), waves_wanted));
   return clampt(std::max(want, largest_at(w)));
 }
 
@@ -921,8 +922,9 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     if (!spill_enabled()) {
       learned_fast = learned;
     } else {
-      const uint32_t mean_t = learned_mean_table(S), max_t = learned_max_table(S, ef, R.lds_per_cu);
       const uint64_t need = std::min<uint64_t>(16, (nq + R.cus - 1) / R.cus);
+      const uint32_t mean_t = learned_mean_table(S),
+                     max_t = learned_max_table(S, ef, R.lds_per_cu, static_cast<uint32_t>(std::min<uint64_t>(16, 2 * need)));
       const bool max_fits = max_t && R.lds_per_cu / lds_alloc_bytes(search_fast_lds_bytes(max_t, ef, 4)) >= need;
       // (the mean-sized power of two at 100M ids: 4,096 entries, load 0.62 at the mean, 3.39 M QPS, profiles/r05/
       // scale_cfg4_100m_hash_vs_bitmap.jsonl)
@@ -954,9 +956,9 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
                        (pass != PASS_FAST && learned != 0 && sh.vis_cap == learned);
       if (env_int("SHINE_DEBUG_SHAPE", 0))  // diagnostics: the main pass's shape and what it was learned from
         std::fprintf(stderr, "shape: pass %d nq %u ef %u table %u vis16 %u grid %u learned %u vmax %u handed %u floor %u "
-                     "spill_hash %u\n",
+                     "spill_hash %u learned_fast %u\n",
                      pass, nq, ef, sh.vis_cap, sh.vis16, sh.grid, learned, S.seen.p[3] ? S.seen.p[4] : 0u, handed,
-                     S.table_floor, spill_hashed(h) ? spill_hash_entries(sh.vis_cap) : 0u);
+                     S.table_floor, spill_hashed(h) ? spill_hash_entries(sh.vis_cap) : 0u, learned_fast);
     }
     SearchArgs a{};
     a.g = dev_graph(h, R);

@@ -5,7 +5,7 @@ SpillSet; the id-space bitmap would be 8.5 MB, beyond an XCD's L2), chosen by th
 The records are 16-d (DEEP-shaped, GPU-generated) and the graph sparse (M = 8, efC = 24, the GPU batch builder) so the
 build and the dump images stay small; 64-entry LDS tables (SHINE_DEBUG_VISCAP) make every query spill.  Exact mode
 equals the oracle's knn on the dump bit for bit (ids in heap order, distances, counters); fast mode equals it on every
-tie-free query.
+tie-free query, with the forced tables and with the library's own learned u32 table for this id space.
 """
 import numpy as np
 import pytest
@@ -54,6 +54,19 @@ def test_spill_to_hash_at_27_bit_ids(gpu_available, monkeypatch, capfd):
                 out[mode] = idx.knn(q, k, ef)
                 err = capfd.readouterr().err
                 assert " spill_hash 16384" in err, err  # the library chose the hash-table spill target
+            # the library's own fast table at this id space (capi.cc learned_max_table: u32 entries, load 0.45 at the
+            # previous call's mean query, grown to its residency level) once a call has been seen
+            monkeypatch.delenv("SHINE_DEBUG_VISCAP")
+            monkeypatch.delenv("SHINE_DEBUG_VIS16")
+            idx.set_search_mode(L.MODE_FAST)
+            for _ in range(3):
+                capfd.readouterr()
+                out["learned"] = idx.knn(q, k, ef)
+            err = capfd.readouterr().err
+            shape = [ln for ln in err.splitlines() if ln.startswith("shape: pass 4")][-1].split()
+            table, vis16, learned = int(shape[shape.index("table") + 1]), int(shape[shape.index("vis16") + 1]), \
+                int(shape[shape.index("learned_fast") + 1])
+            assert vis16 == 0 and learned >= 1024 and table % 64 == 0, shape  # u32 entries, a learned size
         step("searched")
     ex, fa = out[L.MODE_EXACT], out[L.MODE_FAST]
     assert ex.stats["overflow_retries"] == 0 and (ex.qstats[:, L.QS_STATUS] == 0).all()
@@ -68,3 +81,9 @@ def test_spill_to_hash_at_27_bit_ids(gpu_available, monkeypatch, capfd):
     np.testing.assert_array_equal(fa.dists[clean].view(np.uint32), s_d[clean].view(np.uint32))
     np.testing.assert_array_equal(np.sort(fa.ids[clean], 1), np.sort(s_ids[clean], 1))
     np.testing.assert_array_equal(fa.qstats[clean][:, :5], ref_qs[clean][:, :5])
+    le = out["learned"]
+    clean = le.qstats[:, L.QS_TIES] == 0
+    assert clean.mean() >= 0.9 and (le.qstats[:, L.QS_STATUS] == 0).all()
+    np.testing.assert_array_equal(le.dists[clean].view(np.uint32), s_d[clean].view(np.uint32))
+    np.testing.assert_array_equal(np.sort(le.ids[clean], 1), np.sort(s_ids[clean], 1))
+    np.testing.assert_array_equal(le.qstats[clean][:, :5], ref_qs[clean][:, :5])
