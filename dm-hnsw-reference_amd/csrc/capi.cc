@@ -1478,6 +1478,7 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
                              ? 0xFFFFFFFFu
                              : static_cast<uint32_t>(std::min<int64_t>(chunk_env, 0x7FFFFFFF));
   std::vector<uint8_t> chunked(G, 0);
+  std::vector<uint32_t> csize(G, chunk);  // a slot's chunk size when its share is split
   // every slot's batch is staged through pinned host memory and enqueued before any wait
   for (uint32_t r = 0; r < G; ++r) {
     const uint32_t n = static_cast<uint32_t>(part[r].size());
@@ -1520,14 +1521,21 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     for (hipStream_t hs : R.hstreams) HIP_TRY(hipStreamWaitEvent(hs, R.hfork, 0));
     // each chunk is staged just before its launch (the first starts after one chunk's copy, not the whole call's) and
     // signals an event, so its results are copied out while later chunks still run (below)
-    const uint32_t n_chunks = (n + chunk - 1) / chunk;
+    // as many chunks on every host stream (the call ends when its longest stream does: 10,000 queries as ten chunks of
+    // 1,024 left two of the four streams a chunk behind), each near `chunk` queries
+    const uint32_t S = static_cast<uint32_t>(R.hstreams.size());
+    const uint32_t per_stream = std::max<uint32_t>(1, static_cast<uint32_t>((static_cast<uint64_t>(n) + S * static_cast<uint64_t>(chunk) / 2) /
+                                                                            (S * static_cast<uint64_t>(chunk))));
+    const uint32_t m_chunk = static_cast<uint32_t>((n + S * per_stream - 1) / (S * per_stream));
+    csize[r] = m_chunk;
+    const uint32_t n_chunks = (n + m_chunk - 1) / m_chunk;
     while (R.hchunk.size() < n_chunks) {
       hipEvent_t ev = nullptr;
       HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
       R.hchunk.push_back(ev);
     }
-    for (uint32_t c = 0, off = 0; off < n; ++c, off += chunk) {
-      const uint32_t m = std::min(chunk, n - off);
+    for (uint32_t c = 0, off = 0; off < n; ++c, off += m_chunk) {
+      const uint32_t m = std::min(m_chunk, n - off);
       hipStream_t hs = R.hstreams[c % R.hstreams.size()];
       stage(off, off + m);
       if (int rc = enqueue_search(h, R, dq + static_cast<size_t>(off) * d, m, k, ef, dids + static_cast<size_t>(off) * k,
@@ -1594,9 +1602,9 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     Replica& R = h->reps[r];
     HIP_TRY(hipSetDevice(R.device));
     if (chunked[r]) {  // chunk by chunk, in order, while the later ones run
-      for (uint32_t c = 0, off = 0; off < n; ++c, off += chunk) {
+      for (uint32_t c = 0, off = 0; off < n; ++c, off += csize[r]) {
         HIP_TRY(hipEventSynchronize(R.hchunk[c]));
-        collect(r, off, std::min(n, off + chunk));
+        collect(r, off, std::min(n, off + csize[r]));
       }
     }
     HIP_TRY(hipStreamSynchronize(R.stream));
