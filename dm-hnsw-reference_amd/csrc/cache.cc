@@ -7,9 +7,6 @@
 #include <algorithm>
 #include <cmath>
 #include <new>
-#ifndef SHINE_CACHE_PF
-#define SHINE_CACHE_PF 4
-#endif
 
 namespace shine {
 
@@ -87,6 +84,7 @@ RecordCache::RecordCache(uint32_t entries, uint64_t seed, uint32_t key_space)
   modB_ = FastMod(B_);
   modCT_ = FastMod(CT_);
   for (uint32_t n = 1; n <= kInPlace; ++n) mod_n_[n] = FastMod(n);
+  for (uint32_t i = 0; i < kAhead; ++i) push_draw(i);
   std::fill(key_of_.data(), key_of_.data() + entries, kInv);
   std::fill(dev_of_.data(), dev_of_.data() + entries, kInv);
 }
@@ -97,7 +95,7 @@ bool RecordCache::size_ok(uint32_t entries) {
   return entries > kCoolingBucketEntries * ct;
 }
 
-uint64_t RecordCache::rand() {
+uint64_t RecordCache::next_draw() {
   state_ += 0x9E3779B97F4A7C15ull;
   uint64_t z = state_;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -105,79 +103,106 @@ uint64_t RecordCache::rand() {
   return z ^ (z >> 31);
 }
 
+void RecordCache::push_draw(uint32_t slot) {
+  ring_[slot] = next_draw();
+  if (C_) __builtin_prefetch(brec(static_cast<uint32_t>(modB_(ring_[slot]))));
+}
+
+uint64_t RecordCache::rand() {
+  const uint64_t v = ring_[head_];
+  push_draw(head_);
+  head_ = head_ + 1 == kAhead ? 0u : head_ + 1;
+  return v;
+}
+
 uint32_t RecordCache::bucket_of(uint32_t key) const { return static_cast<uint32_t>(modB_(murmur64(key))); }
 uint32_t RecordCache::cool_of(uint32_t key) const { return static_cast<uint32_t>(modCT_(splitmix(key))); }
 
-uint32_t RecordCache::bfind(uint32_t b, uint32_t key) const {
+int RecordCache::bfind(uint32_t b, uint32_t key, Ent& e) const {
   const uint32_t* r = brec(b);
-  const uint32_t in = r[0] < kInPlace ? r[0] : kInPlace;
+  const uint32_t n = bcount(r), in = n < kInPlace ? n : kInPlace;
   for (uint32_t i = 0; i < in; ++i)
-    if (r[1 + 2 * i] == key) return r[2 + 2 * i];
-  if (r[0] > kInPlace) {
+    if (r[1 + 3 * i] == key) {
+      e = {key, r[2 + 3 * i], r[3 + 3 * i], ((r[0] >> (16 + i)) & 1u) != 0};
+      return static_cast<int>(i);
+    }
+  if (n > kInPlace) {
     const std::vector<uint32_t>& o = bover_.at(b);
-    for (size_t i = 0; i < o.size(); i += 2)
-      if (o[i] == key) return o[i + 1];
+    for (size_t i = 0; i < o.size(); i += 4)
+      if (o[i] == key) {
+        e = {key, o[i + 1], o[i + 2], o[i + 3] != 0};
+        return static_cast<int>(kInPlace + i / 4);
+      }
   }
-  return kInv;
+  return -1;
 }
 
 uint32_t RecordCache::slot_of(uint32_t key) const {
   if (C_ == 0 || key >= key_space_) return kInv;
-  return bfind(bucket_of(key), key);
+  Ent e;
+  return bfind(bucket_of(key), key, e) >= 0 ? e.slot : kInv;
 }
 
-void RecordCache::bget(uint32_t b, uint32_t i, uint32_t& key, uint32_t& slot) const {
+RecordCache::Ent RecordCache::bget(uint32_t b, uint32_t i) const {
+  const uint32_t* r = brec(b);
+  if (i < kInPlace) return {r[1 + 3 * i], r[2 + 3 * i], r[3 + 3 * i], ((r[0] >> (16 + i)) & 1u) != 0};
+  const uint32_t* o = bover_.at(b).data() + 4 * (i - kInPlace);
+  return {o[0], o[1], o[2], o[3] != 0};
+}
+
+void RecordCache::bset_cool(uint32_t b, uint32_t i, bool cool) {
   if (i < kInPlace) {
-    key = brec(b)[1 + 2 * i];
-    slot = brec(b)[2 + 2 * i];
-    return;
+    uint32_t* r = brec(b);
+    r[0] = cool ? r[0] | (1u << (16 + i)) : r[0] & ~(1u << (16 + i));
+  } else {
+    bover_[b][4 * (i - kInPlace) + 3] = cool ? 1u : 0u;
   }
-  const std::vector<uint32_t>& o = bover_.at(b);
-  key = o[2 * (i - kInPlace)];
-  slot = o[2 * (i - kInPlace) + 1];
 }
 
-void RecordCache::bpush(uint32_t b, uint32_t key, uint32_t slot) {
+void RecordCache::bpush(uint32_t b, uint32_t key, uint32_t slot, uint32_t dev) {
   uint32_t* r = brec(b);
-  if (r[0] < kInPlace) {
-    r[1 + 2 * r[0]] = key;
-    r[2 + 2 * r[0]] = slot;
+  const uint32_t n = bcount(r);
+  if (n < kInPlace) {
+    r[1 + 3 * n] = key;
+    r[2 + 3 * n] = slot;
+    r[3 + 3 * n] = dev;
+    r[0] &= ~(1u << (16 + n));
   } else {
     auto& o = bover_[b];
-    o.push_back(key);
-    o.push_back(slot);
+    o.insert(o.end(), {key, slot, dev, 0u});
   }
   ++r[0];
 }
 
-// remove key from bucket b, keeping the others in order (vector::erase in the reference's Bucket)
-void RecordCache::berase(uint32_t b, uint32_t key) {
+void RecordCache::berase(uint32_t b, uint32_t i) {
   uint32_t* r = brec(b);
-  const uint32_t n = r[0];
-  const uint32_t in = n < kInPlace ? n : kInPlace;
-  uint32_t i = 0;
-  while (i < in && r[1 + 2 * i] != key) ++i;
+  const uint32_t n = bcount(r), in = n < kInPlace ? n : kInPlace;
   if (i < in) {
     for (uint32_t j = i; j + 1 < in; ++j) {
-      r[1 + 2 * j] = r[3 + 2 * j];
-      r[2 + 2 * j] = r[4 + 2 * j];
+      r[1 + 3 * j] = r[4 + 3 * j];
+      r[2 + 3 * j] = r[5 + 3 * j];
+      r[3 + 3 * j] = r[6 + 3 * j];
     }
+    const uint32_t bits = r[0] >> 16, low = bits & ((1u << i) - 1u), high = (bits >> (i + 1)) << i;
+    uint32_t nb = low | high;
     if (n > kInPlace) {  // the first entry past the in-place ones moves in
       auto it = bover_.find(b);
-      r[1 + 2 * (kInPlace - 1)] = it->second[0];
-      r[2 + 2 * (kInPlace - 1)] = it->second[1];
-      it->second.erase(it->second.begin(), it->second.begin() + 2);
+      const uint32_t* o = it->second.data();
+      r[1 + 3 * (kInPlace - 1)] = o[0];
+      r[2 + 3 * (kInPlace - 1)] = o[1];
+      r[3 + 3 * (kInPlace - 1)] = o[2];
+      nb = (nb & ~(1u << (kInPlace - 1))) | ((o[3] != 0 ? 1u : 0u) << (kInPlace - 1));
+      it->second.erase(it->second.begin(), it->second.begin() + 4);
       if (it->second.empty()) bover_.erase(it);
     }
+    r[0] = (n - 1) | ((nb & ((1u << kInPlace) - 1u)) << 16);
   } else {
     auto it = bover_.find(b);
-    auto& o = it->second;
-    size_t k = 0;
-    while (o[k] != key) k += 2;
-    o.erase(o.begin() + k, o.begin() + k + 2);
-    if (o.empty()) bover_.erase(it);
+    const size_t k = 4 * (i - kInPlace);
+    it->second.erase(it->second.begin() + k, it->second.begin() + k + 4);
+    if (it->second.empty()) bover_.erase(it);
+    r[0] = (r[0] & 0xFFFF0000u) | (n - 1);
   }
-  r[0] = n - 1;
 }
 
 bool RecordCache::ct_remove(uint32_t key) {  // cooling_table.hh:52-75
@@ -204,65 +229,58 @@ bool RecordCache::ct_insert(uint32_t key, uint32_t& victim) {  // cooling_table.
   return pushed;
 }
 
-// The draw i ahead of the stream without taking it (prefetch hints only).
-uint64_t RecordCache::peek(uint32_t i) const {
-  uint64_t z = state_ + 0x9E3779B97F4A7C15ull * i;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
+// The draw i ahead of the stream without taking it (1 <= i <= kAhead; prefetch hints only).
+uint64_t RecordCache::peek(uint32_t i) const { return ring_[(head_ + i - 1) % kAhead]; }
 
-// The next pick of the eviction scan, read ahead (its bucket's line was requested SHINE_CACHE_PF draws earlier): the
-// lines its step will touch — the entry's cooling flag, its cooling-table bucket and, when that bucket is full, the
-// hash bucket of the key it would push out — are requested now, so that the victim lookup, the scan's one dependent
-// miss, overlaps this step's.  A hint only: the step itself re-reads everything.
+// The next pick of the eviction scan, read ahead (its bucket's line was requested kAhead draws earlier): when the
+// step will start an entry cooling, its cooling-table bucket and — when that bucket is full — the hash bucket of the
+// key it would push out are requested now, so that the victim lookup, the scan's one dependent miss, overlaps this
+// step's.  A hint only: the step itself re-reads everything.
 void RecordCache::lookahead() const {
   const uint32_t* r = brec(static_cast<uint32_t>(modB_(peek(1))));
-  const uint32_t n = r[0];
+  const uint32_t n = bcount(r);
   if (n == 0 || n > kInPlace) return;
   const uint32_t i = static_cast<uint32_t>(mod_n_[n](peek(2)));
-  const uint32_t key = r[1 + 2 * i];
-  __builtin_prefetch(&cooling_[r[2 + 2 * i]]);
-  const uint32_t* c = &ct_[static_cast<size_t>(cool_of(key)) * kCW];
+  if ((r[0] >> (16 + i)) & 1u) return;  // already cooling: the step changes nothing
+  const uint32_t* c = &ct_[static_cast<size_t>(cool_of(r[1 + 3 * i])) * kCW];
   if (c[0] == kCoolingBucketEntries) __builtin_prefetch(brec(bucket_of(c[kCoolingBucketEntries])));
 }
 
-uint32_t RecordCache::evict() {  // cache.hh:232-311
+RecordCache::Victim RecordCache::evict() {  // cache.hh:232-311
   for (;;) {
-    const uint32_t b = static_cast<uint32_t>(modB_(rand()));
-    // the next pick's bucket is one or two draws ahead (an empty bucket takes no entry draw): both requested now, so
-    // the loop's dependent misses overlap
-    for (uint32_t a = 1; a <= SHINE_CACHE_PF; ++a) __builtin_prefetch(brec(static_cast<uint32_t>(modB_(peek(a)))));
-    const uint32_t n = brec(b)[0];
+    const uint32_t b = static_cast<uint32_t>(modB_(rand()));  // (its bucket was requested kAhead draws ago)
+    const uint32_t n = bcount(brec(b));
     if (n == 0) continue;
-    uint32_t key, slot;
-    bget(b, static_cast<uint32_t>(n <= kInPlace ? mod_n_[n](rand()) : rand() % n), key, slot);
+    const uint32_t i = static_cast<uint32_t>(n <= kInPlace ? mod_n_[n](rand()) : rand() % n);
+    const Ent e = bget(b, i);
     lookahead();
     uint32_t victim = kInv;
     bool has_victim = false;
-    if (!cooling_[slot]) {  // hot -> cooling; the table may push its oldest key out
-      has_victim = ct_insert(key, victim);
-      cooling_[slot] = 1;
-      if (flagged_) flagged_->push_back(slot);
+    if (!e.cool) {  // hot -> cooling; the table may push its oldest key out
+      has_victim = ct_insert(e.key, victim);
+      bset_cool(b, i, true);
+      cooling_[e.slot] = 1;
+      if (flagged_) flagged_->push_back(e.slot);
     }
     if (!has_victim) continue;
     const uint32_t vb = bucket_of(victim);
-    const uint32_t vslot = bfind(vb, victim);
-    if (vslot == kInv || !cooling_[vslot]) continue;  // rescued meanwhile: no eviction
-    berase(vb, victim);
-    cooling_[vslot] = 0;
+    Ent v;
+    const int vi = bfind(vb, victim, v);
+    if (vi < 0 || !v.cool) continue;  // rescued meanwhile: no eviction
+    berase(vb, static_cast<uint32_t>(vi));
+    cooling_[v.slot] = 0;
     ++evicted;
-    return vslot;
+    return {v.slot, v.dev};
   }
 }
 
 void RecordCache::insert(uint32_t key, uint32_t dev, std::vector<CacheUpdate>& updates) {  // cache.hh:147-203
-  const uint32_t slot = next_idx_ < C_ ? next_idx_++ : evict();
-  updates.push_back({slot, dev, dev_of_[slot]});
-  bpush(bucket_of(key), key, slot);
-  key_of_[slot] = key;
-  dev_of_[slot] = dev;
-  cooling_[slot] = 0;
+  const Victim v = next_idx_ < C_ ? Victim{next_idx_++, kInv} : evict();
+  updates.push_back({v.slot, dev, v.dev});
+  bpush(bucket_of(key), key, v.slot, dev);
+  key_of_[v.slot] = key;
+  dev_of_[v.slot] = dev;
+  cooling_[v.slot] = 0;
   ++admitted;
 }
 
@@ -308,29 +326,33 @@ void RecordCache::apply_call(std::vector<uint32_t> rescued_keys, std::vector<Cac
                              std::vector<CacheUpdate>& updates, std::vector<uint32_t>& flagged) {
   if (C_ == 0) return;
   flagged_ = &flagged;
-  std::sort(rescued_keys.begin(), rescued_keys.end());
+  if (!std::is_sorted(rescued_keys.begin(), rescued_keys.end())) std::sort(rescued_keys.begin(), rescued_keys.end());
   rescued_keys.erase(std::unique(rescued_keys.begin(), rescued_keys.end()), rescued_keys.end());
-  constexpr size_t kAhead = 8;  // lookups requested this many keys ahead (each one a likely miss)
+  constexpr size_t kLookAhead = 8;  // lookups requested this many keys ahead (each one a likely miss)
   const size_t nr = rescued_keys.size();
   for (size_t i = 0; i < nr; ++i) {  // cache.hh:128-132
-    if (i + kAhead < nr && rescued_keys[i + kAhead] < key_space_) {
-      const uint32_t k = rescued_keys[i + kAhead];
+    if (i + kLookAhead < nr && rescued_keys[i + kLookAhead] < key_space_) {
+      const uint32_t k = rescued_keys[i + kLookAhead];
       __builtin_prefetch(brec(bucket_of(k)));
       __builtin_prefetch(&ct_[static_cast<size_t>(cool_of(k)) * kCW]);
     }
     const uint32_t key = rescued_keys[i];
-    const uint32_t slot = slot_of(key);
-    if (slot != kInv && cooling_[slot] && ct_remove(key)) {
-      cooling_[slot] = 0;
-      flagged.push_back(slot);
+    if (key >= key_space_) continue;
+    const uint32_t b = bucket_of(key);
+    Ent e;
+    const int at = bfind(b, key, e);
+    if (at >= 0 && e.cool && ct_remove(key)) {
+      bset_cool(b, static_cast<uint32_t>(at), false);
+      cooling_[e.slot] = 0;
+      flagged.push_back(e.slot);
       ++rescued;
     }
   }
   sort_candidates(candidates);  // (query, key): a query offers a key once, so the order is total
   const size_t nc = candidates.size();
   for (size_t i = 0; i < nc; ++i) {
-    if (i + kAhead < nc && candidates[i + kAhead].key < key_space_)
-      __builtin_prefetch(brec(bucket_of(candidates[i + kAhead].key)));
+    if (i + kLookAhead < nc && candidates[i + kLookAhead].key < key_space_)
+      __builtin_prefetch(brec(bucket_of(candidates[i + kLookAhead].key)));
     const CacheCandidate& c = candidates[i];
     if (c.key >= key_space_ || contains(c.key)) continue;  // admitted by an earlier miss (cache.hh:171-179)
     if (c.always || !full() || c.coin) insert(c.key, c.dev_id, updates);

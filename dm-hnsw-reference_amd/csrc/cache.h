@@ -103,35 +103,52 @@ class RecordCache {
   uint64_t admitted = 0, evicted = 0, rescued = 0;
 
  private:
-  uint64_t rand();
-  uint64_t peek(uint32_t i) const;
-  uint32_t evict();  // cache.hh:232-311: frees one slot
+  uint64_t rand();                    // the next draw of the stream
+  uint64_t peek(uint32_t i) const;    // the draw i ahead (1 <= i <= kAhead), not taken
+  uint64_t next_draw();               // SplitMix64 step: the draw kAhead ahead of rand()'s
+  void push_draw(uint32_t slot);      // ring slot <- the next draw, its bucket requested
+  struct Victim {
+    uint32_t slot, dev;
+  };
+  Victim evict();  // cache.hh:232-311: frees one slot (and names the device id that leaves it)
   void lookahead() const;
   void insert(uint32_t key, uint32_t dev, std::vector<CacheUpdate>& updates);
   bool ct_remove(uint32_t key);
   bool ct_insert(uint32_t key, uint32_t& victim);
 
-  // Hash buckets (keys in insertion order, each with its arena slot) as flat 64-byte records, one cache line each:
-  // [count, key0, slot0, ..., key6, slot6, -].  A lookup, the eviction scan's random pick and an erase each touch one
-  // line: the key -> slot map needs no array of its own (a key-space array was a second random miss per step; the
-  // policy is a chain of dependent misses, ~1 us per admission into a full cache).  A bucket holds 7 entries in place
-  // and the rare rest (Poisson(1) occupancy: ~1e-5 of the buckets) in `bover_`, in order.  Cooling-table buckets:
-  // 8-word records [count, up to 6 keys newest first].
-  static constexpr uint32_t kBW = 16, kInPlace = 7, kCW = 8;
+  // Hash buckets as flat 64-byte records, one cache line each: [count | cooling bits << 16, (key, slot, device id) x 5]
+  // in insertion order.  A lookup, the eviction scan's random pick with its cooling flag, and an erase with the
+  // leaving device id each touch that one line: no key -> slot array, no slot -> flag or slot -> device read on the
+  // scan's path (the policy is a chain of dependent misses; each array read on it was one more).  A bucket holds 5
+  // entries in place and the rare rest (Poisson(1) occupancy: ~6e-4 of the buckets) in `bover_` as (key, slot,
+  // device, cooling) in order.  The slot arrays below are written on the way for the callers' per-slot reads.
+  // Cooling-table buckets: 8-word records [count, up to 6 keys newest first].
+  static constexpr uint32_t kBW = 16, kInPlace = 5, kCW = 8;
+  struct Ent {
+    uint32_t key, slot, dev;
+    bool cool;
+  };
   uint32_t* brec(uint32_t b) { return bk_.data() + static_cast<size_t>(b) * kBW; }
   const uint32_t* brec(uint32_t b) const { return bk_.data() + static_cast<size_t>(b) * kBW; }
+  static uint32_t bcount(const uint32_t* r) { return r[0] & 0xFFFFu; }
   uint32_t bucket_of(uint32_t key) const;
   uint32_t cool_of(uint32_t key) const;  // the key's cooling-table bucket
-  uint32_t bfind(uint32_t b, uint32_t key) const;  // the key's slot, or 0xFFFFFFFF
-  void bget(uint32_t b, uint32_t i, uint32_t& key, uint32_t& slot) const;
-  void bpush(uint32_t b, uint32_t key, uint32_t slot);
-  void berase(uint32_t b, uint32_t key);
+  int bfind(uint32_t b, uint32_t key, Ent& e) const;  // the key's position in bucket b (its entry in e), or -1
+  Ent bget(uint32_t b, uint32_t i) const;
+  void bset_cool(uint32_t b, uint32_t i, bool cool);
+  void bpush(uint32_t b, uint32_t key, uint32_t slot, uint32_t dev);
+  void berase(uint32_t b, uint32_t i);  // entry i out, the others in order (vector::erase in the reference's Bucket)
 
   uint32_t C_ = 0, B_ = 1, CT_ = 1, next_idx_ = 0, key_space_ = 0;
   FastMod modB_, modCT_, mod_n_[kInPlace + 1];  // % B_, % CT_, % n for in-place bucket sizes n
   uint64_t state_ = 0;
+  // the next kAhead draws, computed once each with their hash bucket (a draw picks a bucket, or an entry of one): each
+  // bucket is requested kAhead draws before the eviction scan may read it
+  static constexpr uint32_t kAhead = 8;
+  uint64_t ring_[kAhead] = {};
+  uint32_t head_ = 0;
   HugeArray<uint32_t> bk_;  // [B_][kBW] (page-aligned: records on cache-line boundaries)
-  std::unordered_map<uint32_t, std::vector<uint32_t>> bover_;  // bucket -> (key, slot) pairs past kInPlace
+  std::unordered_map<uint32_t, std::vector<uint32_t>> bover_;  // bucket -> (key, slot, dev, cool) past kInPlace
   HugeArray<uint32_t> ct_;                                     // [CT_][kCW]
   HugeArray<uint32_t> key_of_, dev_of_;                        // slot -> key / device id
   HugeArray<uint8_t> cooling_;                                 // slot -> cooling
