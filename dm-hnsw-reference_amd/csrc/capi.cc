@@ -1274,19 +1274,40 @@ namespace {
 // updates of a call are applied before it returns (the round-3/4 behaviour: the host waits for the replay).
 bool cache_lagged() { return env_int("SHINE_CACHE_LAG", 1) != 0; }
 
-int fetch_logs(shine_index* h, Replica& R) {
-  if (!R.logn.p) return 0;
-  HIP_TRY(hipSetDevice(R.device));
-  uint32_t cnt[2] = {0, 0};
-  HIP_TRY(hipMemcpy(cnt, R.logn.p, sizeof(cnt), hipMemcpyDeviceToHost));
-  const uint32_t n0 = std::min(cnt[0], R.clog_cap), n1 = std::min(cnt[1], R.rlog_cap);
-  const size_t b0 = R.pend_clog.size(), b1 = R.pend_rlog.size();
-  R.pend_clog.resize(b0 + n0);
-  R.pend_rlog.resize(b1 + n1);
-  if (n0) HIP_TRY(hipMemcpy(R.pend_clog.data() + b0, R.clog.p, n0 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-  if (n1) HIP_TRY(hipMemcpy(R.pend_rlog.data() + b1, R.rlog.p, n1 * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  R.pend_lost += (cnt[0] - n0) + (cnt[1] - n1);
-  HIP_TRY(hipMemsetAsync(R.logn.p, 0, 2 * sizeof(uint32_t), R.stream));  // before the slot's next search
+// Every slot's logs, the copies of all slots in flight together on their streams (counts first, then the logs they
+// size) into pinned memory: two waits in all instead of three blocking copies per slot (24 round trips at 8 slots)
+int fetch_logs(shine_index* h) {
+  for (Replica& R : h->reps) {
+    if (!R.logn.p) continue;
+    HIP_TRY(hipSetDevice(R.device));
+    if (int rc = R.logn_h.grow(2)) return rc;
+    HIP_TRY(hipMemcpyAsync(R.logn_h.p, R.logn.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, R.stream));
+  }
+  for (Replica& R : h->reps) {
+    if (!R.logn.p) continue;
+    HIP_TRY(hipSetDevice(R.device));
+    HIP_TRY(hipStreamSynchronize(R.stream));
+  }
+  for (Replica& R : h->reps) {
+    if (!R.logn.p) continue;
+    HIP_TRY(hipSetDevice(R.device));
+    const uint32_t n0 = std::min(R.logn_h.p[0], R.clog_cap), n1 = std::min(R.logn_h.p[1], R.rlog_cap);
+    if (int rc = R.clog_h.grow(std::max<uint32_t>(n0, 1))) return rc;
+    if (int rc = R.rlog_h.grow(std::max<uint32_t>(n1, 1))) return rc;
+    if (n0) HIP_TRY(hipMemcpyAsync(R.clog_h.p, R.clog.p, n0 * sizeof(unsigned long long), hipMemcpyDeviceToHost, R.stream));
+    if (n1) HIP_TRY(hipMemcpyAsync(R.rlog_h.p, R.rlog.p, n1 * sizeof(uint32_t), hipMemcpyDeviceToHost, R.stream));
+    HIP_TRY(hipMemsetAsync(R.logn.p, 0, 2 * sizeof(uint32_t), R.stream));  // before the slot's next search
+  }
+  for (Replica& R : h->reps) {
+    if (!R.logn.p) continue;
+    HIP_TRY(hipSetDevice(R.device));
+    HIP_TRY(hipStreamSynchronize(R.stream));
+    const uint32_t c0 = R.logn_h.p[0], c1 = R.logn_h.p[1];
+    const uint32_t n0 = std::min(c0, R.clog_cap), n1 = std::min(c1, R.rlog_cap);
+    R.pend_clog.insert(R.pend_clog.end(), R.clog_h.p, R.clog_h.p + n0);
+    R.pend_rlog.insert(R.pend_rlog.end(), R.rlog_h.p, R.rlog_h.p + n1);
+    R.pend_lost += (c0 - n0) + (c1 - n1);
+  }
   return 0;
 }
 
@@ -1294,12 +1315,22 @@ int fetch_logs(shine_index* h, Replica& R) {
 void replay(const shine_index* h, Replica& R, shine_stats* agg) {
   if (R.pend_clog.empty() && R.pend_rlog.empty()) return;
   const auto t0 = std::chrono::steady_clock::now();
-  std::vector<uint32_t> rescued_keys;  // hits on cooling entries, by device id
-  rescued_keys.reserve(R.pend_rlog.size());
-  for (uint32_t x : R.pend_rlog)
-    if (x < h->uid_of_dev.size()) rescued_keys.push_back(h->uid_of_dev[x]);
-  std::sort(rescued_keys.begin(), rescued_keys.end());
-  rescued_keys.erase(std::unique(rescued_keys.begin(), rescued_keys.end()), rescued_keys.end());
+  // hits on cooling entries (by device id, every hit logged): each key once, deduplicated in an open-addressed set over
+  // twice the log (a sort of the raw log was most of this step), then sorted by the engine
+  std::vector<uint32_t> rescued_keys;
+  {
+    uint32_t rmask = 63;
+    while (rmask + 1 < 2 * R.pend_rlog.size()) rmask = 2 * rmask + 1;
+    std::vector<uint32_t> seen(rmask + 1, kInvalid);
+    for (uint32_t x : R.pend_rlog) {
+      if (x >= h->uid_of_dev.size()) continue;
+      uint32_t q = (x * 0x9E3779B1u) & rmask;
+      while (seen[q] != kInvalid && seen[q] != x) q = (q + 1) & rmask;
+      if (seen[q] == x) continue;
+      seen[q] = x;
+      rescued_keys.push_back(h->uid_of_dev[x]);
+    }
+  }
   std::vector<CacheCandidate> cand(R.pend_clog.size());
   for (size_t i = 0; i < cand.size(); ++i) {
     const unsigned long long e = R.pend_clog[i];
@@ -1345,14 +1376,25 @@ void replay(const shine_index* h, Replica& R, shine_stats* agg) {
     fill.push_back(order[i]);
     fill.push_back(last_new[i]);
   }
-  std::vector<uint32_t> touched = std::move(flagged);
-  touched.insert(touched.end(), order.begin(), order.end());
-  std::sort(touched.begin(), touched.end());
-  touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
+  // the engine's final cooling state of every slot this replay changed, each slot once (an open-addressed set over
+  // twice the slots: a sort of the ~9K touched slots took a third of the updates' time)
   std::vector<uint32_t> cool;
-  for (uint32_t slot : touched) {  // the engine's final cooling state of every slot this replay changed
-    cool.push_back(slot);
-    cool.push_back(R.cache.cooling(slot) ? 1u : 0u);
+  {
+    const size_t nt = flagged.size() + order.size();
+    uint32_t smask = 63;
+    while (smask + 1 < 2 * nt) smask = 2 * smask + 1;
+    std::vector<uint32_t> seen(smask + 1, kInvalid);
+    cool.reserve(2 * nt);
+    auto add = [&](uint32_t slot) {
+      uint32_t q = (slot * 0x9E3779B1u) & smask;
+      while (seen[q] != kInvalid && seen[q] != slot) q = (q + 1) & smask;
+      if (seen[q] == slot) return;
+      seen[q] = slot;
+      cool.push_back(slot);
+      cool.push_back(R.cache.cooling(slot) ? 1u : 0u);
+    };
+    for (uint32_t slot : flagged) add(slot);
+    for (uint32_t slot : order) add(slot);
   }
   upd.clear();
   upd.insert(upd.end(), drop.begin(), drop.end());
@@ -1403,16 +1445,15 @@ int enqueue_update(shine_index* h, Replica& R) {
   return 0;
 }
 
-// replay on every slot with pending logs, one thread each (8 slots of a 10M-record index filling their caches took
-// ~0.3 s a call one after the other, profiles/r03/config_lines_cfg4_10m.jsonl)
+// replay on every slot with pending logs, one thread each from the handle's pool (8 slots of a 10M-record index filling
+// their caches took ~0.3 s a call one after the other, profiles/r03/config_lines_cfg4_10m.jsonl)
 void replay_all(shine_index* h, std::vector<shine_stats>& per) {
   const size_t G = h->reps.size();
   per.assign(G, shine_stats{});
-  std::vector<std::thread> th;
+  std::vector<size_t> todo;
   for (size_t r = 0; r < G; ++r)
-    if (!h->reps[r].pend_clog.empty() || !h->reps[r].pend_rlog.empty())
-      th.emplace_back([h, r, &per] { replay(h, h->reps[r], &per[r]); });
-  for (auto& t : th) t.join();
+    if (!h->reps[r].pend_clog.empty() || !h->reps[r].pend_rlog.empty()) todo.push_back(r);
+  h->pool.run(todo.size(), [&](size_t i) { replay(h, h->reps[todo[i]], &per[todo[i]]); });
 }
 
 // Queries per chunk of a large host-API call (the bench's batch) and the chunks in flight per slot: four, as the bench
@@ -1637,9 +1678,9 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
         HIP_TRY(hipDeviceSynchronize());
         R.dev_api_dirty = false;
       }
-      if (int e2 = fetch_logs(h, R)) return e2;
       ++R.dyn_call;  // the coin's call counter: one per host call
     }
+    if (int e2 = fetch_logs(h)) return e2;
     if (!lagged) {  // the updates before the call returns
       replay_all(h, per);
       for (uint32_t r = 0; r < G; ++r) {
@@ -1985,8 +2026,8 @@ int shine_cache_update(shine_index_t h) {
     HIP_TRY(hipSetDevice(R.device));
     HIP_TRY(hipDeviceSynchronize());
     R.dev_api_dirty = false;
-    if (int rc = fetch_logs(h, R)) return rc;
   }
+  if (int rc = fetch_logs(h)) return rc;
   std::vector<shine_stats> per;
   replay_all(h, per);  // every log not replayed yet (a pipelined call's, device-API searches')
   for (auto& R : h->reps) {
