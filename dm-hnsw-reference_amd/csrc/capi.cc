@@ -52,6 +52,7 @@ DevGraph dev_graph(const shine_index* h, const Replica& r) {
   g.div_shift = h->div_shift;
   if (h->cache_policy == SHINE_CACHE_DYNAMIC && g.sharded && r.cslot.p) {
     g.cslot = r.cslot.p;
+    g.cbits = r.cbits.p;
     g.cvec = r.cvec.p;
     g.cool = r.cool.p;
     g.clog = r.clog.p;
@@ -1278,7 +1279,7 @@ bool cache_lagged() { return env_int("SHINE_CACHE_LAG", 1) != 0; }
 // size) into pinned memory: two waits in all instead of three blocking copies per slot (24 round trips at 8 slots)
 int fetch_logs(shine_index* h) {
   for (Replica& R : h->reps) {
-    if (!R.logn.p) continue;
+    if (!R.logn.p || R.counts_inflight) continue;  // (knn_host enqueues the counts behind its searches)
     HIP_TRY(hipSetDevice(R.device));
     if (int rc = R.logn_h.grow(2)) return rc;
     HIP_TRY(hipMemcpyAsync(R.logn_h.p, R.logn.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, R.stream));
@@ -1307,6 +1308,7 @@ int fetch_logs(shine_index* h) {
     R.pend_clog.insert(R.pend_clog.end(), R.clog_h.p, R.clog_h.p + n0);
     R.pend_rlog.insert(R.pend_rlog.end(), R.rlog_h.p, R.rlog_h.p + n1);
     R.pend_lost += (c0 - n0) + (c1 - n1);
+    R.counts_inflight = false;
   }
   return 0;
 }
@@ -1436,9 +1438,9 @@ int enqueue_update(shine_index* h, Replica& R) {
   if (int rc = R.upd_host.grow(n)) return rc;
   std::memcpy(R.upd_host.p, R.upd_vec.data(), n * sizeof(uint32_t));
   HIP_TRY(hipMemcpyAsync(R.upd.p, R.upd_host.p, n * sizeof(uint32_t), hipMemcpyHostToDevice, R.stream));
-  hipError_t e = launch_cache_apply(R.upd.p, R.upd_drop, R.upd_fill, R.upd_cool, R.cslot.p, R.cvec.p, R.cool.p,
-                                    reinterpret_cast<const uint8_t*>(h->svec.view[R.slot].va), row_bytes(h->dim, h->elem),
-                                    R.stream);
+  hipError_t e = launch_cache_apply(R.upd.p, R.upd_drop, R.upd_fill, R.upd_cool, R.cslot.p, R.cbits.p, R.cvec.p,
+                                    R.cool.p, reinterpret_cast<const uint8_t*>(h->svec.view[R.slot].va),
+                                    row_bytes(h->dim, h->elem), R.stream);
   if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("cache update: ") + hipGetErrorString(e));
   R.upd_vec.clear();
   R.upd_drop = R.upd_fill = R.upd_cool = 0;
@@ -1550,6 +1552,11 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
       stage(0, n);
       if (int rc = enqueue_search(h, R, dq, n, k, ef, dids, dd, dqs, R.stream, true, access ? (*access)[r].p : nullptr))
         return drain(r + 1, rc);
+      if (h->cache_policy == SHINE_CACHE_DYNAMIC && !access && R.logn.p) {  // the log counts behind the searches, so
+        if (int rc = R.logn_h.grow(2)) return drain(r + 1, rc);          // they are home when the results are
+        HIP_TRY(hipMemcpyAsync(R.logn_h.p, R.logn.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, R.stream));
+        R.counts_inflight = true;
+      }
       continue;
     }
     // A large call runs as chunks of `chunk` queries kept in flight on the slot's host streams, as a serving loop keeps
@@ -1677,6 +1684,7 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
       if (!lagged || R.dev_api_dirty) {
         HIP_TRY(hipDeviceSynchronize());
         R.dev_api_dirty = false;
+        R.counts_inflight = false;  // counted again after every stream's searches
       }
       ++R.dyn_call;  // the coin's call counter: one per host call
     }
@@ -2001,12 +2009,14 @@ int shine_set_cache_policy(shine_index_t h, int policy, double ratio_percent, ui
     R.clog_cap = 1u << 22;
     R.rlog_cap = 1u << 22;  // every hit on a cooling entry is logged (duplicates too)
     int rc = 0;
-    if ((rc = R.cslot.grow(h->id_space)) || (rc = R.cvec.grow(entries * vrow)) || (rc = R.cool.grow(entries)) ||
+    if ((rc = R.cslot.grow(h->id_space)) || (rc = R.cbits.grow((h->id_space + 31) / 32)) ||
+        (rc = R.cvec.grow(entries * vrow)) || (rc = R.cool.grow(entries)) ||
         (rc = R.clog.grow(R.clog_cap)) || (rc = R.rlog.grow(R.rlog_cap)) || (rc = R.logn.grow(2))) {
       R.release_dynamic();
       return rc;
     }
     HIP_TRY(hipMemsetAsync(R.cslot.p, 0xFF, h->id_space * sizeof(uint32_t), R.stream));
+    HIP_TRY(hipMemsetAsync(R.cbits.p, 0, (h->id_space + 31) / 32 * sizeof(uint32_t), R.stream));
     HIP_TRY(hipMemsetAsync(R.cool.p, 0, entries * sizeof(uint32_t), R.stream));
     HIP_TRY(hipMemsetAsync(R.logn.p, 0, 2 * sizeof(uint32_t), R.stream));
     HIP_TRY(hipStreamSynchronize(R.stream));
@@ -2026,6 +2036,7 @@ int shine_cache_update(shine_index_t h) {
     HIP_TRY(hipSetDevice(R.device));
     HIP_TRY(hipDeviceSynchronize());
     R.dev_api_dirty = false;
+    R.counts_inflight = false;  // device-API searches may have logged since: counted again
   }
   if (int rc = fetch_logs(h)) return rc;
   std::vector<shine_stats> per;

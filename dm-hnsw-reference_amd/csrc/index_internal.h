@@ -187,7 +187,7 @@ struct Replica {
   hipEvent_t hfork = nullptr;
   DevBuf<unsigned long long> prof;  // SHINE_PHASE_PROFILE diagnostics
   // dynamic record cache (SHINE_CACHE_DYNAMIC): this GPU's arena, lookup table, logs and the host policy engine
-  DevBuf<uint32_t> cslot, cool, rlog, logn, upd;
+  DevBuf<uint32_t> cslot, cbits, cool, rlog, logn, upd;
   DevBuf<uint8_t> cvec;
   DevBuf<unsigned long long> clog;
   uint32_t clog_cap = 0, rlog_cap = 0, dyn_call = 0;
@@ -200,11 +200,12 @@ struct Replica {
   std::vector<uint32_t> upd_vec;
   uint32_t upd_drop = 0, upd_fill = 0, upd_cool = 0;
   HostBuf<uint32_t> logn_h, rlog_h;  // pinned landing of the log counts and logs (copies of all slots in flight at once)
+  bool counts_inflight = false;      // the counts' copy is enqueued behind this call's searches
   HostBuf<unsigned long long> clog_h;
   HostBuf<uint32_t> upd_host;
   bool dev_api_dirty = false;
   void release_dynamic() {
-    for (auto* b : {&cslot, &cool, &rlog, &logn, &upd}) b->release();
+    for (auto* b : {&cslot, &cbits, &cool, &rlog, &logn, &upd}) b->release();
     cvec.release();
     clog.release();
     upd_host.release();
@@ -212,6 +213,7 @@ struct Replica {
     rlog_h.release();
     clog_h.release();
     clog_cap = rlog_cap = dyn_call = 0;
+    counts_inflight = false;
     cache = RecordCache();
     pend_clog.clear();
     pend_rlog.clear();

@@ -414,11 +414,11 @@ __device__ __forceinline__ void load_byte_row(NbrBuf<D, E, P>& B, int p, const E
   }
 }
 
-// Off-stripe record x of a dynamic-cache view (DevGraph::cslot): its arena row when cached, else its xGMI row.
+// Off-stripe record x of a dynamic-cache view (DevGraph::cbits, cslot): its arena row when cached, else its xGMI row.
 __device__ __forceinline__ u32 read_class(const DevGraph& g, u32 x, u32 cached);
 template <int D, typename E>
 __device__ __forceinline__ const E* cached_row(const DevGraph& g, const E* row, u32 x) {
-  if (read_class(g, x, 0u) == 2u) {
+  if (read_class(g, x, 0u) == 2u && ((g.cbits[x >> 5] >> (x & 31)) & 1u)) {
     const u32 c = g.cslot[x];
     if (c != INV) return static_cast<const E*>(g.cvec) + static_cast<u64>(c) * kRowElems<D, E>;
   }
@@ -706,7 +706,7 @@ __device__ __forceinline__ void count_vec_reads(const SearchArgs& A, ReadCount& 
     u32 c = active ? read_class(A.g, x, A.g.cached_rows) : 0u;
     if constexpr (ACCT == 2) {
       if (c == 2u) {
-        const u32 slot = A.g.cslot[x];
+        const u32 slot = ((A.g.cbits[x >> 5] >> (x & 31)) & 1u) ? A.g.cslot[x] : INV;
         if (slot != INV) {
           c = 1u;
           // a hit on a cooling entry: its second chance (cache.hh:128-132) is the host's to give, so every such hit is
