@@ -1569,12 +1569,13 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     for (hipStream_t hs : R.hstreams) HIP_TRY(hipStreamWaitEvent(hs, R.hfork, 0));
     // each chunk is staged just before its launch (the first starts after one chunk's copy, not the whole call's) and
     // signals an event, so its results are copied out while later chunks still run (below)
-    // as many chunks on every host stream (the call ends when its longest stream does: 10,000 queries as ten chunks of
-    // 1,024 left two of the four streams a chunk behind), each near `chunk` queries
-    const uint32_t S = static_cast<uint32_t>(R.hstreams.size());
-    const uint32_t per_stream = std::max<uint32_t>(1, static_cast<uint32_t>((static_cast<uint64_t>(n) + S * static_cast<uint64_t>(chunk) / 2) /
-                                                                            (S * static_cast<uint64_t>(chunk))));
-    const uint32_t m_chunk = static_cast<uint32_t>((n + S * per_stream - 1) / (S * per_stream));
+    // chunks near `chunk` queries, and once there are at least as many as host streams, as many on every stream (the
+    // call ends when its longest stream does: 10,000 queries as ten chunks of 1,024 left two of the four streams a
+    // chunk behind); a call just past one chunk is not cut into launches too small to fill the GPU
+    const uint64_t S = R.hstreams.size();
+    uint64_t n_split = std::max<uint64_t>(1, (static_cast<uint64_t>(n) + chunk / 2) / chunk);
+    if (n_split >= S) n_split = (n_split + S / 2 - 1) / S * S;  // (a tie takes the larger chunks)
+    const uint32_t m_chunk = static_cast<uint32_t>((n + n_split - 1) / n_split);
     csize[r] = m_chunk;
     const uint32_t n_chunks = (n + m_chunk - 1) / m_chunk;
     while (R.hchunk.size() < n_chunks) {

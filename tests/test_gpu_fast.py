@@ -409,12 +409,13 @@ def test_host_api_splits_large_calls_into_chunks_in_flight(mode, gpu_available, 
     """shine_knn_batch with more queries than one chunk (capi.cc knn_host: chunks near 1,024 queries, as many on each
     of four host streams forked from and joined into the handle's stream) returns exactly what one launch over the
     whole call returns (SHINE_HOST_CHUNK=0), query by query: ids, distances and counters; exact mode also equals the
-    oracle.  4,500 queries: four chunks of 1,125 at the default, eight of 563 at 700, twelve of 375 at 300."""
+    oracle.  4,500 queries: four chunks of 1,125 at the default and at 700, sixteen of 282 at 300, two of 2,250 at
+    2,000."""
     base = D.deep_like(5000, seed=401, d=96)
     q = D.deep_like(4500, seed=402, d=96)
     dumps, _, _ = O.build(base, 16, 80, 0, 1, seed=7)
     out = {}
-    for chunk in ("0", "1024", "700", "300"):
+    for chunk in ("0", "1024", "700", "300", "2000"):
         monkeypatch.setenv("SHINE_HOST_CHUNK", chunk)
         with shine_amd.Index.from_buffers(dumps, 96, 16, 0, gpus=[0]) as idx:
             idx.set_search_mode(mode)
