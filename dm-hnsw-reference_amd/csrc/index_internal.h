@@ -290,9 +290,10 @@ class TaskPool {
   // f(i) for every i < n, on up to n - 1 pool threads and the caller's; returns when all are done
   void run(size_t n, const std::function<void(size_t)>& f) {
     if (n == 0) return;
-    while (th_.size() + 1 < n) th_.emplace_back([this] { worker(); });
     {
       std::lock_guard<std::mutex> lk(m_);
+      // a new worker starts from the current generation, so it joins this run, not a finished one
+      while (th_.size() + 1 < n) th_.emplace_back([this, g = gen_] { worker(g); });
       f_ = &f;
       n_ = n;
       next_ = 0;
@@ -307,8 +308,7 @@ class TaskPool {
   }
 
  private:
-  void worker() {
-    uint64_t seen = 0;
+  void worker(uint64_t seen) {
     std::unique_lock<std::mutex> lk(m_);
     for (;;) {
       go_.wait(lk, [&] { return stop_ || gen_ != seen; });
