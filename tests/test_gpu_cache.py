@@ -122,3 +122,40 @@ def test_dynamic_cache_recovers_after_the_zipf_head_moves(gpu_available):
     before, after, end = rates[11], rates[12], rates[23]
     assert after < before          # the head moved: the cached records no longer serve it
     assert end > after + 0.02      # and the cache follows it without a new warmup
+
+
+@pytest.mark.parametrize("lag", [True, False], ids=["pipelined", "synchronous"])
+def test_dynamic_cache_with_device_api_searches_between_calls(lag, gpu_available, monkeypatch):
+    """Device-API searches (shine_knn_batch_device on a caller stream) between host calls of a handle under the dynamic
+    policy: they read and log through the same arena, so the host waits for the device before it fetches the logs or
+    uploads an update (capi.cc dev_api_dirty) and shine_cache_update replays what they logged.  Every result equals a
+    cache-less handle's, and the cache still fills."""
+    import torch
+    monkeypatch.setenv("SHINE_CACHE_LAG", "1" if lag else "0")
+    base = D.deep_like(8000, seed=421, d=96)
+    pool = D.deep_like(600, seed=422, d=96)
+    dumps, _, _ = O.build(base, 12, 64, 0, 4, seed=8)
+    slots, k, ef, B = 2, 10, 48, 128
+    q, _, _ = D.zipf_query_mix(pool, 10 * B, 1.0, seed=4)
+    stream = torch.cuda.Stream()
+    with shine_amd.Index.from_buffers(dumps, 96, 12, 0, gpus=[0] * slots, placement="sharded") as plain, \
+            shine_amd.Index.from_buffers(dumps, 96, 12, 0, gpus=[0] * slots, placement="sharded") as idx:
+        idx.set_cache_policy(L.CACHE_DYNAMIC, ratio_percent=5.0, seed=13)
+        qd = torch.from_numpy(q).cuda()
+        ids_d = torch.empty((B, k), dtype=torch.int32, device="cuda")
+        for b in range(10):
+            qq = q[b * B:(b + 1) * B]
+            qid = np.arange(b * B, (b + 1) * B, dtype=np.uint32)
+            if b % 2:  # a device-API batch on slot b % slots, then the host API
+                idx.knn_device(qd[b * B:(b + 1) * B].data_ptr(), B, k, ef, ids_d.data_ptr(), None, None,
+                               stream=stream.cuda_stream, gpu_slot=b % slots)
+                stream.synchronize()
+                ref_slot = plain.knn(qq, k, ef, query_ids=np.full(B, b % slots, dtype=np.uint32))
+                np.testing.assert_array_equal(ids_d.cpu().numpy().view(np.uint32), ref_slot.ids)
+            r = idx.knn(qq, k, ef, query_ids=qid)
+            ref = plain.knn(qq, k, ef, query_ids=qid)
+            np.testing.assert_array_equal(r.ids, ref.ids)
+            assert (r.qstats[:, L.QS_STATUS] == 0).all()
+        idx.cache_update()  # the device-API searches' logs too
+        assert sum(len(idx.cache_keys(s)) for s in range(slots)) > 0
+        idx.release_stream(stream.cuda_stream)

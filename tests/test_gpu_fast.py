@@ -492,3 +492,25 @@ def test_hash_spill_overflow_hands_queries_on(gpu_available, monkeypatch):
             np.testing.assert_array_equal(r.qstats[:, :5], ref[2][:, :5])
         else:  # the light pass runs the exact heap kernel and writes ascending order
             _check_tie_free_exact(r, ref, 0.95)
+
+
+@pytest.mark.parametrize("mode", [L.MODE_FAST, L.MODE_EXACT])
+def test_prepare_leaves_results_and_stats_unchanged(mode, gpu_available):
+    """shine_prepare (setup before a measured query phase: streams, scratch, staging, kernel code, by a search over
+    all-zero queries whose results are discarded) changes nothing a later call returns: ids, distances, counters."""
+    base = D.deep_like(3000, seed=431, d=96)
+    q = D.deep_like(2500, seed=432, d=96)
+    dumps, _, _ = O.build(base, 12, 64, 0, 1, seed=9)
+    out = []
+    for prep in (False, True):
+        with shine_amd.Index.from_buffers(dumps, 96, 12, 0, gpus=[0]) as idx:
+            idx.set_search_mode(mode)
+            if prep:
+                idx.prepare(q.shape[0], 10, 64)
+            out.append(idx.knn(q, 10, 64))
+    a, b = out
+    np.testing.assert_array_equal(a.ids, b.ids)
+    np.testing.assert_array_equal(a.dists.view(np.uint32), b.dists.view(np.uint32))
+    np.testing.assert_array_equal(a.qstats[:, :8], b.qstats[:, :8])
+    assert a.stats["processed"] == b.stats["processed"] == q.shape[0]
+    assert a.stats["distcomps"] == b.stats["distcomps"]
