@@ -1537,7 +1537,14 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     if (int rc = R.hids.grow(static_cast<size_t>(n) * k, kMapped)) return drain(r, rc);
     if (int rc = R.hd.grow(static_cast<size_t>(n) * k, kMapped)) return drain(r, rc);
     if (int rc = R.hqs.grow(static_cast<size_t>(n) * kQsWords + 8, kMapped)) return drain(r, rc);
+    // (the slot's share in call order from position lo on: one copy of the run instead of a copy per query)
+    const bool identity = n == nq || (n > 0 && part[r][n - 1] - part[r][0] == n - 1);
     auto stage = [&](uint32_t lo, uint32_t hi) {  // queries lo .. hi-1 of the slot into the staging
+      if (identity) {
+        std::memcpy(R.hq.p + static_cast<size_t>(lo) * d, queries + static_cast<size_t>(part[r][lo]) * d,
+                    static_cast<size_t>(hi - lo) * d * sizeof(float));
+        return;
+      }
       for (uint32_t j = lo; j < hi; ++j)
         std::memcpy(R.hq.p + static_cast<size_t>(j) * d, queries + static_cast<size_t>(part[r][j]) * d, d * sizeof(float));
     };
@@ -1618,10 +1625,21 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
   // results of the slot's queries lo .. hi-1 out of the staging into the caller's arrays, and their counters
   auto collect = [&](uint32_t r, uint32_t lo, uint32_t hi) {
     const Replica& R = h->reps[r];
+    const std::vector<uint32_t>& pr = part[r];
+    const bool run = hi > lo && pr[hi - 1] - pr[lo] == hi - 1 - lo;  // queries in call order: bulk copies
+    if (run) {
+      std::memcpy(out_ids + static_cast<size_t>(pr[lo]) * k, R.hids.p + static_cast<size_t>(lo) * k,
+                  static_cast<size_t>(hi - lo) * k * 4);
+      if (out_dists)
+        std::memcpy(out_dists + static_cast<size_t>(pr[lo]) * k, R.hd.p + static_cast<size_t>(lo) * k,
+                    static_cast<size_t>(hi - lo) * k * 4);
+    }
     for (size_t j = lo; j < hi; ++j) {
-      const uint32_t qi = part[r][j];
-      std::memcpy(out_ids + static_cast<size_t>(qi) * k, R.hids.p + j * k, k * 4);
-      if (out_dists) std::memcpy(out_dists + static_cast<size_t>(qi) * k, R.hd.p + j * k, k * 4);
+      const uint32_t qi = pr[j];
+      if (!run) {
+        std::memcpy(out_ids + static_cast<size_t>(qi) * k, R.hids.p + j * k, k * 4);
+        if (out_dists) std::memcpy(out_dists + static_cast<size_t>(qi) * k, R.hd.p + j * k, k * 4);
+      }
       const uint32_t* qs = R.hqs.p + j * kQsWords;
       if (qstats) std::memcpy(qstats + static_cast<size_t>(qi) * SHINE_QS_WORDS, qs, SHINE_QS_WORDS * 4);
       if (qs[SHINE_QS_STATUS] != 0 && rc == SHINE_OK)
