@@ -584,6 +584,13 @@ uint32_t learned_table(const Scratch& S) {
 // DEEP-shaped 10M index at ef = 256 a query visits 2.9K nodes on average but up to 7K (profiles/r02/
 // config_lines_cfg3_10m_final.jsonl), and a table sized for the maximum holds half the wavefronts per CU.  Never below
 // the floor a call that exhausted the spill bitmaps set.
+// The previous call's mean visited count per query (0: nothing to learn from; see learned_mean_table)
+uint32_t mean_visits(const Scratch& S) {
+  if (!S.seen.p || !S.seen.p[3] || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
+  const uint32_t nq = S.seen.p[6];
+  return nq == 0 || nq >= (1u << 18) ? 0u : S.seen.p[5] / nq;
+}
+
 uint32_t learned_mean_table(const Scratch& S) {
   // (the visited sum is a u32 word of per-query counts capped at 16,384: calls of fewer than 2^18 queries cannot wrap
   // it — 2^18 x 2^14 is 2^32; seen[6] is the queries of the call that wrote the sum, which need not be the last one
@@ -742,7 +749,8 @@ uint32_t bitmap_slot_cap(const shine_index* h) {
 // that (at least one per CU, at most what LDS shares and bitmap memory allow): its workgroups of a call with few
 // overflows exit at once, and a launch of thousands of them delays the stream's next batch (-7 % QPS at ef = 32).
 LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint32_t ef, int pass,
-                       uint32_t handed = 0xFFFFFFFFu, uint32_t learned = 0, uint32_t learned_mean = 0) {
+                       uint32_t handed = 0xFFFFFFFFu, uint32_t learned = 0, uint32_t learned_mean = 0,
+                       uint32_t mean_visits = 0) {
   LaunchShape sh{};
   const uint64_t top_bytes = align16(8ull * ef);
   const uint32_t cus = R.cus, lds = R.lds_per_cu;
@@ -806,6 +814,27 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
         sh.vis_cap = learned_mean;
         sh.vis16 = v16;
         wpc = w;
+      }
+    }
+    // Where spills go to the hash set beyond L2 (100M / 50M ids: u32 entries), the fast pass's table rule (learned_max_
+    // table): load 0.45 at the mean query, grown to the largest u32 table at the same wavefronts per CU, next_candidates
+    // keeping 5 · ef entries — taken only where it puts more wavefronts on a CU than the table above: 100M ids at
+    // ef = 128, 6,528 entries and 5 per CU against 8,192 and 4, 1.51 M against 1.42 M QPS; at 50M ids and ef = 250 it
+    // holds the same 3 per CU with less room for next_candidates and ran at 0.38 M against 0.41 M
+    // (profiles/r05/scale_cfg{4,5}_exact_rule.jsonl).
+    if (mean_visits && sh.vis16 == 0 && spill_enabled() && spill_hashed(h) && env_int("SHINE_EXACT_LOAD_RULE", 1)) {
+      const uint64_t fixed = top_bytes + align16(8ull * 5 * ef) + 512;
+      auto waves = [&](uint64_t t) {
+        return std::min<uint64_t>(want, lds / lds_alloc_bytes(fixed + align16(4ull * t)));
+      };
+      const uint64_t t0 = (static_cast<uint64_t>(mean_visits) * 20 / 9 + 63) / 64 * 64;
+      const uint64_t w = std::max<uint64_t>(1, waves(t0));
+      const uint64_t per = lds / w / 1024 * 1024;
+      const uint64_t t = per > fixed + 4096 ? std::min<uint64_t>(16384, (per - fixed) / 4 / 64 * 64) : 0;
+      if (t >= t0 && t >= 1024 && w > wpc) {
+        sh.vis_cap = static_cast<uint32_t>(t);
+        sh.vis16 = 0;
+        wpc = static_cast<uint32_t>(w);
       }
     }
     if (const char* e = std::getenv("SHINE_DEBUG_VISCAP")) {  // test hook
@@ -912,6 +941,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   // the fast pass sizes its table for the mean query when it can spill in place; the exact pass keeps the maximum
   // (its tables sized from the mean ran slower, profiles/r03/ab1_merge_spill_tables.jsonl)
   const uint32_t learned = ef != S.last_ef ? 0 : learned_exact_table(S, ef, R.recent_vmax());
+  const uint32_t mean_v = ef != S.last_ef ? 0 : mean_visits(S);
   // The fast table: sized for the previous call's mean query — the smallest power of two above 1.25x it (mean-sized,
   // spilling the rest, where the spill bitmap stays in an XCD's 4 MiB L2: at 10M ids the mean-sized table's residency
   // wins, cfg5-shaped 10M at ef = 250: 1.82 M against 1.59 M with the worst query's table, profiles/r04/
@@ -948,7 +978,8 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     const LaunchShape sh =
         pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu, h->id_space, learned_fast, handed > 0,
                                           elem_is_byte(h->elem))
-                          : pick_shape(h, R, nq, ef, pass, handed, learned, learned_mean);
+                          : pick_shape(h, R, nq, ef, pass, handed, learned, learned_mean,
+                                       i == 0 ? mean_v : 0u);
     if (i == 0) {
       S.last_table = sh.vis_cap;
       S.last_fast = pass == PASS_FAST;
