@@ -145,6 +145,46 @@ def check_same_index(dist, torch, info, world: int, rank: int, device: str):
     return every
 
 
+def rank_report(dist, torch, device: str, elapsed: float, queries: int, steps: int, world: int):
+    """What the job's record needs to explain itself before an 8-GPU node has run it: how many rank processes the
+    collective saw (an all-reduce of ones over the same group the timing's max-over-ranks uses: RCCL on GPUs, gloo in
+    the CPU test) and every rank's own rate (an all-gather of the ranks' timed wall times), so a slow or missing rank
+    is visible in the line rather than only in `value`."""
+    if not dist:
+        return 1, [{"rank": 0, "value": queries / elapsed, "ms_per_step": elapsed * 1e3 / steps}]
+    one = torch.ones(1, dtype=torch.float64, device=device)
+    dist.all_reduce(one)
+    mine = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    every = torch.empty(world, dtype=torch.float64, device=device)
+    dist.all_gather_into_tensor(every, mine)
+    per = [{"rank": r, "value": queries / t, "ms_per_step": t * 1e3 / steps} for r, t in enumerate(every.tolist())]
+    return int(round(one.item())), per
+
+
+def peer_access(torch):
+    """hipDeviceCanAccessPeer over every pair of the node's GPUs (torch.cuda.can_device_access_peer): the sharded
+    placement reads other GPUs' stripes as peer loads (include/shine_gpu.h SHINE_PLACE_SHARDED), so the line records
+    whether the node offers them.  None without a GPU (the CPU stub)."""
+    if torch is None or not torch.cuda.is_available():
+        return {"devices": 0, "can_access": None}
+    n = torch.cuda.device_count()
+    m = [[True if i == j else bool(torch.cuda.can_device_access_peer(i, j)) for j in range(n)] for i in range(n)]
+    return {"devices": n, "can_access": m, "all_pairs": all(all(r) for r in m)}
+
+
+def attach_sharded_leg(a, world: int, out: dict):
+    """The sharded leg after the replica measurement, reported under `sharded`; the replica line is this run's `value`,
+    so a failing or hung child (it has never run on more than one physical GPU of this pool) is reported there instead
+    of losing the line."""
+    if not (a.sharded_leg == "on" or (a.sharded_leg == "auto" and world > 1)):
+        return
+    try:
+        out["sharded"] = sharded_leg(a, world)
+    except (SystemExit, Exception) as e:
+        log(f"sharded leg failed: {e}")
+        out["sharded"] = {"error": str(e)}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -262,7 +302,7 @@ def sharded_leg(a, world: int):
     t0 = time.time()
     r = child_json(cmd, env=env, timeout=float(os.environ.get("SHINE_SHARDED_LEG_TIMEOUT", "480")))
     keys = ("value", "ms_per_step", "n_gpus", "gpu_slots", "recall_at_10", "search_mode", "scaling", "one_gpu_value",
-            "speedup_vs_one_gpu", "reads", "bounds", "config", "data", "stub")
+            "speedup_vs_one_gpu", "reads", "per_slot", "bounds", "config", "data", "stub")
     out = {k: r[k] for k in keys if k in r}
     out["wall_s"] = time.time() - t0
     return out
@@ -380,11 +420,12 @@ def main():
         if dist:
             dist.barrier()
         elapsed = max_over_ranks(t1 - t0, dist, "cuda")
+        elapsed_rank = t1 - t0
         kern_ms = [s.elapsed_time(e) for s, e in evs]
         span_ms = max(evs[0][0].elapsed_time(e) for _, e in evs)  # first launch's start to the last one's end
         bytes_steps = [bq_batch[(a.warmup + i) % a.nbatches] for i in range(a.steps)]
-        return dict(elapsed=elapsed, kern_ms=kern_ms, span_ms=span_ms, bytes_steps=bytes_steps, recall=recall,
-                    qs=qs_h, ids=res, dists=res_d)
+        return dict(elapsed=elapsed, elapsed_rank=elapsed_rank, kern_ms=kern_ms, span_ms=span_ms,
+                    bytes_steps=bytes_steps, recall=recall, qs=qs_h, ids=res, dists=res_d)
 
     def host_legs(mode, ref_ids):
         """SURVEY §8d's query phase, host to host, K steps between barriers, batches in flight as above:
@@ -559,6 +600,7 @@ def main():
             traffic = pmc.get("hbm_bytes_per_launch")
             traffic_src = str(Path(a.pmc_json).relative_to(ROOT)) if Path(a.pmc_json).is_relative_to(ROOT) else a.pmc_json
 
+    ranks_seen, per_rank = rank_report(dist, torch, "cuda", head["elapsed_rank"], a.steps * a.batch, a.steps, world)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         cpu = cpu_baseline(paths, q, a, gt, runs["exact"]["ids"] if "exact" in runs else None)
@@ -570,6 +612,9 @@ def main():
             "value": total_q / elapsed,
             "unit": "queries/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,
+            "per_rank": per_rank,
+            "peer_access": peer_access(torch),
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": elapsed * 1e3 / a.steps,
@@ -615,16 +660,9 @@ def main():
     if dist:
         dist.destroy_process_group()
     if rank == 0:
-        if a.sharded_leg == "on" or (a.sharded_leg == "auto" and world > 1):
-            del qd, ids, dists, qs
-            torch.cuda.empty_cache()
-            # the replica measurement above is this line's `value`: a failing sharded child (it has never run on
-            # more than one physical GPU of this pool) is reported in the line instead of losing the line
-            try:
-                out["sharded"] = sharded_leg(a, world)
-            except (SystemExit, Exception) as e:
-                log(f"sharded leg failed: {e}")
-                out["sharded"] = {"error": str(e)}
+        del qd, ids, dists, qs
+        torch.cuda.empty_cache()
+        attach_sharded_leg(a, world, out)
         print(json.dumps(out), flush=True)
 
 
@@ -636,23 +674,22 @@ def stub_rank(a):
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    dist = None
     if world > 1:
+        import torch.distributed as dist
         dist.init_process_group("gloo")
-        t = torch.ones(1)
-        dist.all_reduce(t)
-        seen = int(t.item())
         # the same entry-point check the GPU ranks run, over gloo, on a stand-in index description
         check_same_index(dist, torch, {"entry_uid": 7, "max_level": 3, "num_nodes": 1000}, world, rank, "cpu")
+    # the same per-rank report as the GPU ranks, on a stand-in timing (rank r "took" 1 + r/10 s)
+    seen, per_rank = rank_report(dist, torch, "cpu", 1.0 + rank / 10, a.steps * a.batch, a.steps, world)
+    if dist:
         dist.destroy_process_group()
-    else:
-        seen = 1
     if rank != 0:
         return
     out = {"metric": "QPS at recall@10>=0.95, SIFT1M d=128 batch=1024", "value": 0.0, "unit": "queries/s",
-           "n_gpus": world, "ranks_seen": seen, "stub": True, "scaling": "weak",
-           "config": {"parallelism": f"replica{world}"}}
-    if a.sharded_leg == "on" or (a.sharded_leg == "auto" and world > 1):
-        out["sharded"] = sharded_leg(a, world)
+           "n_gpus": world, "ranks_seen": seen, "per_rank": per_rank, "peer_access": peer_access(None), "stub": True,
+           "scaling": "weak", "config": {"parallelism": f"replica{world}"}}
+    attach_sharded_leg(a, world, out)
     print(json.dumps(out), flush=True)
 
 
@@ -677,7 +714,12 @@ def run_sharded(a):
     if int(os.environ.get("WORLD_SIZE", "1")) != 1:
         raise SystemExit("--placement sharded runs as one process driving every GPU slot (not under torchrun)")
     if os.environ.get("SHINE_BENCH_STUB"):
-        print(json.dumps({"value": 0.0, "n_gpus": a.gpus, "gpu_slots": a.slots or a.gpus, "stub": True}), flush=True)
+        if os.environ.get("SHINE_BENCH_STUB_FAIL_SHARDED"):  # CPU test: a sharded child that fails
+            raise SystemExit(3)
+        S = a.slots or a.gpus
+        print(json.dumps({"value": 0.0, "n_gpus": a.gpus, "gpu_slots": S, "stub": True,
+                          "per_slot": [{"slot": s, "gpu": s % max(1, a.gpus), "span_ms_per_step": None,
+                                        "reads": None} for s in range(S)]}), flush=True)
         return
     import torch
     import shine_amd
@@ -726,13 +768,21 @@ def run_sharded(a):
                    for b in range(nb)])
         streams.append(slot_streams[s])
 
-    def step(i):
+    def step(i, evs=None):
         b = i % nb
         for s in range(S):
             n = len(rows[b][s])
             if n:
+                st = streams[s][i % len(streams[s])]
+                if evs is not None:
+                    evs[s].append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+                    with torch.cuda.device(gpus[s]):
+                        evs[s][-1][0].record(st)
                 idx.knn_device(qd[s][b].data_ptr(), n, k, ef, ids[s][b].data_ptr(), None, qs[s][b].data_ptr(),
-                               stream=streams[s][i % len(streams[s])].cuda_stream, gpu_slot=s)
+                               stream=st.cuda_stream, gpu_slot=s)
+                if evs is not None:
+                    with torch.cuda.device(gpus[s]):
+                        evs[s][-1][1].record(st)
 
     def sync():
         for d in sorted(set(gpus)):
@@ -758,11 +808,24 @@ def run_sharded(a):
         for i in range(a.warmup):
             step(i)
         sync()
+        evs = [[] for _ in range(S)]
         t0 = time.perf_counter()
         for i in range(a.steps):
-            step(a.warmup + i)
+            step(a.warmup + i, evs)
         sync()
         el = time.perf_counter() - t0
+        # every slot's own GPU span over the K steps (its first launch's start to its last launch's end, HIP events on
+        # its streams) and its read classes (qstats words 8-11 per query it answered: vector / list reads over xGMI,
+        # vector / list reads served by its local copies)
+        per_slot = []
+        for s in range(S):
+            span = max(evs[s][0][0].elapsed_time(e) for _, e in evs[s]) if evs[s] else None
+            mine = np.concatenate([np.asarray(rows[b][s], dtype=np.int64) for b in range(nb)])
+            cls = st[mine][:, 8:12].astype(np.float64).mean(0) if mine.size else np.zeros(4)
+            per_slot.append({"slot": s, "gpu": gpus[s], "span_ms_per_step": span / a.steps if span else None,
+                             "queries_per_step": int(np.mean([len(rows[b][s]) for b in range(nb)])),
+                             "reads": {"xgmi_vec_per_query": cls[0], "xgmi_list_per_query": cls[1],
+                                       "cached_vec_per_query": cls[2], "cached_list_per_query": cls[3]}})
         algo = idx.algorithmic_bytes(st) / st.shape[0]
         remote = (st[:, 8].astype(np.float64) * dim * 4 + st[:, 9].astype(np.float64) * 4 * 2 * M).mean()
         vec_hits, vec_remote = int(st[:, 10].sum()), int(st[:, 8].sum())
@@ -793,6 +856,7 @@ def run_sharded(a):
                       "off_stripe_hit_rate": vec_hits / max(1, vec_hits + vec_remote),
                       "node_reads": node_reads, "cache_hits": vec_hits, "cache_misses": node_reads - vec_hits,
                       "off_stripe_record_hits": hits, "off_stripe_record_misses": misses},
+            "per_slot": per_slot,
             "bounds": {"hbm_qps": phys * HBM_PEAK_GBPS * 1e9 / algo,
                        "xgmi_qps": (phys * xgmi_in / remote) if phys > 1 and remote > 0 else None,
                        "note": "xgmi_qps: every GPU's off-stripe reads at 7 x 153 GB/s inbound; with repeated slots "

@@ -60,6 +60,8 @@ DevGraph dev_graph(const shine_index* h, const Replica& r) {
     g.rlog = r.rlog.p;
     g.clog_cap = r.clog_cap;
     g.rlog_cap = r.rlog_cap;
+    g.rlogged = r.rlogged.p;
+    g.dyn_epoch = r.log_epoch;
     g.dyn_full = r.cache.full() ? 1u : 0u;
     g.dyn_call = r.dyn_call;
     g.dyn_seed = h->cache_seed + r.slot;
@@ -110,6 +112,8 @@ void release_state(IndexState* h) {
     R.hd.release();
     R.hids.release();
     R.hqs.release();
+    R.hcnt.release();
+    R.hcnt_dev = nullptr;
     for (hipStream_t s : R.hstreams) (void)hipStreamDestroy(s);
     for (hipEvent_t e : R.hjoin) (void)hipEventDestroy(e);
     for (hipEvent_t e : R.hchunk) (void)hipEventDestroy(e);
@@ -553,9 +557,11 @@ bool spill_hashed(const shine_index* h) {
 uint32_t spill_hash_entries(uint32_t vis_cap) {
   return std::min<uint32_t>(kSpillHashMax, std::max<uint32_t>(16384, pow2_at_least(8 * std::max<uint32_t>(vis_cap, 1))));
 }
-// Words per spill / fallback slot: the id-space bitmap, or at least the largest hash table.
+// Words per spill / fallback slot: the id-space bitmap, or at least the largest hash table; a multiple of 4 words, so
+// that every slot starts 16-byte aligned (spill_release clears a hash table with 16-byte stores from the slot base).
 uint64_t slot_words(const shine_index* h) {
-  return spill_hashed(h) ? std::max<uint64_t>(h->words_per_slot, kSpillHashMax) : h->words_per_slot;
+  const uint64_t w = spill_hashed(h) ? std::max<uint64_t>(h->words_per_slot, kSpillHashMax) : h->words_per_slot;
+  return (w + 3) / 4 * 4;
 }
 
 // Fast mode: the sorted list lives in VGPRs, LDS holds only the visited table.  The table holds between pow2(40·ef)
@@ -898,7 +904,7 @@ int ensure_bitmaps(shine_index* h, Scratch& S, hipStream_t s, uint32_t slots) {
 // size of the list pass i hands on at [4 + i].  Everything stays on the device: asynchronous and still exact.
 int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, uint32_t k, uint32_t ef,
                    uint32_t* d_ids, float* d_dists, uint32_t* d_qs, hipStream_t s, bool timed,
-                   uint32_t* d_access = nullptr) {
+                   uint32_t* d_access = nullptr, uint32_t* d_call_out = nullptr) {
   Scratch& S = scratch_for(R, s);
   if (int rc = S.counter.grow(kCallWords)) return rc;
   if (S.ovf.n < 3ull * nq) HIP_TRY(hipStreamSynchronize(s));  // a reallocation must not pull the list from under
@@ -1064,6 +1070,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     } else {
       a.call_counters = S.counter.p;
       a.host_counts = S.seen_dev;
+      a.call_out = d_call_out;
     }
     hipError_t e = launch_search(h->dim, h->metric, h->elem, sh.grid, a, s);
     if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("search launch: ") + hipGetErrorString(e));
@@ -1329,6 +1336,7 @@ int fetch_logs(shine_index* h) {
     if (n0) HIP_TRY(hipMemcpyAsync(R.clog_h.p, R.clog.p, n0 * sizeof(unsigned long long), hipMemcpyDeviceToHost, R.stream));
     if (n1) HIP_TRY(hipMemcpyAsync(R.rlog_h.p, R.rlog.p, n1 * sizeof(uint32_t), hipMemcpyDeviceToHost, R.stream));
     HIP_TRY(hipMemsetAsync(R.logn.p, 0, 2 * sizeof(uint32_t), R.stream));  // before the slot's next search
+    ++R.log_epoch;  // searches enqueued from here on log into the emptied buffers: a new epoch
   }
   for (Replica& R : h->reps) {
     if (!R.logn.p) continue;
@@ -1462,6 +1470,9 @@ int enqueue_update(shine_index* h, Replica& R) {
   if (R.dev_api_dirty) {
     HIP_TRY(hipDeviceSynchronize());
     R.dev_api_dirty = false;
+    // a count copy enqueued behind this call's own searches (knn_host) may predate entries the device-API searches
+    // logged after it: the counts are copied again once the call's searches are done (fetch_logs)
+    R.counts_inflight = false;
   }
   const size_t n = R.upd_vec.size();
   if (R.upd.n < n || R.upd_host.n < n) HIP_TRY(hipStreamSynchronize(R.stream));
@@ -1470,7 +1481,7 @@ int enqueue_update(shine_index* h, Replica& R) {
   std::memcpy(R.upd_host.p, R.upd_vec.data(), n * sizeof(uint32_t));
   HIP_TRY(hipMemcpyAsync(R.upd.p, R.upd_host.p, n * sizeof(uint32_t), hipMemcpyHostToDevice, R.stream));
   hipError_t e = launch_cache_apply(R.upd.p, R.upd_drop, R.upd_fill, R.upd_cool, R.cslot.p, R.cbits.p, R.cvec.p,
-                                    R.cool.p, reinterpret_cast<const uint8_t*>(h->svec.view[R.slot].va),
+                                    R.cool.p, R.rlogged.p, reinterpret_cast<const uint8_t*>(h->svec.view[R.slot].va),
                                     row_bytes(h->dim, h->elem), R.stream);
   if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("cache update: ") + hipGetErrorString(e));
   R.upd_vec.clear();
@@ -1612,7 +1623,10 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     // chunk behind); a call just past one chunk is not cut into launches too small to fill the GPU
     const uint64_t S = R.hstreams.size();
     uint64_t n_split = std::max<uint64_t>(1, (static_cast<uint64_t>(n) + chunk / 2) / chunk);
-    if (n_split >= S) n_split = (n_split + S / 2 - 1) / S * S;  // (a tie takes the larger chunks)
+    if (n_split >= S) {  // the nearest multiple of S (a tie takes the larger chunks)
+      const uint64_t q = n_split / S, rem = n_split % S;
+      n_split = (q + (2 * rem > S ? 1 : 0)) * S;
+    }
     const uint32_t m_chunk = static_cast<uint32_t>((n + n_split - 1) / n_split);
     csize[r] = m_chunk;
     const uint32_t n_chunks = (n + m_chunk - 1) / m_chunk;
@@ -1621,12 +1635,22 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
       HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
       R.hchunk.push_back(ev);
     }
+    // every chunk's handed-on count lands in a word pair of its own (a stream's counter words belong to whichever of
+    // its calls finished last)
+    if (R.hcnt.n < 2ull * n_chunks) {
+      if (int rc = R.hcnt.grow(2ull * n_chunks, kMapped)) return drain(r, rc);
+      void* dp = nullptr;
+      HIP_TRY(hipHostGetDevicePointer(&dp, R.hcnt.p, 0));
+      R.hcnt_dev = static_cast<uint32_t*>(dp);
+    }
+    std::memset(R.hcnt.p, 0, 2ull * n_chunks * sizeof(uint32_t));
     for (uint32_t c = 0, off = 0; off < n; ++c, off += m_chunk) {
       const uint32_t m = std::min(m_chunk, n - off);
       hipStream_t hs = R.hstreams[c % R.hstreams.size()];
       stage(off, off + m);
       if (int rc = enqueue_search(h, R, dq + static_cast<size_t>(off) * d, m, k, ef, dids + static_cast<size_t>(off) * k,
-                                  dd + static_cast<size_t>(off) * k, dqs + static_cast<size_t>(off) * kQsWords, hs, false))
+                                  dd + static_cast<size_t>(off) * k, dqs + static_cast<size_t>(off) * kQsWords, hs, false,
+                                  nullptr, R.hcnt_dev + 2ull * c))
         return drain(r + 1, rc);  // (the slot's host streams drain with the device below)
       HIP_TRY(hipEventRecord(R.hchunk[c], hs));
     }
@@ -1703,6 +1727,8 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
       for (uint32_t c = 0, off = 0; off < n; ++c, off += csize[r]) {
         HIP_TRY(hipEventSynchronize(R.hchunk[c]));
         collect(r, off, std::min(n, off + csize[r]));
+        const volatile uint32_t* cc = R.hcnt.p + 2ull * c;
+        if (cc[1]) retries += cc[0];
       }
     }
     HIP_TRY(hipStreamSynchronize(R.stream));
@@ -1714,11 +1740,6 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     if (!chunked[r]) {
       const uint32_t* cnt = R.main.seen.p;  // written by the call's last pass (finish_call)
       retries += cnt[0] + cnt[1] + cnt[2];  // queries handed on by each pass
-    } else {  // chunks: the last chunk of every host stream (its counter words hold its own call only)
-      for (hipStream_t hs : R.hstreams) {
-        const uint32_t* cnt = scratch_for(R, hs).seen.p;
-        if (cnt && cnt[3]) retries += cnt[0] + cnt[1] + cnt[2];
-      }
     }
     if (env_int("SHINE_PHASE_PROFILE", 0) && R.prof.p) print_phase_profile(h, R);
   }
@@ -1790,19 +1811,37 @@ int shine_prepare(shine_index_t h, uint32_t nq, uint32_t k, uint32_t ef) {
   std::vector<float> q(n * h->dim, 0.f);
   std::vector<uint32_t> ids(n * k);
   const bool dynamic = h->cache_policy == SHINE_CACHE_DYNAMIC;
-  std::vector<uint32_t> calls;
-  for (const Replica& R : h->reps) calls.push_back(R.dyn_call);
-  if (int rc = knn_host(h, q.data(), nullptr, nq, k, ef, ids.data(), nullptr, nullptr, nullptr, nullptr)) return rc;
-  if (dynamic) {  // the setup searches leave the cache as it was: their logs dropped, the coin's call count restored
+  // The setup searches leave the cache as it was: the logs of earlier calls not replayed yet (a pipelined call's) are
+  // set aside, so that the setup call does not replay them with its statistics discarded, and put back after it;
+  // the setup's own logs are dropped and the coin's call count restored.
+  struct Stash {
+    std::vector<unsigned long long> clog;
+    std::vector<uint32_t> rlog;
+    uint64_t lost = 0;
+    uint32_t call = 0;
+  };
+  std::vector<Stash> stash(h->reps.size());
+  if (dynamic) {
     for (size_t r = 0; r < h->reps.size(); ++r) {
       Replica& R = h->reps[r];
-      R.pend_clog.clear();
-      R.pend_rlog.clear();
+      stash[r].clog.swap(R.pend_clog);
+      stash[r].rlog.swap(R.pend_rlog);
+      stash[r].lost = R.pend_lost;
+      stash[r].call = R.dyn_call;
       R.pend_lost = 0;
-      R.dyn_call = calls[r];
     }
   }
-  return SHINE_OK;
+  const int rc = knn_host(h, q.data(), nullptr, nq, k, ef, ids.data(), nullptr, nullptr, nullptr, nullptr);
+  if (dynamic) {
+    for (size_t r = 0; r < h->reps.size(); ++r) {
+      Replica& R = h->reps[r];
+      R.pend_clog.swap(stash[r].clog);
+      R.pend_rlog.swap(stash[r].rlog);
+      R.pend_lost = stash[r].lost;
+      R.dyn_call = stash[r].call;
+    }
+  }
+  return rc;
 }
 
 int shine_cache_warmup(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
@@ -2057,10 +2096,12 @@ int shine_set_cache_policy(shine_index_t h, int policy, double ratio_percent, ui
     HIP_TRY(hipDeviceSynchronize());
     R.release_dynamic();
     R.clog_cap = 1u << 22;
-    R.rlog_cap = 1u << 22;  // every hit on a cooling entry is logged (duplicates too)
+    // hits on cooling entries: each arena slot at most once per log epoch (kernels_impl.h count_vec_reads), and an
+    // epoch's slots change occupant at most once (the updates between calls): twice the arena holds every entry
+    R.rlog_cap = static_cast<uint32_t>(std::max<uint64_t>(4096, 2 * entries));
     int rc = 0;
     if ((rc = R.cslot.grow(h->id_space)) || (rc = R.cbits.grow((h->id_space + 31) / 32)) ||
-        (rc = R.cvec.grow(entries * vrow)) || (rc = R.cool.grow(entries)) ||
+        (rc = R.cvec.grow(entries * vrow)) || (rc = R.cool.grow(entries)) || (rc = R.rlogged.grow(entries)) ||
         (rc = R.clog.grow(R.clog_cap)) || (rc = R.rlog.grow(R.rlog_cap)) || (rc = R.logn.grow(2))) {
       R.release_dynamic();
       return rc;
@@ -2068,6 +2109,7 @@ int shine_set_cache_policy(shine_index_t h, int policy, double ratio_percent, ui
     HIP_TRY(hipMemsetAsync(R.cslot.p, 0xFF, h->id_space * sizeof(uint32_t), R.stream));
     HIP_TRY(hipMemsetAsync(R.cbits.p, 0, (h->id_space + 31) / 32 * sizeof(uint32_t), R.stream));
     HIP_TRY(hipMemsetAsync(R.cool.p, 0, entries * sizeof(uint32_t), R.stream));
+    HIP_TRY(hipMemsetAsync(R.rlogged.p, 0xFF, entries * sizeof(uint32_t), R.stream));
     HIP_TRY(hipMemsetAsync(R.logn.p, 0, 2 * sizeof(uint32_t), R.stream));
     HIP_TRY(hipStreamSynchronize(R.stream));
     R.cache = RecordCache(static_cast<uint32_t>(entries), seed + R.slot, h->inv_size);  // keys: uids < inv_size

@@ -184,13 +184,16 @@ struct Replica {
   std::vector<hipStream_t> hstreams;
   std::vector<hipEvent_t> hjoin;
   std::vector<hipEvent_t> hchunk;  // one per chunk of the current call: its results are in the staging
+  HostBuf<uint32_t> hcnt;          // per chunk of the current call (mapped): queries its passes handed on, written flag
+  uint32_t* hcnt_dev = nullptr;
   hipEvent_t hfork = nullptr;
   DevBuf<unsigned long long> prof;  // SHINE_PHASE_PROFILE diagnostics
   // dynamic record cache (SHINE_CACHE_DYNAMIC): this GPU's arena, lookup table, logs and the host policy engine
-  DevBuf<uint32_t> cslot, cbits, cool, rlog, logn, upd;
+  DevBuf<uint32_t> cslot, cbits, cool, rlog, rlogged, logn, upd;
   DevBuf<uint8_t> cvec;
   DevBuf<unsigned long long> clog;
   uint32_t clog_cap = 0, rlog_cap = 0, dyn_call = 0;
+  uint32_t log_epoch = 0;  // advanced every time the logs are fetched and zeroed (DevGraph::dyn_epoch)
   RecordCache cache;
   // the policy's pipeline (capi.cc): logs of past calls copied to the host and not replayed yet; the arena updates a
   // replay made, not uploaded yet; a device-API search ran on another stream since the last update
@@ -205,14 +208,14 @@ struct Replica {
   HostBuf<uint32_t> upd_host;
   bool dev_api_dirty = false;
   void release_dynamic() {
-    for (auto* b : {&cslot, &cbits, &cool, &rlog, &logn, &upd}) b->release();
+    for (auto* b : {&cslot, &cbits, &cool, &rlog, &rlogged, &logn, &upd}) b->release();
     cvec.release();
     clog.release();
     upd_host.release();
     logn_h.release();
     rlog_h.release();
     clog_h.release();
-    clog_cap = rlog_cap = dyn_call = 0;
+    clog_cap = rlog_cap = dyn_call = log_epoch = 0;
     counts_inflight = false;
     cache = RecordCache();
     pend_clog.clear();

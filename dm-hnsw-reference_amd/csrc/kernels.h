@@ -39,8 +39,10 @@ struct DevGraph {
   unsigned long long* clog;   // admission candidates: (query << 32) | x | always << 31 | coin << 63
   uint32_t* clog_n;           // [0] candidates logged (may exceed clog_cap: the overflow is counted, not stored);
                               // [1] hits on cooling entries logged
-  uint32_t* rlog;             // device ids of the hits on cooling entries
+  uint32_t* rlog;             // device ids of the hits on cooling entries, each arena slot once per log epoch
+  uint32_t* rlogged;          // [arena slots]: the log epoch in which the slot's hit was logged (reset when it is filled)
   uint32_t clog_cap, rlog_cap;
+  uint32_t dyn_epoch;         // log epoch: the logs' contents since the host last fetched and zeroed them
   uint32_t dyn_full;          // the cache was full when the call started: level-0 misses draw the coin
   uint32_t dyn_call;          // call counter (coin input)
   unsigned long long dyn_seed;
@@ -78,6 +80,9 @@ struct SearchArgs {
   uint32_t* host_counts;     // to finish copies words 4..6 to host_counts[0..2] (host memory), sets host_counts[3] = 1,
                              // copies words 3 and 8 to host_counts[4] and [5], the call's nq to [6], and zeroes the words for the next call
                              // on the stream (word 7 counts finished groups)
+  uint32_t* call_out;        // last pass (nullable): call_out[0] = the queries the call's passes handed on (words 4..6
+                             // summed), call_out[1] = 1 — a per-call copy (host_counts is the stream's, and a later call
+                             // on the stream may overwrite it before the host reads it)
   uint32_t* vis_max;         // every pass (nullable): the call's counter word 3, the most nodes any query marked
                              // visited (atomicMax per query) — sizes the next call's visited tables
   uint32_t* vis_sum;         // every pass (nullable): the call's counter word 8, the nodes its queries marked visited
@@ -251,8 +256,8 @@ hipError_t radix_sort_u32_pairs(void* temp, size_t* temp_bytes, const uint32_t* 
 // their arena slots and point cslot at them; set the cooling flags.  upd = [drop ids (n_drop) | (slot, id) pairs
 // (n_fill) | (slot, flag) pairs (n_cool)].
 hipError_t launch_cache_apply(const uint32_t* upd, uint32_t n_drop, uint32_t n_fill, uint32_t n_cool, uint32_t* cslot,
-                              uint32_t* cbits, uint8_t* cvec, uint32_t* cool, const uint8_t* vec, uint64_t row_bytes,
-                              hipStream_t s);
+                              uint32_t* cbits, uint8_t* cvec, uint32_t* cool, uint32_t* rlogged, const uint8_t* vec,
+                              uint64_t row_bytes, hipStream_t s);
 
 // Diagnostics: replay push / pop / push_k sequences through the device heap routines (one wavefront).
 hipError_t launch_heap_replay(int is_max, const int32_t* ops, const float* vals, const uint32_t* ids, uint32_t n_ops,

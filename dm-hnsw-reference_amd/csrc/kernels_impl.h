@@ -709,12 +709,17 @@ __device__ __forceinline__ void count_vec_reads(const SearchArgs& A, ReadCount& 
         const u32 slot = ((A.g.cbits[x >> 5] >> (x & 31)) & 1u) ? A.g.cslot[x] : INV;
         if (slot != INV) {
           c = 1u;
-          // a hit on a cooling entry: its second chance (cache.hh:128-132) is the host's to give, so every such hit is
-          // logged by device id and the flag is left as the host engine set it: the flags on the device always equal
-          // the engine's after its last update, which is what lets the updates trail the calls (capi.cc replay)
+          // a hit on a cooling entry: its second chance (cache.hh:128-132) is the host's to give, so the hit is logged
+          // by device id and the flag is left as the host engine set it: the flags on the device always equal the
+          // engine's after its last update, which is what lets the updates trail the calls (capi.cc replay).  The
+          // host takes each key once, so each slot logs once per log epoch (the plain read filters repeat hits
+          // before the exchange that decides): the log holds at most one entry per arena slot and cannot overflow
           if (A.g.cool[slot]) {
-            const u32 i = atomicAdd(&A.g.clog_n[1], 1u);
-            if (i < A.g.rlog_cap) A.g.rlog[i] = x;
+            const u32 ep = A.g.dyn_epoch;
+            if (A.g.rlogged[slot] != ep && atomicExch(&A.g.rlogged[slot], ep) != ep) {
+              const u32 i = atomicAdd(&A.g.clog_n[1], 1u);
+              if (i < A.g.rlog_cap) A.g.rlog[i] = x;
+            }
           }
         } else {
           const bool coin = admission_coin(A.g.dyn_seed, A.g.dyn_call, qi, x);
@@ -1212,6 +1217,11 @@ __device__ __forceinline__ void finish_call(const SearchArgs& A, int lane) {
   host[6] = A.nq;  // the call the sum belongs to (several calls may be in flight on the stream)
   host[7] = __atomic_load_n(&c[9], __ATOMIC_RELAXED);
   host[3] = 1u;
+  if (A.call_out) {
+    volatile u32* co = A.call_out;
+    co[0] = h0 + h1 + h2;
+    co[1] = 1u;
+  }
 #pragma unroll
   for (int i = 0; i < static_cast<int>(kCallWords); ++i) __atomic_store_n(&c[i], 0u, __ATOMIC_RELAXED);
 }

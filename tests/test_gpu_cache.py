@@ -159,3 +159,41 @@ def test_dynamic_cache_with_device_api_searches_between_calls(lag, gpu_available
         idx.cache_update()  # the device-API searches' logs too
         assert sum(len(idx.cache_keys(s)) for s in range(slots)) > 0
         idx.release_stream(stream.cuda_stream)
+
+
+def test_dynamic_cache_device_api_batch_in_flight_across_a_host_call(gpu_available, monkeypatch):
+    """A device-API batch still running on a caller stream when a pipelined host call starts: the host call
+    copies its log counts behind its own searches, the update it uploads drains the device first, and the counts are
+    then copied again, so nothing the device-API batch logged after the early copy is lost.  The same sequence with the
+    caller stream synchronized before every host call leaves the same cache contents, slot by slot."""
+    import torch
+    monkeypatch.setenv("SHINE_CACHE_LAG", "1")
+    base = D.deep_like(8000, seed=431, d=96)
+    pool = D.deep_like(600, seed=432, d=96)
+    dumps, _, _ = O.build(base, 12, 64, 0, 4, seed=8)
+    slots, k, ef, B = 2, 10, 48, 256
+    q, _, _ = D.zipf_query_mix(pool, 8 * B, 1.0, seed=5)
+    keys = {}
+    for sync in (True, False):
+        stream = torch.cuda.Stream()
+        with shine_amd.Index.from_buffers(dumps, 96, 12, 0, gpus=[0] * slots, placement="sharded") as idx:
+            idx.set_cache_policy(L.CACHE_DYNAMIC, ratio_percent=5.0, seed=17)
+            qd = torch.from_numpy(q).cuda()
+            ids_d = torch.empty((B, k), dtype=torch.int32, device="cuda")
+            for b in range(8):
+                qq = q[b * B:(b + 1) * B]
+                qid = np.arange(b * B, (b + 1) * B, dtype=np.uint32)
+                idx.knn_device(qd[b * B:(b + 1) * B].data_ptr(), B, k, ef, ids_d.data_ptr(), None, None,
+                               stream=stream.cuda_stream, gpu_slot=b % slots)
+                if sync:
+                    stream.synchronize()
+                r = idx.knn(qq, k, ef, query_ids=qid)
+                assert (r.qstats[:, L.QS_STATUS] == 0).all()
+                assert r.stats["cache_log_dropped"] == 0
+            stream.synchronize()
+            idx.cache_update()
+            keys[sync] = [np.asarray(idx.cache_keys(s)) for s in range(slots)]
+            idx.release_stream(stream.cuda_stream)
+    for s in range(slots):
+        assert keys[True][s].size > 0
+        np.testing.assert_array_equal(keys[False][s], keys[True][s])

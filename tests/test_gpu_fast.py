@@ -514,3 +514,47 @@ def test_prepare_leaves_results_and_stats_unchanged(mode, gpu_available):
     np.testing.assert_array_equal(a.qstats[:, :8], b.qstats[:, :8])
     assert a.stats["processed"] == b.stats["processed"] == q.shape[0]
     assert a.stats["distcomps"] == b.stats["distcomps"]
+
+
+@pytest.mark.parametrize("nq", [1100, 2600])
+def test_host_api_one_host_stream(nq, gpu_available, monkeypatch):
+    """SHINE_HOST_STREAMS=1: a slot share just past one chunk is not rounded to zero chunks (capi.cc
+    knn_host rounds the chunk count to the nearest multiple of the host streams; at one stream the count stands).
+    Results equal one launch over the whole call, query by query."""
+    base = D.deep_like(4000, seed=411, d=96)
+    q = D.deep_like(nq, seed=412, d=96)
+    dumps, _, _ = O.build(base, 16, 80, 0, 1, seed=7)
+    out = {}
+    for streams, chunk in (("4", "0"), ("1", "1024"), ("3", "300")):
+        monkeypatch.setenv("SHINE_HOST_STREAMS", streams)
+        monkeypatch.setenv("SHINE_HOST_CHUNK", chunk)
+        with shine_amd.Index.from_buffers(dumps, 96, 16, 0, gpus=[0]) as idx:
+            idx.set_search_mode(L.MODE_FAST)
+            out[(streams, chunk)] = idx.knn(q, 10, 64)
+    want = out[("4", "0")]
+    for r in out.values():
+        assert r.stats["processed"] == nq
+        np.testing.assert_array_equal(r.ids, want.ids)
+        np.testing.assert_array_equal(r.qstats[:, :5], want.qstats[:, :5])
+
+
+def test_host_api_counts_every_chunks_hand_ons(gpu_available, monkeypatch):
+    """overflow_retries of a chunked call sums every chunk's hand-ons (it counted the last chunk of each
+    host stream only).  With 256-entry tables and the in-place spill off, whether a query is handed on depends on that
+    query alone, so one launch and any chunking hand the same number on."""
+    base = D.deep_like(5000, seed=413, d=96)
+    q = D.deep_like(2500, seed=414, d=96)
+    dumps, _, _ = O.build(base, 16, 80, 0, 1, seed=7)
+    monkeypatch.setenv("SHINE_DEBUG_VISCAP", "256")
+    monkeypatch.setenv("SHINE_DEBUG_NO_SPILL", "1")
+    monkeypatch.setenv("SHINE_DEBUG_NO_LEARN", "1")
+    got = {}
+    for chunk in ("0", "300", "1024"):
+        monkeypatch.setenv("SHINE_HOST_CHUNK", chunk)
+        with shine_amd.Index.from_buffers(dumps, 96, 16, 0, gpus=[0]) as idx:
+            idx.set_search_mode(L.MODE_FAST)
+            r = idx.knn(q, 10, 64)
+            assert (r.qstats[:, L.QS_STATUS] == 0).all()
+            got[chunk] = r.stats["overflow_retries"]
+    assert got["0"] > 0, got
+    assert got["300"] == got["0"] and got["1024"] == got["0"], got
