@@ -108,19 +108,11 @@ void release_state(IndexState* h) {
     R.release_dynamic();
     R.prof.release();
     R.vec.release();
-    R.hq.release();
-    R.hd.release();
-    R.hids.release();
-    R.hqs.release();
-    R.hcnt.release();
-    R.hcnt_dev = nullptr;
+    for (auto& st : R.stages_free) st->release();
+    R.stages_free.clear();
     for (hipStream_t s : R.hstreams) (void)hipStreamDestroy(s);
-    for (hipEvent_t e : R.hjoin) (void)hipEventDestroy(e);
-    for (hipEvent_t e : R.hchunk) (void)hipEventDestroy(e);
-    R.hchunk.clear();
     if (R.hfork) (void)hipEventDestroy(R.hfork);
     R.hstreams.clear();
-    R.hjoin.clear();
     R.hfork = nullptr;
     if (R.ev0) (void)hipEventDestroy(R.ev0);
     if (R.ev1) (void)hipEventDestroy(R.ev1);
@@ -903,8 +895,8 @@ int ensure_bitmaps(shine_index* h, Scratch& S, hipStream_t s, uint32_t slots) {
 // Enqueue the pass chain on stream s (see PassKind).  Counter words of the call: queue head of pass i at [i],
 // size of the list pass i hands on at [4 + i].  Everything stays on the device: asynchronous and still exact.
 int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, uint32_t k, uint32_t ef,
-                   uint32_t* d_ids, float* d_dists, uint32_t* d_qs, hipStream_t s, bool timed,
-                   uint32_t* d_access = nullptr, uint32_t* d_call_out = nullptr) {
+                   uint32_t* d_ids, float* d_dists, uint32_t* d_qs, hipStream_t s, uint32_t* d_access = nullptr,
+                   uint32_t* d_call_out = nullptr) {
   Scratch& S = scratch_for(R, s);
   if (int rc = S.counter.grow(kCallWords)) return rc;
   if (S.ovf.n < 3ull * nq) HIP_TRY(hipStreamSynchronize(s));  // a reallocation must not pull the list from under
@@ -918,7 +910,6 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   // the counter words start at zero: left so by the last call's last pass, else (first call, a failed call) set here
   if (!S.counters_zero) HIP_TRY(hipMemsetAsync(S.counter.p, 0, kCallWords * sizeof(uint32_t), s));
   S.counters_zero = false;
-  if (timed) HIP_TRY(hipEventRecord(R.ev0, s));
   const int start = static_cast<int>(env_int("SHINE_DEBUG_START_MODE", 0));  // test hook: the fallback passes alone
   const bool fast_mode = h->search_mode == SHINE_MODE_FAST;
   const bool fast_kernel = fast_mode && ef <= kFastMaxEf && h->M0 <= 64;
@@ -1082,7 +1073,6 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
                                             ", vis16 " + std::to_string(sh.vis16) + "): " + hipGetErrorString(e));
     }
   }
-  if (timed) HIP_TRY(hipEventRecord(R.ev1, s));
   S.counters_zero = true;
   return 0;
 }
@@ -1183,7 +1173,7 @@ namespace shine {
 int search_enqueue(shine_index* h, uint32_t slot, const float* d_q, uint32_t nq, uint32_t k, uint32_t ef,
                    uint32_t* d_ids, float* d_dists, uint32_t* d_qs, hipStream_t s) {
   if (slot >= h->reps.size()) return set_error(SHINE_ERR_ARG, "gpu_slot out of range");
-  return enqueue_search(h, h->reps[slot], d_q, nq, k, ef, d_ids, d_dists, d_qs, s, false);
+  return enqueue_search(h, h->reps[slot], d_q, nq, k, ef, d_ids, d_dists, d_qs, s);
 }
 
 void index_release(shine_index* h) { release_index(h); }
@@ -1295,7 +1285,7 @@ int shine_knn_batch_device(shine_index_t h, uint32_t gpu_slot, const float* d_qu
     qs = S.qs.p;
   }
   if (h->cache_policy == SHINE_CACHE_DYNAMIC) R.dev_api_dirty = true;  // it reads the arena and logs into its buffers
-  return enqueue_search(h, R, d_queries, nq, k, ef, d_out_ids, d_out_dists, qs, s, false);
+  return enqueue_search(h, R, d_queries, nq, k, ef, d_out_ids, d_out_dists, qs, s);
 }
 
 }  // extern "C"
@@ -1505,9 +1495,9 @@ void replay_all(shine_index* h, std::vector<shine_stats>& per) {
 constexpr uint32_t kHostChunk = 1024;
 constexpr uint32_t kHostStreams = 4;
 
-// The slot's host streams and their events, created together on first use: streams created back to back take
-// consecutive hardware queues of HIP's round-robin, so four chunks in flight run on four queues (two batches sharing a
-// queue run back to back: DESIGN §4 "Hardware queues").
+// The slot's host streams, created together on first use: streams created back to back take consecutive hardware
+// queues of HIP's round-robin, so four chunks in flight run on four queues (two batches sharing a queue run back to
+// back: DESIGN §4 "Hardware queues").
 int ensure_host_streams(Replica& R) {
   if (!R.hstreams.empty()) return 0;
   const uint32_t n = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_HOST_STREAMS", kHostStreams)));
@@ -1515,20 +1505,90 @@ int ensure_host_streams(Replica& R) {
     hipStream_t s = nullptr;
     HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     R.hstreams.push_back(s);
-    hipEvent_t e = nullptr;
-    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    R.hjoin.push_back(e);
   }
   HIP_TRY(hipEventCreateWithFlags(&R.hfork, hipEventDisableTiming));
   return 0;
 }
 
-// shine_knn_batch with the handle locked.  access (nullable): per-slot device counters of record reads (warmup).
-int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k, uint32_t ef,
-             uint32_t* out_ids, float* out_dists, uint32_t* qstats, shine_stats* stats,
-             std::vector<DevBuf<uint32_t>>* access) {
+// A staging set of the slot's pool, large enough for n queries in chunks (a synchronous call gives it back before it
+// returns; an asynchronous one when it is waited for).
+int take_stage(Replica& R, uint32_t n, uint32_t k, uint32_t d, uint32_t n_chunks, std::unique_ptr<HostStage>& out) {
+  if (!R.stages_free.empty()) {
+    out = std::move(R.stages_free.back());
+    R.stages_free.pop_back();
+  } else {
+    out = std::make_unique<HostStage>();
+  }
+  HostStage& S = *out;
+  constexpr unsigned kMapped = hipHostMallocMapped | hipHostMallocPortable;
+  auto dev = [](void* host, auto** dp) -> hipError_t { return hipHostGetDevicePointer(reinterpret_cast<void**>(dp), host, 0); };
+  const size_t nq = std::max<uint32_t>(n, 1);
+  if (S.hq.n < nq * d) {
+    if (int rc = S.hq.grow(nq * d, kMapped)) return rc;
+    HIP_TRY(dev(S.hq.p, &S.dq));
+  }
+  if (S.hids.n < nq * k) {
+    if (int rc = S.hids.grow(nq * k, kMapped)) return rc;
+    HIP_TRY(dev(S.hids.p, &S.dids));
+  }
+  if (S.hd.n < nq * k) {
+    if (int rc = S.hd.grow(nq * k, kMapped)) return rc;
+    HIP_TRY(dev(S.hd.p, &S.dd));
+  }
+  if (S.hqs.n < nq * kQsWords + 8) {
+    if (int rc = S.hqs.grow(nq * kQsWords + 8, kMapped)) return rc;
+    HIP_TRY(dev(S.hqs.p, &S.dqs));
+  }
+  if (S.hcnt.n < 2ull * std::max<uint32_t>(n_chunks, 1)) {
+    if (int rc = S.hcnt.grow(2ull * std::max<uint32_t>(n_chunks, 1), kMapped)) return rc;
+    HIP_TRY(dev(S.hcnt.p, &S.hcnt_dev));
+  }
+  std::memset(S.hcnt.p, 0, S.hcnt.n * sizeof(uint32_t));
+  while (S.hchunk.size() < n_chunks) {  // timing events: the call's kernel_ms is its first start to its last chunk's end
+    hipEvent_t ev = nullptr;
+    HIP_TRY(hipEventCreate(&ev));
+    S.hchunk.push_back(ev);
+  }
+  if (!S.ev0) HIP_TRY(hipEventCreate(&S.ev0));
+  return 0;
+}
+
+void give_stage(Replica& R, std::unique_ptr<HostStage>& s) {
+  if (s) R.stages_free.push_back(std::move(s));
+}
+
+}  // namespace
+
+// One host-API call between its enqueue and its collection (shine_knn_batch runs both at once; shine_knn_batch_async
+// returns in between and shine_wait collects).
+struct shine_request {
+  shine_index* h = nullptr;
+  uint32_t nq = 0, k = 0;
+  uint32_t* out_ids = nullptr;
+  float* out_dists = nullptr;
+  uint32_t* qstats = nullptr;
+  std::vector<DevBuf<uint32_t>>* access = nullptr;
+  std::vector<std::vector<uint32_t>> part;           // [slot] the call's query positions answered there
+  std::vector<std::unique_ptr<HostStage>> stage;     // [slot] its staging (null: the slot has no queries)
+  std::vector<uint8_t> chunked;                      // [slot] 1: chunks on the host streams, 0: one launch on R.stream
+  std::vector<uint32_t> csize, nchunks;              // [slot] chunk size and count
+  bool dynamic = false, lagged = false;
+  std::vector<shine_stats> per;                      // the lagged replay's statistics
+  double replay_ms = 0;
+  int rc = SHINE_OK;                                 // an error already met (collected calls drain first)
+  bool collected = false;
+  shine_stats stats{};
+};
+
+namespace {
+
+// Enqueue a host-API call: route its queries, stage each slot's share in that slot's pinned mapped staging and launch
+// it, in chunks on the slot's host streams (SHINE_HOST_CHUNK, default 1,024 queries), or as one launch on the slot's
+// own stream where the dynamic cache logs the call or a warmup counts its reads.  Returns before any search finishes.
+int knn_enqueue(shine_index* h, shine_request& C, const float* queries, const uint32_t* query_ids, uint32_t ef) {
   const uint32_t G = static_cast<uint32_t>(h->reps.size());
   const size_t d = h->dim;
+  const uint32_t nq = C.nq, k = C.k;
   if (env_int("SHINE_DEBUG_VALIDATE", 0))
     if (int rc = validate_views(h)) return rc;
   // queries are split over the slots as compute nodes split them, by id (read_data.hh:57-58: id % num_clients ==
@@ -1536,19 +1596,18 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
   // their region instead
   std::vector<uint32_t> dest(nq);
   route_batch(h, queries, query_ids, nq, dest.data());
-  std::vector<std::vector<uint32_t>> part(G);
-  for (uint32_t i = 0; i < nq; ++i) part[dest[i]].push_back(i);
-  // the staging buffers below are written by plain host stores and may be regrown: nothing on a slot's stream may
-  // still read them (an earlier call that failed after enqueueing, or device-API work on the handle's stream)
-  for (uint32_t r = 0; r < G; ++r) {
-    if (part[r].empty()) continue;
-    HIP_TRY(hipSetDevice(h->reps[r].device));
-    HIP_TRY(hipStreamSynchronize(h->reps[r].stream));
-  }
+  C.part.assign(G, {});
+  for (uint32_t i = 0; i < nq; ++i) C.part[dest[i]].push_back(i);
+  C.stage.resize(G);
+  C.chunked.assign(G, 0);
+  C.csize.assign(G, 0);
+  C.nchunks.assign(G, 0);
+  C.dynamic = h->cache_policy == SHINE_CACHE_DYNAMIC && !C.access;
+  C.lagged = C.dynamic && cache_lagged();
   // on an error after the first enqueue, the slots already enqueued are drained before returning
   auto drain = [&](uint32_t upto, int rc) {
     for (uint32_t r = 0; r < upto; ++r) {
-      if (part[r].empty()) continue;
+      if (C.part[r].empty()) continue;
       (void)hipSetDevice(h->reps[r].device);
       (void)hipStreamSynchronize(h->reps[r].stream);
       for (hipStream_t hs : h->reps[r].hstreams) (void)hipStreamSynchronize(hs);
@@ -1557,146 +1616,126 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
   };
   // Calls of more than `chunk` queries on a slot are split into chunks kept in flight (SHINE_HOST_CHUNK, default
   // 1,024: the bench's batch; 0 = never split).  Not while the dynamic cache logs a call (its replay orders admissions
-  // by query within one launch) or a warmup counts reads.
+  // by query within one launch) or a warmup counts reads: those run as one launch on the slot's own stream.
   const int64_t chunk_env = env_int("SHINE_HOST_CHUNK", kHostChunk);
-  const uint32_t chunk = (chunk_env <= 0 || access || h->cache_policy == SHINE_CACHE_DYNAMIC)
-                             ? 0xFFFFFFFFu
-                             : static_cast<uint32_t>(std::min<int64_t>(chunk_env, 0x7FFFFFFF));
-  std::vector<uint8_t> chunked(G, 0);
-  std::vector<uint32_t> csize(G, chunk);  // a slot's chunk size when its share is split
-  // every slot's batch is staged through pinned host memory and enqueued before any wait
+  const bool own_stream = C.access || C.dynamic;
+  const uint32_t chunk = chunk_env <= 0 ? 0xFFFFFFFFu : static_cast<uint32_t>(std::min<int64_t>(chunk_env, 0x7FFFFFFF));
   for (uint32_t r = 0; r < G; ++r) {
-    const uint32_t n = static_cast<uint32_t>(part[r].size());
+    const uint32_t n = static_cast<uint32_t>(C.part[r].size());
     if (n == 0) continue;
     Replica& R = h->reps[r];
     HIP_TRY(hipSetDevice(R.device));
+    // chunks near `chunk` queries, and once there are at least as many as host streams, as many on every stream (the
+    // call ends when its longest stream does: 10,000 queries as ten chunks of 1,024 left two of the four streams a
+    // chunk behind); a call just past one chunk is not cut into launches too small to fill the GPU
+    uint32_t m_chunk = n, n_chunks = 1;
+    if (!own_stream) {
+      if (int rc = ensure_host_streams(R)) return drain(r, rc);
+      const uint64_t S = R.hstreams.size();
+      uint64_t n_split = n <= chunk ? 1 : std::max<uint64_t>(1, (static_cast<uint64_t>(n) + chunk / 2) / chunk);
+      if (n_split >= S) {  // the nearest multiple of S (a tie takes the larger chunks)
+        const uint64_t q = n_split / S, rem = n_split % S;
+        n_split = (q + (2 * rem > S ? 1 : 0)) * S;
+      }
+      m_chunk = static_cast<uint32_t>((n + n_split - 1) / n_split);
+      n_chunks = (n + m_chunk - 1) / m_chunk;
+    }
+    C.csize[r] = m_chunk;
+    C.nchunks[r] = n_chunks;
     // zero copy: the pinned staging is mapped into the GPU's address space; the kernels read the queries and write
     // ids, distances and counters over PCIe themselves.  Copy-engine transfers would add a cross-engine dependency
     // per batch (copy -> kernel -> copy) that held the host back until each kernel finished: 3.0 M against 6.1 M QPS
     // with four batches in flight (profiles/r02/host_leg_probe.jsonl)
-    constexpr unsigned kMapped = hipHostMallocMapped | hipHostMallocPortable;
-    if (int rc = R.hq.grow(n * d, kMapped)) return drain(r, rc);
-    if (int rc = R.hids.grow(static_cast<size_t>(n) * k, kMapped)) return drain(r, rc);
-    if (int rc = R.hd.grow(static_cast<size_t>(n) * k, kMapped)) return drain(r, rc);
-    if (int rc = R.hqs.grow(static_cast<size_t>(n) * kQsWords + 8, kMapped)) return drain(r, rc);
+    if (int rc = take_stage(R, n, k, static_cast<uint32_t>(d), n_chunks, C.stage[r])) return drain(r, rc);
+    HostStage& S = *C.stage[r];
+    const std::vector<uint32_t>& pr = C.part[r];
     // (the slot's share in call order from position lo on: one copy of the run instead of a copy per query)
-    const bool identity = n == nq || (n > 0 && part[r][n - 1] - part[r][0] == n - 1);
+    const bool identity = n == nq || pr[n - 1] - pr[0] == n - 1;
     auto stage = [&](uint32_t lo, uint32_t hi) {  // queries lo .. hi-1 of the slot into the staging
       if (identity) {
-        std::memcpy(R.hq.p + static_cast<size_t>(lo) * d, queries + static_cast<size_t>(part[r][lo]) * d,
+        std::memcpy(S.hq.p + static_cast<size_t>(lo) * d, queries + static_cast<size_t>(pr[lo]) * d,
                     static_cast<size_t>(hi - lo) * d * sizeof(float));
         return;
       }
       for (uint32_t j = lo; j < hi; ++j)
-        std::memcpy(R.hq.p + static_cast<size_t>(j) * d, queries + static_cast<size_t>(part[r][j]) * d, d * sizeof(float));
+        std::memcpy(S.hq.p + static_cast<size_t>(j) * d, queries + static_cast<size_t>(pr[j]) * d, d * sizeof(float));
     };
-    float *dq = nullptr, *dd = nullptr;
-    uint32_t *dids = nullptr, *dqs = nullptr;
-    hipError_t pe = hipHostGetDevicePointer(reinterpret_cast<void**>(&dq), R.hq.p, 0);
-    if (pe == hipSuccess) pe = hipHostGetDevicePointer(reinterpret_cast<void**>(&dids), R.hids.p, 0);
-    if (pe == hipSuccess) pe = hipHostGetDevicePointer(reinterpret_cast<void**>(&dd), R.hd.p, 0);
-    if (pe == hipSuccess) pe = hipHostGetDevicePointer(reinterpret_cast<void**>(&dqs), R.hqs.p, 0);
-    if (pe != hipSuccess) return drain(r, set_error(SHINE_ERR_HIP, std::string("hipHostGetDevicePointer: ") + hipGetErrorString(pe)));
-    if (n <= chunk) {
+    if (own_stream) {
       stage(0, n);
-      if (int rc = enqueue_search(h, R, dq, n, k, ef, dids, dd, dqs, R.stream, true, access ? (*access)[r].p : nullptr))
+      HIP_TRY(hipEventRecord(S.ev0, R.stream));
+      if (int rc = enqueue_search(h, R, S.dq, n, k, ef, S.dids, S.dd, S.dqs, R.stream, C.access ? (*C.access)[r].p : nullptr))
         return drain(r + 1, rc);
-      if (h->cache_policy == SHINE_CACHE_DYNAMIC && !access && R.logn.p) {  // the log counts behind the searches, so
-        if (int rc = R.logn_h.grow(2)) return drain(r + 1, rc);          // they are home when the results are
+      HIP_TRY(hipEventRecord(S.hchunk[0], R.stream));
+      if (C.dynamic && R.logn.p) {  // the log counts behind the searches, so they are home when the results are
+        if (int rc = R.logn_h.grow(2)) return drain(r + 1, rc);
         HIP_TRY(hipMemcpyAsync(R.logn_h.p, R.logn.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, R.stream));
         R.counts_inflight = true;
       }
       continue;
     }
-    // A large call runs as chunks of `chunk` queries kept in flight on the slot's host streams, as a serving loop keeps
-    // batches in flight (the last, longest queries of one chunk overlap the next chunks' first ones): forked from the
-    // handle's stream (after anything enqueued there, e.g. dynamic-cache updates) and joined back into it, so the
-    // waits below and the event span see the whole call.
-    if (int rc = ensure_host_streams(R)) return drain(r, rc);
-    HIP_TRY(hipEventRecord(R.ev0, R.stream));
+    // The chunks run on the slot's host streams, as a serving loop keeps batches in flight (the last, longest queries
+    // of one chunk overlap the next chunks' first ones), after anything enqueued on the slot's own stream before the
+    // call (the fork event).  Nothing joins them back: the call's chunk events are what its collection waits for, so
+    // calls enqueued back to back (shine_knn_batch_async) overlap as chunks of one call do.  Each chunk is staged
+    // just before its launch (the first starts after one chunk's copy, not the whole call's).
+    HIP_TRY(hipEventRecord(S.ev0, R.stream));
     HIP_TRY(hipEventRecord(R.hfork, R.stream));
     for (hipStream_t hs : R.hstreams) HIP_TRY(hipStreamWaitEvent(hs, R.hfork, 0));
-    // each chunk is staged just before its launch (the first starts after one chunk's copy, not the whole call's) and
-    // signals an event, so its results are copied out while later chunks still run (below)
-    // chunks near `chunk` queries, and once there are at least as many as host streams, as many on every stream (the
-    // call ends when its longest stream does: 10,000 queries as ten chunks of 1,024 left two of the four streams a
-    // chunk behind); a call just past one chunk is not cut into launches too small to fill the GPU
-    const uint64_t S = R.hstreams.size();
-    uint64_t n_split = std::max<uint64_t>(1, (static_cast<uint64_t>(n) + chunk / 2) / chunk);
-    if (n_split >= S) {  // the nearest multiple of S (a tie takes the larger chunks)
-      const uint64_t q = n_split / S, rem = n_split % S;
-      n_split = (q + (2 * rem > S ? 1 : 0)) * S;
-    }
-    const uint32_t m_chunk = static_cast<uint32_t>((n + n_split - 1) / n_split);
-    csize[r] = m_chunk;
-    const uint32_t n_chunks = (n + m_chunk - 1) / m_chunk;
-    while (R.hchunk.size() < n_chunks) {
-      hipEvent_t ev = nullptr;
-      HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-      R.hchunk.push_back(ev);
-    }
-    // every chunk's handed-on count lands in a word pair of its own (a stream's counter words belong to whichever of
-    // its calls finished last)
-    if (R.hcnt.n < 2ull * n_chunks) {
-      if (int rc = R.hcnt.grow(2ull * n_chunks, kMapped)) return drain(r, rc);
-      void* dp = nullptr;
-      HIP_TRY(hipHostGetDevicePointer(&dp, R.hcnt.p, 0));
-      R.hcnt_dev = static_cast<uint32_t*>(dp);
-    }
-    std::memset(R.hcnt.p, 0, 2ull * n_chunks * sizeof(uint32_t));
     for (uint32_t c = 0, off = 0; off < n; ++c, off += m_chunk) {
       const uint32_t m = std::min(m_chunk, n - off);
-      hipStream_t hs = R.hstreams[c % R.hstreams.size()];
+      hipStream_t hs = R.hstreams[R.hnext++ % R.hstreams.size()];
       stage(off, off + m);
-      if (int rc = enqueue_search(h, R, dq + static_cast<size_t>(off) * d, m, k, ef, dids + static_cast<size_t>(off) * k,
-                                  dd + static_cast<size_t>(off) * k, dqs + static_cast<size_t>(off) * kQsWords, hs, false,
-                                  nullptr, R.hcnt_dev + 2ull * c))
-        return drain(r + 1, rc);  // (the slot's host streams drain with the device below)
-      HIP_TRY(hipEventRecord(R.hchunk[c], hs));
+      if (int rc = enqueue_search(h, R, S.dq + static_cast<size_t>(off) * d, m, k, ef, S.dids + static_cast<size_t>(off) * k,
+                                  S.dd + static_cast<size_t>(off) * k, S.dqs + static_cast<size_t>(off) * kQsWords, hs,
+                                  nullptr, S.hcnt_dev + 2ull * c))
+        return drain(r + 1, rc);
+      HIP_TRY(hipEventRecord(S.hchunk[c], hs));
     }
-    for (size_t i = 0; i < R.hstreams.size(); ++i) {
-      HIP_TRY(hipEventRecord(R.hjoin[i], R.hstreams[i]));
-      HIP_TRY(hipStreamWaitEvent(R.stream, R.hjoin[i], 0));
-    }
-    HIP_TRY(hipEventRecord(R.ev1, R.stream));
-    chunked[r] = 1;
+    C.chunked[r] = 1;
   }
   // Dynamic cache, pipelined: the previous call's logs are replayed while this call's searches run, and the updates
   // go onto each slot's stream behind them (they serve from the next call on)
-  const bool dynamic = h->cache_policy == SHINE_CACHE_DYNAMIC && !access;
-  const bool lagged = dynamic && cache_lagged();
-  std::vector<shine_stats> per;
-  double replay_ms = 0;
-  if (lagged) {
+  if (C.lagged) {
     const auto t0 = std::chrono::steady_clock::now();
-    replay_all(h, per);
-    replay_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    replay_all(h, C.per);
+    C.replay_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     for (uint32_t r = 0; r < G; ++r)
       if (int rc = enqueue_update(h, h->reps[r])) return drain(G, rc);
   }
+  return SHINE_OK;
+}
+
+// Collect an enqueued call: each slot's results, chunk by chunk in order while later chunks still run, into the
+// caller's arrays; the statistics; and, under the dynamic cache, the call's logs.  The staging goes back to the pool.
+int knn_collect(shine_index* h, shine_request& C, shine_stats* stats) {
+  const uint32_t G = static_cast<uint32_t>(h->reps.size());
+  const uint32_t k = C.k;
   int rc = SHINE_OK;
   shine_stats agg{};
   const uint64_t e = elem_bytes(h->elem);
+  auto give_all = [&]() {
+    for (uint32_t r = 0; r < G && r < C.stage.size(); ++r) give_stage(h->reps[r], C.stage[r]);
+  };
   // results of the slot's queries lo .. hi-1 out of the staging into the caller's arrays, and their counters
   auto collect = [&](uint32_t r, uint32_t lo, uint32_t hi) {
-    const Replica& R = h->reps[r];
-    const std::vector<uint32_t>& pr = part[r];
+    const HostStage& S = *C.stage[r];
+    const std::vector<uint32_t>& pr = C.part[r];
     const bool run = hi > lo && pr[hi - 1] - pr[lo] == hi - 1 - lo;  // queries in call order: bulk copies
     if (run) {
-      std::memcpy(out_ids + static_cast<size_t>(pr[lo]) * k, R.hids.p + static_cast<size_t>(lo) * k,
+      std::memcpy(C.out_ids + static_cast<size_t>(pr[lo]) * k, S.hids.p + static_cast<size_t>(lo) * k,
                   static_cast<size_t>(hi - lo) * k * 4);
-      if (out_dists)
-        std::memcpy(out_dists + static_cast<size_t>(pr[lo]) * k, R.hd.p + static_cast<size_t>(lo) * k,
+      if (C.out_dists)
+        std::memcpy(C.out_dists + static_cast<size_t>(pr[lo]) * k, S.hd.p + static_cast<size_t>(lo) * k,
                     static_cast<size_t>(hi - lo) * k * 4);
     }
     for (size_t j = lo; j < hi; ++j) {
       const uint32_t qi = pr[j];
       if (!run) {
-        std::memcpy(out_ids + static_cast<size_t>(qi) * k, R.hids.p + j * k, k * 4);
-        if (out_dists) std::memcpy(out_dists + static_cast<size_t>(qi) * k, R.hd.p + j * k, k * 4);
+        std::memcpy(C.out_ids + static_cast<size_t>(qi) * k, S.hids.p + j * k, k * 4);
+        if (C.out_dists) std::memcpy(C.out_dists + static_cast<size_t>(qi) * k, S.hd.p + j * k, k * 4);
       }
-      const uint32_t* qs = R.hqs.p + j * kQsWords;
-      if (qstats) std::memcpy(qstats + static_cast<size_t>(qi) * SHINE_QS_WORDS, qs, SHINE_QS_WORDS * 4);
+      const uint32_t* qs = S.hqs.p + j * kQsWords;
+      if (C.qstats) std::memcpy(C.qstats + static_cast<size_t>(qi) * SHINE_QS_WORDS, qs, SHINE_QS_WORDS * 4);
       if (qs[SHINE_QS_STATUS] != 0 && rc == SHINE_OK)
         rc = set_error(static_cast<int>(qs[SHINE_QS_STATUS]),
                        "query " + std::to_string(qi) + " failed with status " + std::to_string(qs[SHINE_QS_STATUS]));
@@ -1719,40 +1758,43 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
   double kernel_ms = 0;
   uint64_t retries = 0;
   for (uint32_t r = 0; r < G; ++r) {
-    const uint32_t n = static_cast<uint32_t>(part[r].size());
+    const uint32_t n = static_cast<uint32_t>(C.part[r].size());
     if (n == 0) continue;
     Replica& R = h->reps[r];
     HIP_TRY(hipSetDevice(R.device));
-    if (chunked[r]) {  // chunk by chunk, in order, while the later ones run
-      for (uint32_t c = 0, off = 0; off < n; ++c, off += csize[r]) {
-        HIP_TRY(hipEventSynchronize(R.hchunk[c]));
-        collect(r, off, std::min(n, off + csize[r]));
-        const volatile uint32_t* cc = R.hcnt.p + 2ull * c;
+    HostStage& S = *C.stage[r];
+    float ms = 0;
+    for (uint32_t c = 0, off = 0; off < n; ++c, off += C.csize[r]) {  // chunk by chunk, in order
+      HIP_TRY(hipEventSynchronize(S.hchunk[c]));
+      collect(r, off, std::min(n, off + C.csize[r]));
+      float mc = 0;
+      HIP_TRY(hipEventElapsedTime(&mc, S.ev0, S.hchunk[c]));
+      ms = std::max(ms, mc);
+      if (C.chunked[r]) {
+        const volatile uint32_t* cc = S.hcnt.p + 2ull * c;
         if (cc[1]) retries += cc[0];
       }
     }
-    HIP_TRY(hipStreamSynchronize(R.stream));
-    if (!chunked[r]) collect(r, 0, n);
-    float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, R.ev0, R.ev1));
+    if (!C.chunked[r]) {
+      HIP_TRY(hipStreamSynchronize(R.stream));  // (the log counts' copy behind the searches)
+      const uint32_t* cnt = R.main.seen.p;      // written by the call's last pass (finish_call)
+      retries += cnt[0] + cnt[1] + cnt[2];      // queries handed on by each pass
+    }
     kernel_ms = std::max(kernel_ms, static_cast<double>(ms));
     if (r < h->slot_rate.size() && ms > 0) h->slot_rate[r] = n / static_cast<double>(ms);
-    if (!chunked[r]) {
-      const uint32_t* cnt = R.main.seen.p;  // written by the call's last pass (finish_call)
-      retries += cnt[0] + cnt[1] + cnt[2];  // queries handed on by each pass
-    }
     if (env_int("SHINE_PHASE_PROFILE", 0) && R.prof.p) print_phase_profile(h, R);
   }
+  give_all();
   agg.overflow_retries = retries;
   agg.kernel_ms = kernel_ms;
-  if (dynamic) {
+  if (C.dynamic) {
     // this call's logs to the host (device-API searches on other streams of a slot log into the same buffers: the
     // device drains first when one ran)
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t r = 0; r < G; ++r) {
       Replica& R = h->reps[r];
       HIP_TRY(hipSetDevice(R.device));
-      if (!lagged || R.dev_api_dirty) {
+      if (!C.lagged || R.dev_api_dirty) {
         HIP_TRY(hipDeviceSynchronize());
         R.dev_api_dirty = false;
         R.counts_inflight = false;  // counted again after every stream's searches
@@ -1760,14 +1802,14 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
       ++R.dyn_call;  // the coin's call counter: one per host call
     }
     if (int e2 = fetch_logs(h)) return e2;
-    if (!lagged) {  // the updates before the call returns
-      replay_all(h, per);
+    if (!C.lagged) {  // the updates before the call returns
+      replay_all(h, C.per);
       for (uint32_t r = 0; r < G; ++r) {
         if (int e2 = enqueue_update(h, h->reps[r])) return e2;
         HIP_TRY(hipStreamSynchronize(h->reps[r].stream));
       }
     }
-    for (const shine_stats& p : per) {
+    for (const shine_stats& p : C.per) {
       agg.cache_admitted += p.cache_admitted;
       agg.cache_evicted += p.cache_evicted;
       agg.cache_rescued += p.cache_rescued;
@@ -1776,12 +1818,31 @@ int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, ui
     if (env_int("SHINE_DEBUG_CACHE_TIMING", 0)) {  // diagnostics: where the time between calls goes
       const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       std::fprintf(stderr, "cache timing: kernel %.3f ms, replay during the searches %.3f ms, after them %.3f ms, "
-                   "admitted %llu (%s)\n", kernel_ms, replay_ms, ms, static_cast<unsigned long long>(agg.cache_admitted),
-                   lagged ? "pipelined" : "synchronous");
+                   "admitted %llu (%s)\n", kernel_ms, C.replay_ms, ms, static_cast<unsigned long long>(agg.cache_admitted),
+                   C.lagged ? "pipelined" : "synchronous");
     }
   }
   if (stats) *stats = agg;
   return rc;
+}
+
+// shine_knn_batch with the handle locked.  access (nullable): per-slot device counters of record reads (warmup).
+int knn_host(shine_index* h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k, uint32_t ef,
+             uint32_t* out_ids, float* out_dists, uint32_t* qstats, shine_stats* stats,
+             std::vector<DevBuf<uint32_t>>* access) {
+  shine_request C;
+  C.h = h;
+  C.nq = nq;
+  C.k = k;
+  C.out_ids = out_ids;
+  C.out_dists = out_dists;
+  C.qstats = qstats;
+  C.access = access;
+  if (int rc = knn_enqueue(h, C, queries, query_ids, ef)) {
+    for (uint32_t r = 0; r < C.stage.size(); ++r) give_stage(h->reps[r], C.stage[r]);
+    return rc;
+  }
+  return knn_collect(h, C, stats);
 }
 
 }  // namespace
@@ -1801,6 +1862,58 @@ int shine_knn_batch_ex(shine_index_t h, const float* queries, const uint32_t* qu
   if (!queries || !out_ids) return set_error(SHINE_ERR_ARG, "NULL host pointer");
   std::lock_guard<std::mutex> lk(h->mu);
   return knn_host(h, queries, query_ids, nq, k, ef, out_ids, out_dists, qstats, stats, nullptr);
+}
+
+int shine_knn_batch_async(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
+                          uint32_t ef, uint32_t* out_ids, float* out_dists, uint32_t* qstats, shine_request_t* out) {
+  if (!out) return set_error(SHINE_ERR_ARG, "NULL request pointer");
+  *out = nullptr;
+  if (int rc = check_knn_args(h, k, ef)) return rc;
+  if (nq > 0 && (!queries || !out_ids)) return set_error(SHINE_ERR_ARG, "NULL host pointer");
+  std::lock_guard<std::mutex> lk(h->mu);
+  auto C = std::make_unique<shine_request>();
+  C->h = h;
+  C->nq = nq;
+  C->k = k;
+  C->out_ids = out_ids;
+  C->out_dists = out_dists;
+  C->qstats = qstats;
+  if (nq > 0) {
+    const int rc = knn_enqueue(h, *C, queries, query_ids, ef);
+    if (rc) {
+      for (uint32_t r = 0; r < C->stage.size(); ++r) give_stage(h->reps[r], C->stage[r]);
+      return rc;
+    }
+    // the dynamic cache replays a call's logs between calls, in call order: such a call is collected at once
+    if (C->dynamic) {
+      C->rc = knn_collect(h, *C, &C->stats);
+      C->collected = true;
+    }
+  } else {
+    C->collected = true;
+  }
+  h->requests.push_back(C.get());
+  *out = C.release();
+  return SHINE_OK;
+}
+
+int shine_wait(shine_request_t req, shine_stats* stats) {
+  if (!req) return set_error(SHINE_ERR_ARG, "request is NULL");
+  shine_index* h = req->h;
+  int rc = SHINE_OK;
+  {
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!req->collected) {
+      req->rc = knn_collect(h, *req, &req->stats);
+      req->collected = true;
+    }
+    rc = req->rc;
+    if (stats) *stats = req->stats;
+    for (uint32_t r = 0; r < req->stage.size(); ++r) give_stage(h->reps[r], req->stage[r]);  // (an error path)
+    h->requests.erase(std::remove(h->requests.begin(), h->requests.end(), req), h->requests.end());
+  }
+  delete req;
+  return rc;  // (shine_last_error holds the message set when the call was collected)
 }
 
 int shine_prepare(shine_index_t h, uint32_t nq, uint32_t k, uint32_t ef) {
@@ -2187,7 +2300,14 @@ int shine_selftest_cache(uint32_t entries, uint64_t seed, uint32_t n_calls, cons
 }
 
 int shine_close(shine_index_t h) {
-  if (h) release_index(h);
+  if (!h) return SHINE_OK;
+  // requests never waited for: their staging goes back to the pools (freed, once the devices drain, with the rest)
+  for (shine_request* q : h->requests) {
+    for (uint32_t r = 0; r < q->stage.size() && r < h->reps.size(); ++r) give_stage(h->reps[r], q->stage[r]);
+    delete q;
+  }
+  h->requests.clear();
+  release_index(h);
   return SHINE_OK;
 }
 

@@ -30,6 +30,7 @@
   } while (0)
 
 struct shine_index;
+struct shine_request;
 
 namespace shine {
 
@@ -154,6 +155,27 @@ struct Scratch {
   }
 };
 
+// Pinned staging of one host-API call on one GPU slot, mapped into the GPU's address space (the kernels read the
+// queries and write ids, distances and counters there over PCIe), with the device addresses, per-chunk hand-on counts
+// and the chunks' completion events.  A slot keeps a pool: a synchronous call takes a set and gives it back before it
+// returns, an asynchronous call (shine_knn_batch_async) holds its own until shine_wait, so calls in flight never share.
+struct HostStage {
+  HostBuf<float> hq, hd;
+  HostBuf<uint32_t> hids, hqs, hcnt;  // hcnt: per chunk, queries its passes handed on and a written flag
+  float *dq = nullptr, *dd = nullptr;
+  uint32_t *dids = nullptr, *dqs = nullptr, *hcnt_dev = nullptr;
+  std::vector<hipEvent_t> hchunk;     // chunk c's results are in the staging once hchunk[c] fired
+  hipEvent_t ev0 = nullptr;           // before the call's first launch (kernel_ms runs to the last chunk's event)
+  void release() {
+    for (auto* b : {&hq, &hd}) b->release();
+    for (auto* b : {&hids, &hqs, &hcnt}) b->release();
+    for (hipEvent_t e : hchunk) (void)hipEventDestroy(e);
+    hchunk.clear();
+    if (ev0) (void)hipEventDestroy(ev0);
+    ev0 = nullptr;
+  }
+};
+
 struct Replica {
   int device = 0;
   uint32_t slot = 0;
@@ -176,16 +198,12 @@ struct Replica {
   // search scratch: the handle's own stream, then caller streams of the device API
   Scratch main;
   std::vector<std::pair<hipStream_t, std::unique_ptr<Scratch>>> by_stream;
-  // staging for the host-pointer API: pinned, mapped into the GPU's address space (the kernels read and write it)
-  HostBuf<float> hq, hd;
-  HostBuf<uint32_t> hids, hqs;
-  // the host-pointer API's own in-flight streams: a call of more than one chunk (shine_knn_batch, kHostChunk queries)
-  // runs its chunks over them, forked from and joined back into `stream` by events
+  // staging sets of the host-pointer API (HostStage), free for the next call
+  std::vector<std::unique_ptr<HostStage>> stages_free;
+  // the host-pointer API's own in-flight streams: a call's chunks (shine_knn_batch, kHostChunk queries) go round-robin
+  // over them, after whatever the slot's own stream held when the call was enqueued (the fork event)
   std::vector<hipStream_t> hstreams;
-  std::vector<hipEvent_t> hjoin;
-  std::vector<hipEvent_t> hchunk;  // one per chunk of the current call: its results are in the staging
-  HostBuf<uint32_t> hcnt;          // per chunk of the current call (mapped): queries its passes handed on, written flag
-  uint32_t* hcnt_dev = nullptr;
+  uint64_t hnext = 0;  // the next chunk's host stream
   hipEvent_t hfork = nullptr;
   DevBuf<unsigned long long> prof;  // SHINE_PHASE_PROFILE diagnostics
   // dynamic record cache (SHINE_CACHE_DYNAMIC): this GPU's arena, lookup table, logs and the host policy engine
@@ -339,6 +357,7 @@ class TaskPool {
 
 // The opaque handle of include/shine_gpu.h.
 struct shine_index : shine::IndexState {
+  std::vector<shine_request*> requests;  // shine_knn_batch_async calls not waited for yet
   std::mutex mu;
   shine::TaskPool pool;  // (declared last: its threads stop before the state they work on goes)
 };

@@ -156,6 +156,8 @@ PROTOTYPES = {
     "shine_knn_batch": (I32, [P, P, P, U32, U32, U32, P, P, C.POINTER(Stats)]),  # SURVEY.md §8b's 9 arguments
     "shine_knn_batch_ex": (I32, [P, P, P, U32, U32, U32, P, P, P, C.POINTER(Stats)]),
     "shine_prepare": (I32, [P, U32, U32, U32]),
+    "shine_knn_batch_async": (I32, [P, P, P, U32, U32, U32, P, P, P, C.POINTER(P)]),
+    "shine_wait": (I32, [P, C.POINTER(Stats)]),
     "shine_release_stream": (I32, [P, P]),
     "shine_set_cache_policy": (I32, [P, I32, C.c_double, U64]),
     "shine_cache_update": (I32, [P]),

@@ -51,6 +51,23 @@ class KnnResult:
     stats: dict          # aggregates (statistics.hh names)
 
 
+class KnnRequest:
+    """A shine_knn_batch_async call in flight: its output arrays are filled by wait()."""
+
+    def __init__(self, req: C.c_void_p, res: KnnResult):
+        self._req = req
+        self._res = res
+
+    def wait(self) -> KnnResult:
+        if self._req is None:
+            return self._res
+        st = L.Stats()
+        req, self._req = self._req, None
+        L.check(L.lib().shine_wait(req, C.byref(st)))
+        self._res.stats = st.as_dict()
+        return self._res
+
+
 class Index:
     def __init__(self, handle: int, dim: int, metric: int):
         self._h = C.c_void_p(handle)
@@ -152,6 +169,23 @@ class Index:
         L.check(L.lib().shine_knn_batch_ex(self._h, _ptr(q), _ptr(qid), nq, k, ef, _ptr(ids), _ptr(dists), _ptr(qs),
                                         C.byref(st)))
         return KnnResult(ids, dists, qs, st.as_dict())
+
+    def knn_async(self, queries: np.ndarray, k: int, ef: int, query_ids: np.ndarray | None = None) -> "KnnRequest":
+        """shine_knn_batch_async: enqueue and return at once; KnnRequest.wait() (shine_wait) gives the KnnResult.
+        Several requests may be in flight on one handle; each is waited for once."""
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        if q.ndim != 2 or q.shape[1] != self.dim:
+            raise ValueError(f"queries must be (nq, {self.dim})")
+        nq = q.shape[0]
+        qid = None if query_ids is None else np.ascontiguousarray(query_ids, dtype=np.uint32)
+        if qid is not None and qid.shape != (nq,):
+            raise ValueError("query_ids must hold one id per query")
+        res = KnnResult(np.empty((nq, k), dtype=np.uint32), np.empty((nq, k), dtype=np.float32),
+                        np.empty((nq, L.QS_WORDS), dtype=np.uint32), {})
+        req = C.c_void_p()
+        L.check(L.lib().shine_knn_batch_async(self._h, _ptr(q), _ptr(qid), nq, k, ef, _ptr(res.ids), _ptr(res.dists),
+                                              _ptr(res.qstats), C.byref(req)))
+        return KnnRequest(req, res)
 
     def prepare(self, nq: int, k: int, ef: int) -> None:
         """shine_prepare: one-time setup (streams, scratch, staging, kernel code) for calls of up to nq queries."""

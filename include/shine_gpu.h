@@ -166,6 +166,20 @@ int shine_open_buffers_ex(const uint8_t* const* dumps, const uint64_t* sizes, ui
 int shine_knn_batch(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
                     uint32_t ef, uint32_t* out_ids, float* out_dists, shine_stats* stats);
 
+/* Asynchronous shine_knn_batch_ex: routes, stages and enqueues the batch, then returns a request without waiting for
+ * any search (the reference keeps T threads x C coroutines of queries in flight across its query loop,
+ * worker_pool.hh:78-89, scheduler.hh:42-96; here a caller keeps several calls in flight).  The queries are copied
+ * before the call returns, so their buffer may be reused at once; out_ids / out_dists / qstats (caller-owned, same
+ * layout as shine_knn_batch_ex) are written by shine_wait and must stay valid until it returns.  Calls enqueued back
+ * to back run concurrently, chunk by chunk, on every slot's host streams; results equal shine_knn_batch's, query by
+ * query.  Under SHINE_CACHE_DYNAMIC the call completes before it returns (the cache replays calls in order).  Every
+ * request is waited for exactly once; shine_close discards the ones never waited for. */
+typedef struct shine_request* shine_request_t;
+int shine_knn_batch_async(shine_index_t h, const float* queries, const uint32_t* query_ids, uint32_t nq, uint32_t k,
+                          uint32_t ef, uint32_t* out_ids, float* out_dists, uint32_t* qstats, shine_request_t* out);
+/* Wait for a request, write its results and statistics (stats nullable), and free it: the call's status. */
+int shine_wait(shine_request_t req, shine_stats* stats);
+
 /* One-time setup before a measured query phase (the GPU side of the reference's compute-thread setup, outside its
  * query timer, compute_node.cc:354-380): on every slot the host streams, per-stream scratch and pinned staging for
  * calls of up to nq queries, and the search kernels' code loaded, by searching nq all-zero queries (results

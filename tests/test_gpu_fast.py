@@ -558,3 +558,32 @@ def test_host_api_counts_every_chunks_hand_ons(gpu_available, monkeypatch):
             got[chunk] = r.stats["overflow_retries"]
     assert got["0"] > 0, got
     assert got["300"] == got["0"] and got["1024"] == got["0"], got
+
+
+@pytest.mark.parametrize("mode", [L.MODE_FAST, L.MODE_EXACT])
+def test_async_calls_in_flight_equal_synchronous_ones(mode, gpu_available):
+    """shine_knn_batch_async + shine_wait (include/shine_gpu.h): three calls enqueued back to back, their chunks in
+    flight together on the host streams, then waited for out of order; every result equals the synchronous call's
+    query by query (ids, distances, counters), and the statistics add up.  A request of zero queries completes at once,
+    and shine_close discards one never waited for."""
+    base = D.deep_like(5000, seed=421, d=96)
+    q = D.deep_like(3 * 2100, seed=422, d=96)
+    dumps, _, _ = O.build(base, 16, 80, 0, 1, seed=7)
+    parts = [q[i * 2100:(i + 1) * 2100] for i in range(3)]
+    with shine_amd.Index.from_buffers(dumps, 96, 16, 0, gpus=[0]) as idx:
+        idx.set_search_mode(mode)
+        want = [idx.knn(p, 10, 64) for p in parts]
+        reqs = [idx.knn_async(p, 10, 64) for p in parts]
+        got = [reqs[i].wait() for i in (2, 0, 1)]
+        got = [got[1], got[2], got[0]]
+        for w, g in zip(want, got):
+            np.testing.assert_array_equal(g.ids, w.ids)
+            np.testing.assert_array_equal(g.dists.view(np.uint32), w.dists.view(np.uint32))
+            np.testing.assert_array_equal(g.qstats[:, :8], w.qstats[:, :8])
+            assert g.stats["processed"] == 2100 and g.stats["distcomps"] == w.stats["distcomps"]
+            assert g.stats["kernel_ms"] > 0
+        assert idx.knn_async(q[:0], 10, 64).wait().stats["processed"] == 0
+        idx.knn_async(parts[0], 10, 64)  # never waited for: shine_close drains and frees it
+    if mode == L.MODE_EXACT:
+        ref_ids, _, _ = O.OracleIndex(dumps, 96, 16, 0).knn(parts[1][:200], 10, 64, threads=8)
+        np.testing.assert_array_equal(got[1].ids[:200], ref_ids)
