@@ -18,8 +18,9 @@ Also reported: `roofline` for the search kernel (algorithmic bytes of the K laun
 events vs 8 TB/s; `avg_launch_ms` is the per-launch event time, which rocprofv3's average duration matches),
 `value_host_to_host` (SURVEY §8d's query phase: queries and results in pinned host memory that the kernels read and
 write over PCIe, K steps, batches in flight as above; `value_host_to_host_copies` the same with copy-engine H2D / D2H;
-`value_host_api` is the drop-in C-ABI host call shine_knn_batch over the rank's whole query set per call, which the
-library runs as chunks in flight; `value_host_api_per_batch` the same call one batch at a time)
+`value_host_api` is the drop-in C-ABI host call over the rank's whole query set per call, which the library runs as
+chunks in flight, two calls kept in flight through shine_knn_batch_async / shine_wait; `value_host_api_sync` the
+synchronous shine_knn_batch the same way, one call at a time; `value_host_api_per_batch` that call one batch at a time)
 and `cpu_baseline` (the CPU oracle — a C++ restatement of the reference's knn — built with the reference's flags on
 the host that runs it, on the host cores, bounded sample, rank 0 at N=1 only).
 
@@ -489,10 +490,29 @@ def main():
         for _ in range(calls):
             idx.knn(q, a.k, a.ef)
         el = max_over_ranks(time.perf_counter() - t0, dist, "cuda")
-        out["value_host_api"] = calls * q.shape[0] * world / el
-        out["ms_per_step_host_api"] = el * 1e3 / (calls * a.nbatches)
-        out["host_api_calls"] = {"calls": calls, "queries_per_call": int(q.shape[0]),
-                                 "same_ids_as_device": bool(ref_ids is not None and (api_ids == ref_ids).all())}
+        out["value_host_api_sync"] = calls * q.shape[0] * world / el
+        # the same calls through shine_knn_batch_async, the next call enqueued before the previous one is waited for
+        # (two in flight: the GPU does not drain between calls), at least three calls
+        acalls = max(3, calls)
+        async_ids = idx.knn_async(q, a.k, a.ef).wait().ids
+        if dist:
+            dist.barrier()
+        t0 = time.perf_counter()
+        pending = []
+        for _ in range(acalls):
+            pending.append(idx.knn_async(q, a.k, a.ef))
+            if len(pending) >= 2:
+                pending.pop(0).wait()
+        for r in pending:
+            r.wait()
+        el = max_over_ranks(time.perf_counter() - t0, dist, "cuda")
+        out["value_host_api"] = acalls * q.shape[0] * world / el
+        out["ms_per_step_host_api"] = el * 1e3 / (acalls * a.nbatches)
+        out["host_api_calls"] = {"calls": acalls, "queries_per_call": int(q.shape[0]), "calls_in_flight": 2,
+                                 "entry": "shine_knn_batch_async + shine_wait",
+                                 "same_ids_as_device": bool(ref_ids is not None and (api_ids == ref_ids).all()),
+                                 "async_same_ids_as_sync": bool((async_ids == api_ids).all()),
+                                 "sync_calls": calls}
         # the same API one batch per call (nothing in flight between calls: the round-4 leg)
         steps_api = max(1, min(a.steps, 20))
         t0 = time.perf_counter()

@@ -18,6 +18,7 @@
 // as lib_assert / exit_with_help_message do (utils.hh:17-23, configuration.hh:88-113).
 #include <algorithm>
 #include <chrono>
+#include <deque>
 #include <cerrno>
 #include <cmath>
 #include <cstdint>
@@ -67,7 +68,7 @@ struct Config {
   // GPU placement (include/shine_gpu.h)
   std::vector<int> gpus{0};
   std::string placement = "replica", search_mode = "exact", rows = "f32", builder = "cpu";
-  uint32_t batch = 0, memory_nodes = 1;
+  uint32_t batch = 0, memory_nodes = 1, calls_in_flight = 1;
 };
 
 const char* kHelp =
@@ -99,6 +100,8 @@ const char* kHelp =
     "                             value, bitwise the same results) (default f32)\n"
     "      --batch N              queries per shine_knn_batch call (default 0: the whole query set in one call, which\n"
     "                             the library runs as 1,024-query chunks kept in flight on four streams per GPU)\n"
+    "      --calls-in-flight N    host calls kept in flight (shine_knn_batch_async / shine_wait; default 1: one\n"
+    "                             synchronous call at a time; with N > 1 and --batch 0 the set goes out in 2N calls)\n"
     "      --builder B            cpu (parallel restatement of HNSW::insert) | gpu (shine_gpu_build, the batch\n"
     "                             builder on the first --gpus device) (default cpu)\n";
 
@@ -153,6 +156,7 @@ Config parse(int argc, char** argv) {
     else if (a == "--num-clients") c.num_clients = static_cast<uint32_t>(parse_uint(a, v));
     else if (a == "--client-id") c.client_id = static_cast<uint32_t>(parse_uint(a, v));
     else if (a == "--batch") c.batch = static_cast<uint32_t>(parse_uint(a, v));
+    else if (a == "--calls-in-flight") c.calls_in_flight = std::max<uint32_t>(1, static_cast<uint32_t>(parse_uint(a, v)));
     else if (a == "--memory-nodes") c.memory_nodes = static_cast<uint32_t>(parse_uint(a, v));
     else if (a == "--placement") c.placement = v;
     else if (a == "--search-mode") c.search_mode = v;
@@ -438,16 +442,44 @@ int run(const Config& c) {
   build_stats.num("index_size", index_size);
   build_stats.num("max_level", info.max_level);
 
+  // queries per call: --batch, or the whole set in one call, or with calls in flight the set in 2N calls
+  auto per_call_of = [&](uint32_t n_total) -> uint32_t {
+    if (c.batch) return c.batch;
+    if (c.calls_in_flight > 1) return std::max<uint32_t>(1, (n_total + 2 * c.calls_in_flight - 1) / (2 * c.calls_in_flight));
+    return std::max<uint32_t>(1, n_total);
+  };
   auto run_batches = [&](const Database& db, ComputeThread& th) {  // th.results sized by the caller
-    const uint32_t per_call = c.batch ? c.batch : std::max<uint32_t>(1, db.num_read());
+    const uint32_t per_call = per_call_of(db.num_read());
+    if (c.calls_in_flight <= 1) {
+      for (uint32_t s = 0; s < db.num_read(); s += per_call) {
+        const uint32_t n = std::min(per_call, db.num_read() - s);
+        shine_stats st{};
+        check(shine_knn_batch(h, db.comps.data() + static_cast<size_t>(s) * db.dim, db.ids.data() + s, n, c.k,
+                              c.ef_search, th.results.data() + static_cast<size_t>(s) * c.k, nullptr, &st),
+              "shine_knn_batch");
+        add(th.stats, st);
+      }
+      return;
+    }
+    // T threads x C coroutines keep queries in flight in the reference (worker_pool.hh:78-89, scheduler.hh:42-96):
+    // here N host calls, the next enqueued before the oldest is waited for, so the GPU never drains between calls
+    std::deque<shine_request_t> inflight;
+    auto wait_oldest = [&]() {
+      shine_stats st{};
+      check(shine_wait(inflight.front(), &st), "shine_wait");
+      inflight.pop_front();
+      add(th.stats, st);
+    };
     for (uint32_t s = 0; s < db.num_read(); s += per_call) {
       const uint32_t n = std::min(per_call, db.num_read() - s);
-      shine_stats st{};
-      check(shine_knn_batch(h, db.comps.data() + static_cast<size_t>(s) * db.dim, db.ids.data() + s, n, c.k,
-                            c.ef_search, th.results.data() + static_cast<size_t>(s) * c.k, nullptr, &st),
-            "shine_knn_batch");
-      add(th.stats, st);
+      shine_request_t req = nullptr;
+      check(shine_knn_batch_async(h, db.comps.data() + static_cast<size_t>(s) * db.dim, db.ids.data() + s, n, c.k,
+                                  c.ef_search, th.results.data() + static_cast<size_t>(s) * c.k, nullptr, nullptr, &req),
+            "shine_knn_batch_async");
+      inflight.push_back(req);
+      if (inflight.size() >= c.calls_in_flight) wait_oldest();
     }
+    while (!inflight.empty()) wait_oldest();
   };
 
   if (c.use_cache) {  // cache warmup (compute_node.cc:116-131): the warmup split runs first, then the cache is reset
@@ -462,7 +494,7 @@ int run(const Config& c) {
 
   // the compute threads' setup, outside the query timer (compute_node.cc:354-380): streams, scratch and staging for
   // the query phase's calls and the kernels' code, by a call over all-zero queries
-  check(shine_prepare(h, std::max<uint32_t>(1, c.batch ? std::min(c.batch, queries.num_read()) : queries.num_read()),
+  check(shine_prepare(h, std::max<uint32_t>(1, std::min(per_call_of(queries.num_read()), queries.num_read())),
                       c.k, c.ef_search),
         "shine_prepare");
   status("run queries");

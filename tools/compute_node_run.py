@@ -32,6 +32,7 @@ def main():
     p.add_argument("--mode", default="fast")
     p.add_argument("--threads", type=int, default=16)
     p.add_argument("--dir", default="/tmp/shine_cn")
+    p.add_argument("--inflight", default="2,3", help="--load-index runs with these --calls-in-flight as well")
     p.add_argument("--out", default=str(ROOT / "gpurun_out" / "compute_node_run.jsonl"))
     a = p.parse_args()
     import torch
@@ -53,7 +54,10 @@ def main():
     common = ["-d", str(d), "-q", "sift", "-t", str(a.threads), "--ef-search", str(a.ef), "-k", "10", "-m", "16",
               "--ef-construction", "200", "--search-mode", a.mode]
     lines = []
-    for label, extra in (("store_gpu_build", ["--store-index", "--builder", "gpu"]), ("load", ["--load-index"])):
+    runs = [("store_gpu_build", ["--store-index", "--builder", "gpu"]), ("load", ["--load-index"])]
+    for n in (int(x) for x in a.inflight.split(",") if x.strip()):  # host calls kept in flight (shine_knn_batch_async)
+        runs.append((f"load_inflight{n}", ["--load-index", "--calls-in-flight", str(n)]))
+    for label, extra in runs:
         t1 = time.time()
         r = subprocess.run([str(exe), *common, *extra], capture_output=True, text=True, timeout=900)
         if r.returncode != 0:
