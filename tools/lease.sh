@@ -14,7 +14,7 @@
 #   host_api             tools/host_api_probe.py
 #   compute_node         tools/compute_node_run.py (the compute-node facade on big-ann files)
 #   k20                  tools/k20_timeline.py (fast and exact)
-#   phase=WORKLOAD       tools/phase_profile.py (bench) or tools/phase_profile_cfg5.py (cfg5)
+#   phase=WORKLOAD       tools/phase_profile.py (bench) or tools/phase_profile_cfg5.py (cfg5[:N records])
 # Environment: every KEY=VALUE in LEASE_ENV (';'-separated) is exported for the whole lease (library hooks).
 set -o pipefail
 TAG=${1:?tag}; shift
@@ -71,7 +71,8 @@ for step in "$@"; do
       run k20 400 python -u tools/k20_timeline.py --reps 3 --warmup 5 --mode fast,exact --out "$O/k20.jsonl" ;;
     phase)
       # (the library prints the phase totals to stderr: phase*.log)
-      if [ "$arg" = cfg5 ]; then run phase_cfg5 600 python -u tools/phase_profile_cfg5.py
+      if [ "${arg%%:*}" = cfg5 ]; then n=10000000; [ "$arg" != cfg5 ] && n=${arg#*:}
+        run phase_cfg5_$n 600 python -u tools/phase_profile_cfg5.py --n $n
       else run phase 400 python -u tools/phase_profile.py; fi ;;
     *)
       echo "unknown step $name"; exit 2 ;;

@@ -2,7 +2,8 @@
 counters of every dispatch land in the pass's CSV and tools/pmc.py / pmc_summary.py keep the search kernel's).
 
   WORKLOAD=sift1m    the bench's index: SIFT-shaped 1M x 128, L2, M=16, efC=200 (bench.py --builder gpu), ef 128
-  WORKLOAD=cfg5_10m  TTI-shaped 10M x 200, inner product, fp16 rows, Zipf(1.0) query mix, ef 250
+  WORKLOAD=cfg5_10m  TTI-shaped 10M x 200, inner product, fp16 rows, Zipf(1.0) query mix, ef 250 (N: another size,
+                     e.g. N=50000000 for cfg 5's full size)
 ROWS=f32|u8|f16 (default: the workload's), MODE=fast|exact, EF, NQ (queries per batch, default 1024), REPS.
 """
 import os
@@ -25,7 +26,7 @@ if work == "sift1m":
     q = D.sift_like(nq, seed=2)
     dim, metric, ef, rows = 128, 0, 128, os.environ.get("ROWS", "f32")
 else:
-    base = D.generate_device("tti_like", 10_000_000, seed=1, d=200)
+    base = D.generate_device("tti_like", int(os.environ.get("N", "10000000")), seed=1, d=200)
     pool = D.generate_device("tti_like", 500_000, seed=2, d=200).cpu().numpy()
     q = np.ascontiguousarray(D.zipf_query_mix(pool, nq, 1.0, seed=3)[0])
     dim, metric, ef, rows = 200, 1, 250, os.environ.get("ROWS", "f16")
