@@ -1573,6 +1573,8 @@ struct shine_request {
   std::vector<uint8_t> chunked;                      // [slot] 1: chunks on the host streams, 0: one launch on R.stream
   std::vector<uint32_t> csize, nchunks;              // [slot] chunk size and count
   bool dynamic = false, lagged = false;
+  bool rotate = false;                               // chunks start at the slot's next host stream (asynchronous
+                                                     // calls in flight spread over the streams), else at stream 0
   std::vector<shine_stats> per;                      // the lagged replay's statistics
   double replay_ms = 0;
   int rc = SHINE_OK;                                 // an error already met (collected calls drain first)
@@ -1681,9 +1683,14 @@ int knn_enqueue(shine_index* h, shine_request& C, const float* queries, const ui
     HIP_TRY(hipEventRecord(S.ev0, R.stream));
     HIP_TRY(hipEventRecord(R.hfork, R.stream));
     for (hipStream_t hs : R.hstreams) HIP_TRY(hipStreamWaitEvent(hs, R.hfork, 0));
+    // A synchronous call starts at stream 0, so that consecutive calls put their chunks on the same streams and each
+    // stream's visited tables are learned from the calls before it (capi.cc learned_*_table: per stream); calls in
+    // flight together start where the previous one stopped
+    const uint64_t first = C.rotate ? R.hnext : 0;
+    if (C.rotate) R.hnext += n_chunks;
     for (uint32_t c = 0, off = 0; off < n; ++c, off += m_chunk) {
       const uint32_t m = std::min(m_chunk, n - off);
-      hipStream_t hs = R.hstreams[R.hnext++ % R.hstreams.size()];
+      hipStream_t hs = R.hstreams[(first + c) % R.hstreams.size()];
       stage(off, off + m);
       if (int rc = enqueue_search(h, R, S.dq + static_cast<size_t>(off) * d, m, k, ef, S.dids + static_cast<size_t>(off) * k,
                                   S.dd + static_cast<size_t>(off) * k, S.dqs + static_cast<size_t>(off) * kQsWords, hs,
@@ -1878,6 +1885,7 @@ int shine_knn_batch_async(shine_index_t h, const float* queries, const uint32_t*
   C->out_ids = out_ids;
   C->out_dists = out_dists;
   C->qstats = qstats;
+  C->rotate = true;
   if (nq > 0) {
     const int rc = knn_enqueue(h, *C, queries, query_ids, ef);
     if (rc) {

@@ -203,7 +203,7 @@ struct Replica {
   // the host-pointer API's own in-flight streams: a call's chunks (shine_knn_batch, kHostChunk queries) go round-robin
   // over them, after whatever the slot's own stream held when the call was enqueued (the fork event)
   std::vector<hipStream_t> hstreams;
-  uint64_t hnext = 0;  // the next chunk's host stream
+  uint64_t hnext = 0;  // the host stream an asynchronous call's first chunk takes
   hipEvent_t hfork = nullptr;
   DevBuf<unsigned long long> prof;  // SHINE_PHASE_PROFILE diagnostics
   // dynamic record cache (SHINE_CACHE_DYNAMIC): this GPU's arena, lookup table, logs and the host policy engine
