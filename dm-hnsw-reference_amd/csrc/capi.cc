@@ -549,6 +549,17 @@ bool spill_hashed(const shine_index* h) {
 uint32_t spill_hash_entries(uint32_t vis_cap) {
   return std::min<uint32_t>(kSpillHashMax, std::max<uint32_t>(16384, pow2_at_least(8 * std::max<uint32_t>(vis_cap, 1))));
 }
+// Two-choice u32 buckets (kernels_impl.h VisitedLds<3>) where the linear-probed u32 table would be used beyond L2 (the
+// 26-27-bit id spaces of cfg 4 / cfg 5), at a load of SHINE_VT3_LOAD / 1000 (default 0.6) at the mean query, grown to
+// the largest table at the same wavefronts per CU: an insert is one read of both buckets and one compare-and-swap
+// whatever the load, so the table runs fuller than the u32 rule's 0.45 and more wavefronts share a CU.  Compiled for
+// replicas only (no read accounting); SHINE_VT3 = 0 turns it off (A/B).
+bool vt3_usable(const shine_index* h) {
+  const bool sharded = h->placement != SHINE_PLACE_REPLICA && h->reps.size() > 1;
+  return !sharded && env_int("SHINE_VT3", 1) != 0;
+}
+uint32_t vt3_load_permille() { return static_cast<uint32_t>(std::min<int64_t>(900, std::max<int64_t>(100, env_int("SHINE_VT3_LOAD", 600)))); }
+
 // Words per spill / fallback slot: the id-space bitmap, or at least the largest hash table; a multiple of 4 words, so
 // that every slot starts 16-byte aligned (spill_release clears a hash table with 16-byte stores from the slot base).
 uint64_t slot_words(const shine_index* h) {
@@ -611,7 +622,8 @@ uint32_t learned_mean_table(const Scratch& S) {
 // against 1.38 M for 7,488 at 5, 1.39 M for 8,192 at 4 and 1.21-1.24 M at 3 (profiles/r05/scale_cfg4_viscap*.jsonl,
 // scale_cfg5_viscap*.jsonl).  The few queries that outgrow the table spill in place to the L2 hash set.
 // SHINE_FAST_TABLE_POW2=1: the round-4 rule (the power of two 9/8 above the last call's worst query).
-uint32_t learned_max_table(const Scratch& S, uint32_t ef, uint32_t lds_per_cu, uint32_t waves_wanted) {
+uint32_t learned_max_table(const Scratch& S, uint32_t ef, uint32_t lds_per_cu, uint32_t waves_wanted,
+                           uint32_t load_permille = 450) {
   if (!S.seen.p || !S.seen.p[3] || env_int("SHINE_DEBUG_NO_LEARN", 0)) return 0;
   auto clampt = [&](uint64_t t) {
     return std::min<uint32_t>(16384, std::max<uint32_t>({1024u, S.table_floor, static_cast<uint32_t>(std::min<uint64_t>(t, 16384))}));
@@ -629,7 +641,7 @@ uint32_t learned_max_table(const Scratch& S, uint32_t ef, uint32_t lds_per_cu, u
     const uint64_t per = lds_per_cu / w / 1024 * 1024;
     return per > overhead + 256 ? (per - overhead) / 4 / 64 * 64 : 0;
   };
-  const uint64_t want = (mean * 20 / 9 + 63) / 64 * 64;  // load 0.45 at the mean query
+  const uint64_t want = (mean * 1000 / std::max<uint32_t>(100, load_permille) + 63) / 64 * 64;  // (0.45: the u32 rule)
   // (no more wavefronts per CU than two batches of this call's size put there: a small call takes a larger table)
   const uint64_t w = std::max<uint64_t>(1, std::min<uint64_t>(waves(want), waves_wanted));
   return clampt(std::max(want, largest_at(w)));
@@ -662,7 +674,7 @@ uint32_t learned_exact_table(const Scratch& S, uint32_t ef, uint32_t recent_vmax
 }
 
 LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds_per_cu, uint64_t id_space,
-                            uint32_t learned = 0, bool grow = false, bool byte_rows = false) {
+                            uint32_t learned = 0, bool grow = false, bool byte_rows = false, uint32_t vt3_table = 0) {
   LaunchShape sh{};
   const uint32_t want = std::max<uint32_t>(1, std::min<uint32_t>(16, (nq + cus - 1) / cus));
   // Waves per CU the tables are sized for, in batches of `want`, and the table floor per ef.  f32 rows: two batches,
@@ -721,8 +733,16 @@ LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds
   // a forced table size: the entries it allows (0: back to u32; u16 buckets need a power of two)
   if (sh.vis16) sh.vis16 = (sh.vis_cap & (sh.vis_cap - 1)) == 0 ? kind16(sh.vis_cap) : 0u;
   if (force16 == 2 && bits <= log2u(sh.vis_cap) + 12) sh.vis16 = 2;  // test hook: two-choice
+  // two-choice u32 buckets: the learned table of vt3_usable indexes beyond L2 (enqueue_search), or forced at any id space
+  // and table size (test hook SHINE_DEBUG_VIS16=3; the size rounded down to whole buckets)
+  if (vt3_table) {
+    sh.vis16 = 3;
+    sh.vis_cap = vt3_table;
+  }
+  if (force16 == 3) sh.vis16 = 3;
+  if (sh.vis16 == 3) sh.vis_cap = std::max<uint32_t>(64, sh.vis_cap / 4 * 4);
   sh.vis_bits = std::max(bits, log2u(sh.vis_cap) + 1);
-  const uint64_t need = lds_alloc_bytes(search_fast_lds_bytes(sh.vis_cap, ef, sh.vis16 ? 2 : 4));
+  const uint64_t need = lds_alloc_bytes(search_fast_lds_bytes(sh.vis_cap, ef, vis_entry_bytes(sh.vis16)));
   const uint32_t fit = std::max<uint32_t>(1, static_cast<uint32_t>(lds_per_cu / need));
   const uint32_t wpc = std::max<uint32_t>(1, std::min<uint32_t>({(nq + cus - 1) / cus, 16u, fit}));
   sh.cap = 0;
@@ -797,7 +817,8 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
       const bool can16 = force16 != 0 && kind != 0;
       vis16 = can16 && (w16 > w32 || force16 >= 1) ? kind : 0;
       if (force16 == 2 && bits <= log2_ceil(vis_cap) + 12) vis16 = 2;  // test hook: two-choice
-      return vis16 ? w16 : w32;
+      if (force16 == 3) vis16 = 3;                                       // test hook: two-choice u32 buckets
+      return vis16 == 1 || vis16 == 2 ? w16 : w32;
     };
     sh.vis_cap = std::min<uint32_t>(16384, std::max<uint32_t>(1024, pow2_at_least(per_ef * ef)));
     // a learned size replaces the fixed one: with the spill in either direction, else only to shrink (or to grow
@@ -820,25 +841,31 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
     // ef = 128, 6,528 entries and 5 per CU against 8,192 and 4, 1.51 M against 1.42 M QPS; at 50M ids and ef = 250 it
     // holds the same 3 per CU with less room for next_candidates and ran at 0.38 M against 0.41 M
     // (profiles/r05/scale_cfg{4,5}_exact_rule.jsonl).
+    // Two-choice u32 buckets (vt3_usable) take the same rule at their higher load (SHINE_VT3_LOAD).
+    const bool vt3 = vt3_usable(h);
     if (mean_visits && sh.vis16 == 0 && spill_enabled() && spill_hashed(h) && env_int("SHINE_EXACT_LOAD_RULE", 1)) {
       const uint64_t fixed = top_bytes + align16(8ull * 5 * ef) + 512;
       auto waves = [&](uint64_t t) {
         return std::min<uint64_t>(want, lds / lds_alloc_bytes(fixed + align16(4ull * t)));
       };
-      const uint64_t t0 = (static_cast<uint64_t>(mean_visits) * 20 / 9 + 63) / 64 * 64;
+      const uint64_t t0 = (static_cast<uint64_t>(mean_visits) * 1000 / (vt3 ? vt3_load_permille() : 450) + 63) / 64 * 64;
       const uint64_t w = std::max<uint64_t>(1, waves(t0));
       const uint64_t per = lds / w / 1024 * 1024;
       const uint64_t t = per > fixed + 4096 ? std::min<uint64_t>(16384, (per - fixed) / 4 / 64 * 64) : 0;
       if (t >= t0 && t >= 1024 && w > wpc) {
         sh.vis_cap = static_cast<uint32_t>(t);
-        sh.vis16 = 0;
+        sh.vis16 = vt3 ? 3u : 0u;
         wpc = static_cast<uint32_t>(w);
       }
     }
+    // beyond L2 every u32 table of a replica takes two-choice buckets: an insert costs one read and one swap where a
+    // linear probe chain grows with the load (the worst queries fill the tables learned from them)
+    if (vt3 && sh.vis16 == 0 && spill_enabled() && spill_hashed(h)) sh.vis16 = 3;
     if (const char* e = std::getenv("SHINE_DEBUG_VISCAP")) {  // test hook
       sh.vis_cap = static_cast<uint32_t>(std::atoll(e));
       wpc = fit(sh.vis_cap, sh.vis16, false);
     }
+    if (sh.vis16 == 3) sh.vis_cap = std::max<uint32_t>(64, sh.vis_cap / 4 * 4);  // whole buckets
     sh.vis_bits = std::max(bits, log2_ceil(sh.vis_cap) + 1);
     budget = (lds / wpc) & ~15u;
   } else if (pass == PASS_WHOLE_CU) {
@@ -848,7 +875,7 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
     budget = kLightFixupLds;
     wpc = static_cast<uint32_t>(env_int("SHINE_DEBUG_LIGHT_WPC", std::max<uint32_t>(1, static_cast<uint32_t>(lds / kLightFixupLds))));
   }
-  const int64_t vis_bytes = static_cast<int64_t>(align16((sh.vis16 ? 2ull : 4ull) * sh.vis_cap));
+  const int64_t vis_bytes = static_cast<int64_t>(align16(static_cast<uint64_t>(vis_entry_bytes(sh.vis16)) * sh.vis_cap));
   const int64_t cap = (static_cast<int64_t>(budget) - static_cast<int64_t>(top_bytes) - vis_bytes - 512) / 8;
   sh.cap = static_cast<uint32_t>(std::max<int64_t>(cap & ~1ll, 2));
   if (pass == PASS_LDS) sh.cap = static_cast<uint32_t>(std::max<int64_t>(1, env_int("SHINE_DEBUG_CAP", sh.cap)));
@@ -945,7 +972,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   // scale_cfg3_cfg5_10m_v6_maxtable.jsonl) or, beyond L2, the u32 table of learned_max_table (load 0.45 at the mean,
   // grown to its residency level), where it holds the wavefronts one batch puts on a CU.  SHINE_FAST_TABLE_MAX=0 / 1
   // forces either (tuning).
-  uint32_t learned_fast = 0, learned_mean = 0;
+  uint32_t learned_fast = 0, learned_mean = 0, learned_vt3 = 0;
   if (ef == S.last_ef) {
     if (!spill_enabled()) {
       learned_fast = learned;
@@ -960,6 +987,9 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
       const int64_t force = env_int("SHINE_FAST_TABLE_MAX", -1);
       learned_fast = (force == 1 || (force < 0 && max_fits && beyond_l2)) ? max_t : mean_t;
       learned_mean = mean_t;
+      if (beyond_l2 && force < 0 && vt3_usable(h))
+        learned_vt3 = learned_max_table(S, ef, R.lds_per_cu, static_cast<uint32_t>(std::min<uint64_t>(16, 2 * need)),
+                                        vt3_load_permille()) / 4 * 4;
     }
   }
   S.last_ef = ef;
@@ -974,14 +1004,14 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     const int pass = chain[i];
     const LaunchShape sh =
         pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu, h->id_space, learned_fast, handed > 0,
-                                          elem_is_byte(h->elem))
+                                          elem_is_byte(h->elem), learned_vt3)
                           : pick_shape(h, R, nq, ef, pass, handed, learned, learned_mean,
                                        i == 0 ? mean_v : 0u);
     if (i == 0) {
       S.last_table = sh.vis_cap;
       S.last_fast = pass == PASS_FAST;
       // the table came from learning, not the fixed rule
-      S.last_learned = (learned_fast != 0 && sh.vis_cap == learned_fast) ||
+      S.last_learned = (learned_fast != 0 && sh.vis_cap == learned_fast) || (learned_vt3 != 0 && sh.vis16 == 3) ||
                        (pass != PASS_FAST && learned != 0 && sh.vis_cap == learned);
       if (env_int("SHINE_DEBUG_SHAPE", 0))  // diagnostics: the main pass's shape and what it was learned from
         std::fprintf(stderr, "shape: pass %d nq %u ef %u table %u vis16 %u grid %u learned %u vmax %u handed %u floor %u "

@@ -91,7 +91,8 @@ struct SearchArgs {
   uint32_t fast;            // 1: sorted-list kernel (SHINE_MODE_FAST; ef <= kFastMaxEf, vis_cap > 0)
   uint32_t sort_out;        // heap kernel writes ascending order (fast-mode fixup passes)
   uint32_t global_heaps;    // 1: heap kernel with both heaps in HBM (last fallback pass; vis_cap must be 0)
-  uint32_t vis16;           // LDS visited table of u16 quotient entries (kernels_impl.h VisitedLds<1>)
+  uint32_t vis16;           // LDS visited table kind (kernels_impl.h VisitedLds<vis16>): 0 u32 linear probing, 1 u16
+                            // quotient entries, 2 u16 two-choice buckets, 3 u32 two-choice buckets (replicas only)
   uint32_t vis_bits;        // ... bits of the id space the multiply permutes (vis_bits - log2(vis_cap) <= 10: buckets of 8, >= 3 distance bits)
   uint32_t vis_mul;         // ... odd multiplier
   uint32_t vis_mul_inv;     // ... its inverse mod 2^32 (decodes an entry back to its id when a table spills)
@@ -153,6 +154,9 @@ struct BuildArgs {
   unsigned long long* stats;  // [0] appended rows [1] pruned rows [2] pools truncated to 64 [3] upper beams stopped
 };
 enum BuildKernel { BUILD_UPPER = 0, BUILD_SELECT = 1, BUILD_PRUNE = 2 };
+
+// bytes of one visited-table entry of SearchArgs::vis16's kind (u16 entries for kinds 1 and 2)
+__host__ __device__ inline uint32_t vis_entry_bytes(uint32_t vis16) { return vis16 == 1 || vis16 == 2 ? 2u : 4u; }
 
 // LDS layout of a search workgroup: top[ef] | next[cap] | visited table[vis_cap] (entry_bytes each) | scratch
 // ids[64], dists[64]

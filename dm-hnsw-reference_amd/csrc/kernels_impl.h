@@ -1195,6 +1195,82 @@ struct VisitedLds<2> {
   }
 };
 
+// VT = 3: u32 keys in two-choice buckets of 4 (16 bytes), for id spaces too wide for the u16 entries (26-27-bit ids:
+// cfg 4's 100M, cfg 5's 50M records), where the linear-probed VT = 0 table needs a load of ~0.45 to keep its probe
+// chains short: the wave's 32 list slots walk their chains in lockstep, so an expansion waits for its longest chain
+// (DESIGN §4, round 5).  Here an id goes to the less filled of its two buckets b1, b2 (two multiplicative hashes; b1 on
+// a tie), at the bucket's first empty word; buckets fill in order and never empty, so an id sits in b2 only if b1 held
+// an entry then, and a guessed swap into an empty b1's word 0 that succeeds proves the id absent from both.  A lookup
+// reads both buckets (two ds_read_b128 in flight together) and plans the insert (word, INV, id), so an insert is one
+// read and one compare-and-swap round trip whatever the load, and the table runs fuller (load ~0.6: more wavefronts per
+// CU).  Both buckets full: an overflow, the query spills in place.  Any multiple of 4 entries (home = umulhi).
+template <>
+struct VisitedLds<3> {
+  static constexpr u32 kPresent = 0xFFFFFFFEu, kFull = 0xFFFFFFFDu;
+  u32* t;
+  u32 nb;
+  using Hint = Plan2;
+  __device__ __forceinline__ VisitedLds(void* base, const SearchArgs& A) : t(static_cast<u32*>(base)), nb(A.vis_cap >> 2) {}
+  static constexpr u32 kBytes = 4;
+  static __device__ __forceinline__ Hint unknown() { return Plan2{INV, 0u, 0u}; }
+  __device__ __forceinline__ void clear(const SearchArgs& A, int lane) {
+    uint4* t4 = reinterpret_cast<uint4*>(t);
+    for (u32 i = lane; i < A.vis_cap / 4; i += 64) t4[i] = make_uint4(INV, INV, INV, INV);
+  }
+  __device__ __forceinline__ u32 b1(u32 x) const { return __umulhi(x * 0x9E3779B1u, nb); }
+  __device__ __forceinline__ u32 b2(u32 x) const { return __umulhi(x * 0x85EBCA77u, nb); }
+  template <class F>
+  __device__ __forceinline__ void for_each(F f, const SearchArgs& A, int lane) const {
+    for (u32 i = lane; i < A.vis_cap; i += 64) {
+      const u32 x = t[i];
+      if (x < A.g.N) f(x);
+    }
+  }
+  __device__ __forceinline__ void insert_first(u32 x) { t[b1(x) * 4] = x; }
+  __device__ __forceinline__ uint4 bucket(u32 b) const { return reinterpret_cast<const uint4*>(t)[b]; }
+  // words in a bucket (they fill in order): the first empty word's index, 4 when full
+  static __device__ __forceinline__ u32 fill(const uint4& w) {
+    return w.x == INV ? 0u : w.y == INV ? 1u : w.z == INV ? 2u : w.w == INV ? 3u : 4u;
+  }
+  __device__ __forceinline__ Hint probe(u32 x) const {
+    const u32 h1 = b1(x), h2 = b2(x);
+    const uint4 w1 = bucket(h1), w2 = bucket(h2);
+    // (written with `|`: short-circuit tests compile to a cascade of exec-mask branches)
+    const bool in = (w1.x == x) | (w1.y == x) | (w1.z == x) | (w1.w == x) | (w2.x == x) | (w2.y == x) | (w2.z == x) |
+                    (w2.w == x);
+    if (in) return Plan2{kPresent, 0u, 0u};
+    const u32 f1 = fill(w1), f2 = fill(w2);
+    const bool second = f2 < f1;
+    const u32 f = second ? f2 : f1;
+    if (f >= 4u) return Plan2{kFull, 0u, 0u};
+    return Plan2{(second ? h2 : h1) * 4 + f, INV, x};
+  }
+  __device__ __forceinline__ bool home_match(u32 /*x*/, const Hint& p) const { return p.pw == kPresent; }
+  __device__ __forceinline__ int begin(u32 /*x*/, const Hint& p, u32& pw, u32& pexp, u32& pold) {
+    if (p.pw == kPresent) return 0;
+    if (p.pw >= kFull) return 2;
+    pw = p.pw;
+    pexp = p.pexp;
+    pold = atomicCAS(&t[pw], p.pexp, p.pnew);
+    return 1;
+  }
+  __device__ __forceinline__ void finish(u32 x, u32 pexp, u32 pold, bool& ovf) {
+    if (pold != pexp) (void)test_and_set(x, ovf, probe(x));
+  }
+  __device__ __forceinline__ bool test_and_set(u32 x, bool& ovf, Hint p = unknown()) {
+    if (p.pw == INV) p = Plan2{b1(x) * 4, INV, x};
+    for (;;) {
+      if (p.pw == kPresent) return false;
+      if (p.pw == kFull) {
+        ovf = true;
+        return false;
+      }
+      if (atomicCAS(&t[p.pw], p.pexp, p.pnew) == p.pexp) return true;
+      p = probe(x);  // a word changed under us (or was not as guessed): read both buckets again
+    }
+  }
+};
+
 // End of the last pass of a call: the last workgroup to finish publishes the queries every pass handed on (host
 // memory: the next call sizes its light pass from them, shine_knn_batch reports them) and zeroes the call's counter
 // words for the next call on this stream, so a call needs neither a memset nor a copy of its own.  No fence is
@@ -2188,7 +2264,7 @@ __global__ __launch_bounds__(64) void heap_replay_kernel(const int32_t* ops, con
 
 template <int D, int METRIC, typename E, int AC>
 hipError_t launch_search_acct(uint32_t grid, const SearchArgs& a, hipStream_t s) {
-  const size_t lds = search_lds_bytes(a.ef, a.cap, a.vis_cap, a.vis16 && a.vis_cap > 0 ? 2 : 4);
+  const size_t lds = search_lds_bytes(a.ef, a.cap, a.vis_cap, a.vis_cap > 0 ? vis_entry_bytes(a.vis16) : 4);
   auto run = [&](auto kern) -> hipError_t {
     if (lds > 65536) {  // beyond the default dynamic-LDS limit: opt in (per device, so every launch)
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -2199,7 +2275,7 @@ hipError_t launch_search_acct(uint32_t grid, const SearchArgs& a, hipStream_t s)
     return hipGetLastError();
   };
   if (a.fast) {  // sorted-list kernel; the launcher's caller guarantees ef <= kFastMaxEf and a visited table in LDS
-    const size_t lds_f = search_fast_lds_bytes(a.vis_cap, a.ef, a.vis16 ? 2 : 4);
+    const size_t lds_f = search_fast_lds_bytes(a.vis_cap, a.ef, vis_entry_bytes(a.vis16));
     auto runf = [&](auto kern) -> hipError_t {
       if (lds_f > 65536) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -2230,6 +2306,10 @@ hipError_t launch_search_acct(uint32_t grid, const SearchArgs& a, hipStream_t s)
       return wide ? runf(search_fast_kernel<D, METRIC, E, 8, 4, AC, VT>) : runf(search_fast_kernel<D, METRIC, E, 8, 2, AC, VT>);
     };
     if (a.vis16 == 2) return pick(std::integral_constant<int, 2>{});
+    if (a.vis16 == 3) {  // two-choice u32 buckets: compiled for replicas (no read accounting) only
+      if constexpr (!AC) return pick(std::integral_constant<int, 3>{});
+      else return hipErrorInvalidValue;
+    }
     return a.vis16 ? pick(std::integral_constant<int, 1>{}) : pick(std::integral_constant<int, 0>{});
   }
   if constexpr (!AC && D == 128 && METRIC == 0 && std::is_same_v<E, float>) {
@@ -2242,6 +2322,10 @@ hipError_t launch_search_acct(uint32_t grid, const SearchArgs& a, hipStream_t s)
     return hipGetLastError();
   }
   if (a.vis_cap > 0 && a.vis16 == 2) return run(search_kernel<D, METRIC, E, 0, AC, 2>);
+  if (a.vis_cap > 0 && a.vis16 == 3) {
+    if constexpr (!AC) return run(search_kernel<D, METRIC, E, 0, AC, 3>);
+    else return hipErrorInvalidValue;
+  }
   if (a.vis_cap > 0) return a.vis16 ? run(search_kernel<D, METRIC, E, 0, AC, 1>) : run(search_kernel<D, METRIC, E, 0, AC, 0>);
   return run(search_kernel<D, METRIC, E, 1, AC>);
 }

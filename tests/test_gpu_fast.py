@@ -587,3 +587,36 @@ def test_async_calls_in_flight_equal_synchronous_ones(mode, gpu_available):
     if mode == L.MODE_EXACT:
         ref_ids, _, _ = O.OracleIndex(dumps, 96, 16, 0).knn(parts[1][:200], 10, 64, threads=8)
         np.testing.assert_array_equal(got[1].ids[:200], ref_ids)
+
+
+@pytest.mark.parametrize("viscap,load", [("2048", "875"), ("2048", "100"), ("512", "1000"), ("1500", "875")],
+                         ids=["fits", "spills_at_10pct", "both_buckets_full", "non_pow2"])
+@pytest.mark.parametrize("mode", [L.MODE_FAST, L.MODE_EXACT])
+def test_two_choice_u32_tables_match_oracle(mode, viscap, load, gpu_available, monkeypatch, capfd):
+    """Two-choice u32 buckets (kernels_impl.h VisitedLds<3>, the large-id-space table of replicas, forced here with
+    SHINE_DEBUG_VIS16=3 on a small index): a table that holds every query, the same with a 10 % load limit (every query
+    spills in place and its table moves to the HBM set), 512 entries filled until both buckets of an id are full (the
+    overflowing insert spills), and a table of 1,500 entries (375 buckets, umulhi homes).  Exact mode equals the oracle
+    bit for bit (ids in heap order, distances, counters); fast mode on every tie-free query."""
+    base = D.deep_like(6000, seed=99, d=96)
+    q = D.deep_like(300, seed=100, d=96)
+    dumps, _, _ = O.build(base, 16, 100, 0, 1, seed=4)
+    ref = O.OracleIndex(dumps, 96, 16, 0).knn(q, 10, 128, threads=8)
+    monkeypatch.setenv("SHINE_DEBUG_VISCAP", viscap)
+    monkeypatch.setenv("SHINE_DEBUG_VISLOAD", load)
+    monkeypatch.setenv("SHINE_DEBUG_VIS16", "3")
+    monkeypatch.setenv("SHINE_DEBUG_SHAPE", "1")
+    with shine_amd.Index.from_buffers(dumps, 96, 16, 0, gpus=[0]) as idx:
+        idx.set_search_mode(mode)
+        capfd.readouterr()
+        runs = [idx.knn(q, 10, 128) for _ in range(2)]  # the second call: every spill slot was handed back zeroed
+        err = capfd.readouterr().err
+    assert " vis16 3 " in err, err
+    for r in runs:
+        assert (r.qstats[:, L.QS_STATUS] == 0).all()
+        if mode == L.MODE_EXACT:
+            np.testing.assert_array_equal(r.ids, ref[0])
+            np.testing.assert_array_equal(r.dists.view(np.uint32), ref[1].view(np.uint32))
+            np.testing.assert_array_equal(r.qstats[:, :5], ref[2][:, :5])
+        else:
+            _check_tie_free_exact(r, ref, 0.95)

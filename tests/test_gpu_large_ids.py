@@ -54,8 +54,8 @@ def test_spill_to_hash_at_27_bit_ids(gpu_available, monkeypatch, capfd):
                 out[mode] = idx.knn(q, k, ef)
                 err = capfd.readouterr().err
                 assert " spill_hash 16384" in err, err  # the library chose the hash-table spill target
-            # the library's own fast table at this id space (capi.cc learned_max_table: u32 entries, load 0.45 at the
-            # previous call's mean query, grown to its residency level) once a call has been seen
+            # the library's own fast table at this id space once a call has been seen: two-choice u32 buckets
+            # (kernels_impl.h VisitedLds<3>; capi.cc learned_max_table at SHINE_VT3_LOAD, grown to its residency level)
             monkeypatch.delenv("SHINE_DEBUG_VISCAP")
             monkeypatch.delenv("SHINE_DEBUG_VIS16")
             idx.set_search_mode(L.MODE_FAST)
@@ -66,7 +66,15 @@ def test_spill_to_hash_at_27_bit_ids(gpu_available, monkeypatch, capfd):
             shape = [ln for ln in err.splitlines() if ln.startswith("shape: pass 4")][-1].split()
             table, vis16, learned = int(shape[shape.index("table") + 1]), int(shape[shape.index("vis16") + 1]), \
                 int(shape[shape.index("learned_fast") + 1])
-            assert vis16 == 0 and learned >= 1024 and table % 64 == 0, shape  # u32 entries, a learned size
+            assert vis16 == 3 and learned >= 1024 and table % 4 == 0, shape  # two-choice u32 buckets, a learned size
+            # and the exact pass's (the same load rule on the recent calls' mean query): bit for bit the oracle's
+            idx.set_search_mode(L.MODE_EXACT)
+            for _ in range(3):
+                capfd.readouterr()
+                out["learned_exact"] = idx.knn(q, k, ef)
+            err = capfd.readouterr().err
+            shape = [ln for ln in err.splitlines() if ln.startswith("shape: pass")][0].split()
+            assert int(shape[shape.index("vis16") + 1]) == 3, shape
         step("searched")
     ex, fa = out[L.MODE_EXACT], out[L.MODE_FAST]
     assert ex.stats["overflow_retries"] == 0 and (ex.qstats[:, L.QS_STATUS] == 0).all()
@@ -81,6 +89,11 @@ def test_spill_to_hash_at_27_bit_ids(gpu_available, monkeypatch, capfd):
     np.testing.assert_array_equal(fa.dists[clean].view(np.uint32), s_d[clean].view(np.uint32))
     np.testing.assert_array_equal(np.sort(fa.ids[clean], 1), np.sort(s_ids[clean], 1))
     np.testing.assert_array_equal(fa.qstats[clean][:, :5], ref_qs[clean][:, :5])
+    lx = out["learned_exact"]
+    assert (lx.qstats[:, L.QS_STATUS] == 0).all()
+    np.testing.assert_array_equal(lx.ids, ref_ids)
+    np.testing.assert_array_equal(lx.dists.view(np.uint32), ref_d.view(np.uint32))
+    np.testing.assert_array_equal(lx.qstats[:, :5], ref_qs[:, :5])
     le = out["learned"]
     clean = le.qstats[:, L.QS_TIES] == 0
     assert clean.mean() >= 0.9 and (le.qstats[:, L.QS_STATUS] == 0).all()

@@ -82,7 +82,7 @@ def run(name, a):
     L = shine_amd._lib
     ef0 = int((a.ef or str(ef)).split(",")[0])
     # the oracle's knn on the GPU-built dump (a checker sample, before the replica takes the build's arrays)
-    orc = oracle_ref(shine_amd, gb, q, a.k, ef0, dim, M, metric, 8 if name == "cfg4" else 1,
+    orc = oracle_ref(shine_amd, gb, q, a.k, ef0, dim, M, metric, 8 if name in ("cfg4", "cfg5") else 1,
                      a.cmp_oracle_n) if a.cmp_oracle else None
     if orc is not None and elem != L.ELEM_F32:  # exact mode on f32 rows of the same graph (the oracle's element type)
         with gb.open_ex(1, elem=L.ELEM_F32, gpus=[0]) as ix:
