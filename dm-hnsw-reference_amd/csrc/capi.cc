@@ -729,13 +729,14 @@ LaunchShape pick_fast_shape(uint32_t nq, uint32_t ef, uint32_t cus, uint32_t lds
   sh.vis16 = can16 && (w16 > w32 || tie16) ? kind16(t16) : 0;
   if (force16 >= 1 && can16) sh.vis16 = kind16(t16);  // test hook: force the u16 entries
   sh.vis_cap = sh.vis16 ? t16 : t32;
+  const bool viscap_hook = std::getenv("SHINE_DEBUG_VISCAP") != nullptr;
   sh.vis_cap = static_cast<uint32_t>(env_int("SHINE_DEBUG_VISCAP", sh.vis_cap));  // test hook
   // a forced table size: the entries it allows (0: back to u32; u16 buckets need a power of two)
   if (sh.vis16) sh.vis16 = (sh.vis_cap & (sh.vis_cap - 1)) == 0 ? kind16(sh.vis_cap) : 0u;
   if (force16 == 2 && bits <= log2u(sh.vis_cap) + 12) sh.vis16 = 2;  // test hook: two-choice
-  // two-choice u32 buckets: the learned table of vt3_usable indexes beyond L2 (enqueue_search), or forced at any id space
-  // and table size (test hook SHINE_DEBUG_VIS16=3; the size rounded down to whole buckets)
-  if (vt3_table) {
+  // two-choice u32 buckets: the learned table of vt3_usable indexes beyond L2 (enqueue_search) unless a test hook fixes
+  // the table, or forced at any id space and table size (test hook SHINE_DEBUG_VIS16=3; whole buckets)
+  if (vt3_table && force16 < 0 && !viscap_hook) {
     sh.vis16 = 3;
     sh.vis_cap = vt3_table;
   }
