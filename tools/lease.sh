@@ -9,7 +9,7 @@
 #   bench[=K]            bench.py as the driver runs it (K steps, default 20, warmup 5)
 #   bench_prof[=K]       bench.py under rocprofv3 --kernel-trace --stats (default K = 200), trace span per launch
 #   pmc[=WORKLOADS]      FETCH_SIZE / WRITE_SIZE and SQ counter passes (tools/r04_pmc.sh; sift1m_f32,sift1m_u8,cfg5_10m_f16)
-#   scale=WHICH[:ARGS]   tools/scale_lines.py --which WHICH (cfg3 / cfg4 / cfg5 / cmp ...), ARGS: extra flags, ',' for ' '
+#   scale=WHICH[:ARGS]   tools/scale_lines.py --which WHICH (cfg3 / cfg4 / cfg5 / cmp ...), ARGS: extra flags, "+" for " "
 #   skew[=SLOTS]         one skew-grid cell (alpha 1.0, 5 % cache), baseline and +cache, on SLOTS slots (default 8)
 #   host_api             tools/host_api_probe.py
 #   compute_node         tools/compute_node_run.py (the compute-node facade on big-ann files)
@@ -58,7 +58,7 @@ for step in "$@"; do
       bash tools/r04_pmc.sh "$TAG/pmc" "${arg:-sift1m_f32}" || exit 1 ;;
     scale)
       which=${arg%%:*}; extra=""; [ "$which" != "$arg" ] && extra=${arg#*:}
-      run scale_$which 1150 python -u tools/scale_lines.py --which "$which" ${extra//,/ } \
+      run scale_$which 1150 python -u tools/scale_lines.py --which "$which" ${extra//+/ } \
         --out "$O/scale_$which.jsonl" ;;
     skew)
       run skew${arg:-8} 600 python -u tools/skew_grid.py --slots ${arg:-8} --alphas 1.0 --ratios 5 \
