@@ -1198,15 +1198,18 @@ struct VisitedLds<2> {
 // VT = 3: u32 keys in two-choice buckets of 4 (16 bytes), for id spaces too wide for the u16 entries (26-27-bit ids:
 // cfg 4's 100M, cfg 5's 50M records), where the linear-probed VT = 0 table needs a load of ~0.45 to keep its probe
 // chains short: the wave's 32 list slots walk their chains in lockstep, so an expansion waits for its longest chain
-// (DESIGN §4, round 5).  Here an id goes to the less filled of its two buckets b1, b2 (two multiplicative hashes; b1 on
-// a tie), at the bucket's first empty word; buckets fill in order and never empty, so an id sits in b2 only if b1 held
-// an entry then, and a guessed swap into an empty b1's word 0 that succeeds proves the id absent from both.  A lookup
-// reads both buckets (two ds_read_b128 in flight together) and plans the insert (word, INV, id), so an insert is one
-// read and one compare-and-swap round trip whatever the load, and the table runs fuller (load ~0.6: more wavefronts per
-// CU).  Both buckets full: an overflow, the query spills in place.  Any multiple of 4 entries (home = umulhi).
+// (DESIGN §4, round 5).  An id goes to the less filled of its two buckets b1, b2 (two multiplicative hashes; b1 on a
+// tie), at the bucket's first empty word; when both are full, to the first bucket after b2 (wrapping) with an empty
+// word.  Buckets fill in order and never empty, so a lookup reads b1 and b2 (two ds_read_b128 in flight together): the
+// id in either, or an empty word in either (then the id is absent: it would have gone there), answers it; only when
+// both are full does it walk on from b2 (rare below a load of ~0.6).  An id sits in b2 or beyond only if b1 held an
+// entry then, so a guessed swap into an empty b1's word 0 that succeeds proves the id absent.  The lookup plans the
+// insert (word, INV, id): an insert is one read and one compare-and-swap round trip in the common case, whatever the
+// load, so the table runs fuller than the linear-probed one and more wavefronts share a CU.  A walk past kMaxWalk
+// buckets is an overflow (the query spills in place).  Any multiple of 4 entries (homes by umulhi).
 template <>
 struct VisitedLds<3> {
-  static constexpr u32 kPresent = 0xFFFFFFFEu, kFull = 0xFFFFFFFDu;
+  static constexpr u32 kPresent = 0xFFFFFFFEu, kFull = 0xFFFFFFFDu, kMaxWalk = 64;
   u32* t;
   u32 nb;
   using Hint = Plan2;
@@ -1232,18 +1235,36 @@ struct VisitedLds<3> {
   static __device__ __forceinline__ u32 fill(const uint4& w) {
     return w.x == INV ? 0u : w.y == INV ? 1u : w.z == INV ? 2u : w.w == INV ? 3u : 4u;
   }
+  // (written with `|`: short-circuit tests compile to a cascade of exec-mask branches)
+  static __device__ __forceinline__ bool has(const uint4& w, u32 x) {
+    return (w.x == x) | (w.y == x) | (w.z == x) | (w.w == x);
+  }
   __device__ __forceinline__ Hint probe(u32 x) const {
     const u32 h1 = b1(x), h2 = b2(x);
     const uint4 w1 = bucket(h1), w2 = bucket(h2);
-    // (written with `|`: short-circuit tests compile to a cascade of exec-mask branches)
-    const bool in = (w1.x == x) | (w1.y == x) | (w1.z == x) | (w1.w == x) | (w2.x == x) | (w2.y == x) | (w2.z == x) |
-                    (w2.w == x);
-    if (in) return Plan2{kPresent, 0u, 0u};
+    if (static_cast<int>(has(w1, x)) | static_cast<int>(has(w2, x))) return Plan2{kPresent, 0u, 0u};
     const u32 f1 = fill(w1), f2 = fill(w2);
     const bool second = f2 < f1;
     const u32 f = second ? f2 : f1;
-    if (f >= 4u) return Plan2{kFull, 0u, 0u};
-    return Plan2{(second ? h2 : h1) * 4 + f, INV, x};
+    Plan2 p{(second ? h2 : h1) * 4 + f, INV, x};
+    if (f >= 4u) {  // both full: the overflow walk from b2 on (one loop exit; see the probe loops above)
+      p.pw = kFull;
+      u32 b = h2;
+      for (u32 i = 0; i < kMaxWalk; ++i) {
+        b = b + 1 == nb ? 0u : b + 1;
+        const uint4 w = bucket(b);
+        if (has(w, x)) {
+          p.pw = kPresent;
+          break;
+        }
+        const u32 fb = fill(w);
+        if (fb < 4u) {
+          p.pw = b * 4 + fb;
+          break;
+        }
+      }
+    }
+    return p;
   }
   __device__ __forceinline__ bool home_match(u32 /*x*/, const Hint& p) const { return p.pw == kPresent; }
   __device__ __forceinline__ int begin(u32 /*x*/, const Hint& p, u32& pw, u32& pexp, u32& pold) {
@@ -1266,7 +1287,7 @@ struct VisitedLds<3> {
         return false;
       }
       if (atomicCAS(&t[p.pw], p.pexp, p.pnew) == p.pexp) return true;
-      p = probe(x);  // a word changed under us (or was not as guessed): read both buckets again
+      p = probe(x);  // a word changed under us (or was not as guessed): read the buckets again
     }
   }
 };
