@@ -247,8 +247,20 @@ def measure(torch, idx, name, a, qd, gt, batch, slots, ef, nb=None):
     lines = []
     efs = [int(x) for x in a.ef.split(",")] if a.ef else [ef]
     modes = [m for m in (("fast", shine_amd.MODE_FAST), ("exact", shine_amd.MODE_EXACT)) if m[0] in a.modes.split(",")]
+    def reset(ef):
+        # every run starts from the same learned state (--envs A/B on one handle): one small call per stream at another
+        # ef drops each stream's table floor and the slot's recent worst queries (capi.cc enqueue_search), so a variant
+        # measured earlier cannot size the next one's tables
+        for st in streams:
+            for s in range(slots):
+                n = min(64, per)
+                idx.knn_device(qd[:n].data_ptr(), n, a.k, ef + 1, ids[0, :n].data_ptr(), dists[0, :n].data_ptr(),
+                               qs[0, :n].data_ptr(), stream=st[s].cuda_stream, gpu_slot=s)
+        torch.cuda.synchronize()
+
     for ef, (mode_name, mode) in [(e, m) for e in efs for m in modes]:
         idx.set_search_mode(mode)
+        reset(ef)
         for i in range(nb):
             step(i)
         torch.cuda.synchronize()
