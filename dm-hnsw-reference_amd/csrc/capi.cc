@@ -988,9 +988,12 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
       const int64_t force = env_int("SHINE_FAST_TABLE_MAX", -1);
       learned_fast = (force == 1 || (force < 0 && max_fits && beyond_l2)) ? max_t : mean_t;
       learned_mean = mean_t;
-      if (beyond_l2 && force < 0 && vt3_usable(h))
-        learned_vt3 = learned_max_table(S, ef, R.lds_per_cu, static_cast<uint32_t>(std::min<uint64_t>(16, 2 * need)),
+      if (beyond_l2 && force < 0 && vt3_usable(h)) {
+        // (SHINE_VT3_BATCHES: the batches in flight whose wavefronts the table may make room for, default 2)
+        const uint64_t batches = static_cast<uint64_t>(std::max<int64_t>(1, env_int("SHINE_VT3_BATCHES", 2)));
+        learned_vt3 = learned_max_table(S, ef, R.lds_per_cu, static_cast<uint32_t>(std::min<uint64_t>(16, batches * need)),
                                         vt3_load_permille()) / 4 * 4;
+      }
     }
   }
   S.last_ef = ef;
