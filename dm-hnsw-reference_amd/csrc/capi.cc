@@ -550,15 +550,20 @@ uint32_t spill_hash_entries(uint32_t vis_cap) {
   return std::min<uint32_t>(kSpillHashMax, std::max<uint32_t>(16384, pow2_at_least(8 * std::max<uint32_t>(vis_cap, 1))));
 }
 // Two-choice u32 buckets (kernels_impl.h VisitedLds<3>) where the linear-probed u32 table would be used beyond L2 (the
-// 26-27-bit id spaces of cfg 4 / cfg 5), at a load of SHINE_VT3_LOAD / 1000 (default 0.6) at the mean query, grown to
+// 26-27-bit id spaces of cfg 4 / cfg 5), at a load of SHINE_VT3_LOAD / 1000 (vt3_load_permille) at the mean query, grown to
 // the largest table at the same wavefronts per CU: an insert is one read of both buckets and one compare-and-swap
 // whatever the load, so the table runs fuller than the u32 rule's 0.45 and more wavefronts share a CU.  Compiled for
-// replicas only (no read accounting); SHINE_VT3 = 0 turns it off (A/B).
+// replicas only (no read accounting); SHINE_VT3 = 0 turns it off, 1 forces it on the fast pass too (A/B).
 bool vt3_usable(const shine_index* h) {
   const bool sharded = h->placement != SHINE_PLACE_REPLICA && h->reps.size() > 1;
   return !sharded && env_int("SHINE_VT3", 1) != 0;
 }
-uint32_t vt3_load_permille() { return static_cast<uint32_t>(std::min<int64_t>(900, std::max<int64_t>(100, env_int("SHINE_VT3_LOAD", 600)))); }
+// Loads measured on the 50M TTI-shaped index (profiles/r06/scale_cfg5_vt3_*.jsonl): fast 0.6 (7,488 entries, 5 wavefronts
+// per CU) 1.41 M QPS, 0.7 (5,952, 6) 1.81 M, 0.85 (4,928, 7) 1.82 M once no call hands queries on; exact 0.6 0.63 M, 0.7
+// 0.61 M (linear-probed u32 at 0.45: 1.42 M / 0.41 M).
+uint32_t vt3_load_permille(bool fast) {
+  return static_cast<uint32_t>(std::min<int64_t>(950, std::max<int64_t>(100, env_int("SHINE_VT3_LOAD", fast ? 700 : 600))));
+}
 
 // Words per spill / fallback slot: the id-space bitmap, or at least the largest hash table; a multiple of 4 words, so
 // that every slot starts 16-byte aligned (spill_release clears a hash table with 16-byte stores from the slot base).
@@ -849,7 +854,7 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
       auto waves = [&](uint64_t t) {
         return std::min<uint64_t>(want, lds / lds_alloc_bytes(fixed + align16(4ull * t)));
       };
-      const uint64_t t0 = (static_cast<uint64_t>(mean_visits) * 1000 / (vt3 ? vt3_load_permille() : 450) + 63) / 64 * 64;
+      const uint64_t t0 = (static_cast<uint64_t>(mean_visits) * 1000 / (vt3 ? vt3_load_permille(false) : 450) + 63) / 64 * 64;
       const uint64_t w = std::max<uint64_t>(1, waves(t0));
       const uint64_t per = lds / w / 1024 * 1024;
       const uint64_t t = per > fixed + 4096 ? std::min<uint64_t>(16384, (per - fixed) / 4 / 64 * 64) : 0;
@@ -988,11 +993,18 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
       const int64_t force = env_int("SHINE_FAST_TABLE_MAX", -1);
       learned_fast = (force == 1 || (force < 0 && max_fits && beyond_l2)) ? max_t : mean_t;
       learned_mean = mean_t;
-      if (beyond_l2 && force < 0 && vt3_usable(h)) {
-        // (SHINE_VT3_BATCHES: the batches in flight whose wavefronts the table may make room for, default 2)
+      // Two-choice u32 buckets where the u32 rule leaves one wavefront per SIMD (the latency-bound regime: cfg 5's 50M
+      // records at d = 200, ef = 250, 4 per CU): at load 0.7 they hold 6, 1.42 M -> 1.81 M QPS.  Where the u32 rule
+      // already holds more (cfg 4's 100M records at ef = 128: 6 per CU), the fuller tables' extra wavefronts did not pay
+      // for the two-bucket look-ahead probe: 4.57-4.70 M against 4.66-4.72 M at loads 0.5-0.6, 4.20 M at 0.7 and 8-10
+      // per CU (profiles/r06/scale_cfg4_vt3_*.jsonl).  SHINE_VT3_BATCHES: the batches in flight whose wavefronts the
+      // table may make room for (default 2).
+      const uint64_t waves_u32 = max_t ? R.lds_per_cu / lds_alloc_bytes(search_fast_lds_bytes(max_t, ef, 4)) : 0;
+      const int64_t vt3_force = env_int("SHINE_VT3", -1);
+      if (beyond_l2 && force < 0 && vt3_usable(h) && (vt3_force == 1 || waves_u32 <= 4)) {
         const uint64_t batches = static_cast<uint64_t>(std::max<int64_t>(1, env_int("SHINE_VT3_BATCHES", 2)));
         learned_vt3 = learned_max_table(S, ef, R.lds_per_cu, static_cast<uint32_t>(std::min<uint64_t>(16, batches * need)),
-                                        vt3_load_permille()) / 4 * 4;
+                                        vt3_load_permille(true)) / 4 * 4;
       }
     }
   }
