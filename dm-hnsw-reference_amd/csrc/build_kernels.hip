@@ -26,7 +26,7 @@ __global__ __launch_bounds__(256) void rows_kernel(const float* __restrict__ src
     if (elem == 0) {
       static_cast<float*>(dst)[r * dim + permuted_index(dim, i)] = v;
     } else if (elem == 1) {
-      static_cast<__half*>(dst)[r * dim + permuted_index(dim, i)] = __float2half(v);
+      static_cast<__half*>(dst)[r * dim + i] = __float2half(v);  // fp16 rows: natural order (kernels.h)
     } else {
       static_cast<uint8_t*>(dst)[r * rowb + permuted_index_bytes(dim, i)] =
           static_cast<uint8_t>(static_cast<int>(v));

@@ -385,10 +385,10 @@ int make_index(HostGraph G, int elem, const int* gpu_ids, uint32_t n_gpus, int p
   std::vector<uint32_t> inv(h->inv_size, kInvalid);
   for (uint64_t g = 0; g < G.N; ++g) inv[G.uid[g]] = dev_id(static_cast<uint32_t>(g));
 
-  // rows in the device layout (kernels.h permuted_index / permuted_index_bytes); config 5 converts records to fp16
-  // at load, byte rows narrow them losslessly (checked above)
+  // rows in the device layout (kernels.h permuted_index / permuted_index_bytes / fp16 rows in natural order); config 5
+  // converts records to fp16 at load, byte rows narrow them losslessly (checked above)
   std::vector<uint32_t> perm(dim);
-  for (uint32_t i = 0; i < dim; ++i) perm[i] = elem_is_byte(elem) ? permuted_index_bytes(dim, i) : permuted_index(dim, i);
+  for (uint32_t i = 0; i < dim; ++i) perm[i] = device_index(dim, elem, i);
   std::vector<uint8_t> vbytes(G.N * vrow, 0);
   {
     float* fp = reinterpret_cast<float*>(vbytes.data());

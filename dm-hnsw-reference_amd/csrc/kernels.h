@@ -205,6 +205,11 @@ __host__ __device__ inline uint32_t permuted_index_bytes(uint32_t dim, uint32_t 
   return ((a >> 1) * nch + (t >> 1)) * 4u + (t & 1u) * 2u + (a & 1u);
 }
 inline bool elem_is_byte(int elem) { return elem == 2 || elem == 3; }
+// fp16 rows (config 5) keep the natural element order: their distances are judged by recall, not bitwise, and run on the
+// matrix cores for inner products (kernels_impl.h pass_dists_mfma), which take each lane's 8 consecutive elements
+__host__ __device__ inline uint32_t device_index(uint32_t dim, int elem, uint32_t i) {
+  return elem == 2 || elem == 3 ? permuted_index_bytes(dim, i) : elem == 1 ? i : permuted_index(dim, i);
+}
 inline uint32_t elem_bytes(int elem) { return elem == 0 ? 4u : elem == 1 ? 2u : 1u; }
 // bytes of one device row
 inline uint64_t row_bytes(uint32_t dim, int elem) {

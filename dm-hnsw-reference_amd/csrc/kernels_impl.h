@@ -310,8 +310,72 @@ struct QueryRegs<D, E, true> {
   bool qint;
 };
 
+// fp16 rows (natural order, see NbrBuf<D, __half>): the query for both distance paths — the MFMA operand of the inner
+// product (lane l: A row l & 15, elements 32s + 8(l >> 4) .. +7 of every step s; row 0 the high halves of q * 2^e, row
+// 1 the low halves q * 2^e - high, the other rows zero, so the product keeps ~21 bits of the f32 query; 2^e brings
+// the largest component near 2^14, clear of fp16's subnormals) and the L2 path's f32 values (lane l: chunk l & 3 of
+// every step).  Elements past D are zero.  (A kernel compiles only the part its metric reads.)
+typedef _Float16 v8h __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+template <int D>
+constexpr int kHalfSteps = (D + 31) / 32;  // 32-element steps of an fp16 row
+template <int D>
+struct QueryRegs<D, __half, false> {
+  static constexpr int NS = kHalfSteps<D>;
+  v8h a[NS];         // MFMA A fragments (inner product)
+  float inv_scale;   // 2^-e
+  float qv[NS][8];   // vector path (L2): this lane's chunk of every step, f32
+};
+
 template <int D, typename E>
 __device__ __forceinline__ void load_query(const float* __restrict__ q, int lane, QueryRegs<D, E>& Q) {
+  if constexpr (std::is_same_v<E, __half>) {
+    constexpr int NS = kHalfSteps<D>;
+    // the query's largest magnitude (every lane reads a strided share; a DPP max over the wave)
+    float mx = 0.f;
+    for (int i = lane; i < D; i += 64) mx = fmaxf(mx, fabsf(q[i]));
+    {
+      int x = __float_as_int(mx);
+#define SHINE_DPP_MAX(CTRL, RM)                                                                                    \
+  x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(0, x, CTRL, RM, 0xF, false))));
+      SHINE_DPP_MAX(0x111, 0xF)
+      SHINE_DPP_MAX(0x112, 0xF)
+      SHINE_DPP_MAX(0x114, 0xF)
+      SHINE_DPP_MAX(0x118, 0xF)
+      SHINE_DPP_MAX(0x142, 0xA)
+      SHINE_DPP_MAX(0x143, 0xC)
+#undef SHINE_DPP_MAX
+      mx = __int_as_float(__builtin_amdgcn_readlane(x, 63));
+    }
+    // 2^e with mx * 2^e in [2^13, 2^14): exact powers of two, so the scaling itself rounds nothing
+    int e = 0;
+    if (mx > 0.f && mx == mx && mx < __builtin_inff()) {
+      int ex;
+      (void)frexpf(mx, &ex);  // mx = f * 2^ex, f in [0.5, 1)
+      e = 14 - ex;
+      e = e > 100 ? 100 : (e < -100 ? -100 : e);
+    }
+    const float scale = ldexpf(1.f, e);
+    Q.inv_scale = ldexpf(1.f, -e);
+    const int m = lane & 15, kg = lane >> 4, c = lane & 3;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      v8h a;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = 32 * s + 8 * kg + j;
+        const float v = (m < 2 && i < D) ? q[i] * scale : 0.f;
+        const _Float16 hi = static_cast<_Float16>(v);
+        a[j] = m == 0 ? hi : static_cast<_Float16>(v - static_cast<float>(hi));
+      }
+      Q.a[s] = a;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = 32 * s + 8 * c + j;
+        Q.qv[s][j] = i < D ? q[i] : 0.f;
+      }
+    }
+  } else {
   constexpr int DB = D >> 4 << 4, PER = DB / 8, TAIL = D - DB;
   const int c2 = 2 * (lane & 3);
 #pragma unroll
@@ -342,6 +406,7 @@ __device__ __forceinline__ void load_query(const float* __restrict__ q, int lane
     Q.qq = qq;
     Q.qint = __ballot(!ok) == 0ull;
   }
+  }  // (f32 and byte rows)
 }
 
 // One chunk = elements (t, t+1) of accumulators (2c, 2c+1): f32 → 4 floats, f16 → 4 halves in 2 words, bytes →
@@ -379,6 +444,34 @@ struct NbrBuf<D, E, P, true> {
   u32 x[P][L::NCH];
   u32 xt[P][TW];
 };
+
+// fp16 rows (config 5) are stored in natural element order (kernels.h row layout): fp16 records are judged by recall
+// against the f32 oracle, not bitwise, so their sums need not follow the reference's eight-accumulator order.  A row is
+// NS = ceil(D / 32) steps of 32 elements; a lane holds one 16-byte chunk (8 halves) per step, elements 32s + 8c ..
+// 32s + 8c + 7 for its chunk index c (0..3); chunks past D are loaded from a valid address and masked to zero.  Inner
+// product runs on the matrix cores (pass_dists_mfma: lane l takes slot l & 15 and chunk c = l >> 4, the B operand
+// layout of v_mfma_f32_16x16x32_f16); L2 on the vector units (pass_dists: slot group g = l >> 2, chunk c = l & 3).
+template <int D, int P>
+struct NbrBuf<D, __half, P, false> {
+  static constexpr int NS = kHalfSteps<D>;
+  static_assert(D % 8 == 0, "fp16 rows are read in chunks of 8 elements");
+  uint4 x[P][NS];
+};
+template <int METRIC, typename E>
+constexpr bool kMfma = METRIC == 1 && std::is_same_v<E, __half>;
+// chunk c of step s lies inside the row
+template <int D>
+__device__ __forceinline__ bool half_chunk_valid(int s, int c) { return 32 * s + 8 * c + 8 <= D; }
+// this lane's chunks (index c) of one fp16 row: a chunk past the row reads the step's first chunk instead (always inside
+// the row; its values are masked where the distances use them)
+template <int D, int P>
+__device__ __forceinline__ void load_half_row(NbrBuf<D, __half, P>& B, int p, const __half* __restrict__ row, int c) {
+#pragma unroll
+  for (int s = 0; s < kHalfSteps<D>; ++s) {
+    const int off = half_chunk_valid<D>(s, c) ? 32 * s + 8 * c : 32 * s;
+    B.x[p][s] = *reinterpret_cast<const uint4*>(row + off);
+  }
+}
 
 // This lane's part of one byte row: NCH words at byte c4 * NCH * 4 in the widest aligned loads, then the tail words.
 template <int D, typename E, int P>
@@ -436,6 +529,8 @@ __device__ __forceinline__ void issue_pass(NbrBuf<D, E, P>& B, int p, const E* _
     if constexpr (CACHE) row = cached_row<D, E>(*cg, row, id);
     if constexpr (kByte<E>) {
       load_byte_row<D, E, P>(B, p, row, c4);
+    } else if constexpr (std::is_same_v<E, __half>) {
+      load_half_row<D, P>(B, p, row, c4);
     } else {
       using C = typename ChunkT<E>::type;
 #pragma unroll
@@ -457,6 +552,8 @@ __device__ __forceinline__ void issue_row(NbrBuf<D, E, P>& B, int p, const E* __
   using L = Lay<D, E>;
   if constexpr (kByte<E>) {
     load_byte_row<D, E, P>(B, p, row, c4);
+  } else if constexpr (std::is_same_v<E, __half>) {
+    load_half_row<D, P>(B, p, row, c4);
   } else {
     using C = typename ChunkT<E>::type;
 #pragma unroll
@@ -568,6 +665,36 @@ __device__ __forceinline__ void pass_dists_int(const QueryRegs<D, E>& Q, const N
 template <int D, int METRIC, typename E, int P>
 __device__ __forceinline__ void pass_dists(const QueryRegs<D, E>& Q, const NbrBuf<D, E, P>& B, float (&out)[P]) {
   using L = Lay<D, E>;
+  if constexpr (std::is_same_v<E, __half>) {
+    // fp16 rows on the vector units (natural order): the lane's chunk c = lane & 3 of every step, two accumulators per
+    // slot (even / odd elements), then the group's four lanes summed into its lane 3 (DPP); chunks past D contribute 0
+    const int c = static_cast<int>(threadIdx.x) & 3;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+      for (int st = 0; st < kHalfSteps<D>; ++st) {
+        const bool ok = st < kHalfSteps<D> - 1 || D % 32 == 0 || half_chunk_valid<D>(st, c);
+        const u32 w[4] = {B.x[p][st].x, B.x[p][st].y, B.x[p][st].z, B.x[p][st].w};
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const float x0 = ok ? half_lo(w[h]) : 0.f, x1 = ok ? half_hi(w[h]) : 0.f;
+          if constexpr (METRIC == 0) {
+            const float d0 = Q.qv[st][2 * h] - x0, d1 = Q.qv[st][2 * h + 1] - x1;
+            a0 = __builtin_fmaf(d0, d0, a0);
+            a1 = __builtin_fmaf(d1, d1, a1);
+          } else {
+            a0 = __builtin_fmaf(Q.qv[st][2 * h], x0, a0);
+            a1 = __builtin_fmaf(Q.qv[st][2 * h + 1], x1, a1);
+          }
+        }
+      }
+      float v = a0 + a1;
+      v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xF, 0xF, false));  // row_shr:1
+      v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x112, 0xF, 0xF, false));  // row_shr:2
+      out[p] = METRIC == 0 ? v : 1.0f - v;
+    }
+  } else {
   if constexpr (kByte<E>) {
     if (Q.qint) {  // byte query, byte rows: exact integer dot products (wave-uniform branch)
       pass_dists_int<D, METRIC, E, P>(Q, B, out);
@@ -627,12 +754,63 @@ __device__ __forceinline__ void pass_dists(const QueryRegs<D, E>& Q, const NbrBu
       out[p] = add_tail<D, METRIC, E>(Q, xt, fold8(acc[p]));
     }
   }
+  }  // (f32 and byte rows)
+}
+
+// Inner products of fp16 rows on the matrix cores: per pass p, lane l holds chunk l >> 4 of slot 16p + (l & 15) (the B
+// operand of v_mfma_f32_16x16x32_f16: B[8(l >> 4) + j][l & 15]), the query's high and low halves are rows 0 and 1 of A
+// (QueryRegs<D, __half>), and one MFMA per 32-element step accumulates C = A B; C[0][n] + C[1][n] (lane n, registers 0
+// and 1) is slot 16p + n's product with the scaled query.  out[p] = 1 - <q, x> of slot 16p + lane in lanes 0..15.
+template <int D, int P>
+__device__ __forceinline__ void pass_dists_mfma(const QueryRegs<D, __half>& Q, const NbrBuf<D, __half, P>& B,
+                                                float (&out)[P]) {
+  const int c = static_cast<int>(threadIdx.x) >> 4;
+  v4f acc[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) acc[p] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int st = 0; st < kHalfSteps<D>; ++st) {
+#pragma unroll
+    for (int p = 0; p < P; ++p) {  // P independent accumulation chains interleaved
+      uint4 w = B.x[p][st];
+      // (only the last step can hold chunks past D: they were loaded from the step's first chunk)
+      if (st == kHalfSteps<D> - 1 && D % 32 != 0 && !half_chunk_valid<D>(st, c)) w = make_uint4(0u, 0u, 0u, 0u);
+      acc[p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(Q.a[st], __builtin_bit_cast(v8h, w), acc[p], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < P; ++p) out[p] = 1.0f - (acc[p][0] + acc[p][1]) * Q.inv_scale;
 }
 
 // slots p0 .. p0 + 16P - 1 of the list (those below n)
 template <int D, int METRIC, typename E, int P, bool CACHE = false>
 __device__ __forceinline__ void dist_chunk(const E* __restrict__ vec, const QueryRegs<D, E>& Q, const u32* sc_ids,
                                            float* sc_d, int p0, int n, int lane, const DevGraph* cg = nullptr) {
+  if constexpr (kMfma<METRIC, E>) {  // fp16 inner products: lane l reads chunk l >> 4 of slot 16p + (l & 15)
+    const int n16 = lane & 15, c = lane >> 4;
+    NbrBuf<D, E, P> B;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const int slot = p0 + 16 * p + n16;
+      const u32 id = slot < n ? sc_ids[slot] : INV;
+      if (id != INV) {
+        const E* row = vec + static_cast<u64>(id) * D;
+        if constexpr (CACHE) row = cached_row<D, E>(*cg, row, id);
+        load_half_row<D, P>(B, p, row, c);
+      } else {
+#pragma unroll
+        for (int st = 0; st < kHalfSteps<D>; ++st) B.x[p][st] = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    float out[P];
+    pass_dists_mfma<D, P>(Q, B, out);
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const int slot = p0 + 16 * p + lane;
+      if (lane < 16 && slot < n) sc_d[slot] = out[p];
+    }
+    return;
+  }
   const int g4 = lane >> 2, c4 = lane & 3;
   NbrBuf<D, E, P> B;
 #pragma unroll
@@ -1789,9 +1967,32 @@ __device__ __forceinline__ u32 quad_bcast(u32 x, int p) {  // lane 4g + p's valu
   }
 }
 
-template <int D, typename E, int P, int ACCT>
+template <int D, int METRIC, typename E, int P, int ACCT>
 __device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restrict__ vec, u32 e, u32 pad, int c4,
                                            const DevGraph& g) {
+  if constexpr (kMfma<METRIC, E>) {
+    // fp16 inner products (pass_dists_mfma): lane l reads chunk l >> 4 of slot 16p + (l & 15), whose entry sits in lane
+    // 4 (l & 15) + p of the list (one ds_bpermute per pass for the id, or the dynamic cache's resolved row address)
+    const int lane = static_cast<int>(threadIdx.x), src = 4 * (lane & 15), c = lane >> 4;
+    if constexpr (ACCT == 2) {
+      const E* row = vec + static_cast<u64>(e == INV ? pad : e) * kRowElems<D, E>;
+      if (e != INV) row = cached_row<D, E>(g, row, e);
+      const u64 rp = reinterpret_cast<u64>(row);
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        const u64 lo = static_cast<u32>(__shfl(static_cast<int>(static_cast<u32>(rp)), src + p));
+        const u64 hi = static_cast<u32>(__shfl(static_cast<int>(static_cast<u32>(rp >> 32)), src + p));
+        load_half_row<D, P>(B, p, reinterpret_cast<const E*>((hi << 32) | lo), c);
+      }
+    } else {
+      u32 sid[P];
+#pragma unroll
+      for (int p = 0; p < P; ++p) sid[p] = static_cast<u32>(__shfl(static_cast<int>(e), src + p));
+#pragma unroll
+      for (int p = 0; p < P; ++p) load_half_row<D, P>(B, p, vec + static_cast<u64>(sid[p] == INV ? pad : sid[p]) * D, c);
+    }
+    return;
+  }
   if constexpr (ACCT == 2) {  // dynamic cache: each lane resolves its own list slot to a row, the groups share it
     const E* row = vec + static_cast<u64>(e == INV ? pad : e) * kRowElems<D, E>;
     if (e != INV) row = cached_row<D, E>(g, row, e);
@@ -1888,7 +2089,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kFastWaves<D
     // prefetched list.  X is refilled for the next candidate as soon as the current distances have consumed it.
     NbrBuf<D, E, P> X;
     u32 e = load_row(status == 0 ? nn : pad);
-    issue_list<D, E, P, ACCT>(X, vec, e, pad, c4, A.g);
+    issue_list<D, METRIC, E, P, ACCT>(X, vec, e, pad, c4, A.g);
     u32 r_id = INV;
     float r_key = INF;
     u32 nid = nn;
@@ -1979,11 +2180,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kFastWaves<D
       u64 acc = 0;
       if (nf > 0) {
         float out[P];
-        pass_dists<D, METRIC, E, P>(Q, X, out);
+        if constexpr (kMfma<METRIC, E>) {  // slot 16p + g's product is in lane g of pass p
+          pass_dists_mfma<D, P>(Q, X, out);
 #pragma unroll
-        for (int p = 0; p < P; ++p) {  // the group's sum is complete in its lane 3 (fold8)
-          const float v = __uint_as_float(quad_bcast(__float_as_uint(out[p]), 3));
-          if (c4 == p) my_d = v;
+          for (int p = 0; p < P; ++p) {
+            const float v = __shfl(out[p], g4);
+            if (c4 == p) my_d = v;
+          }
+        } else {
+          pass_dists<D, METRIC, E, P>(Q, X, out);
+#pragma unroll
+          for (int p = 0; p < P; ++p) {  // the group's sum is complete in its lane 3 (fold8)
+            const float v = __uint_as_float(quad_bcast(__float_as_uint(out[p]), 3));
+            if (c4 == p) my_d = v;
+          }
         }
         if (!fresh) my_d = INF;
         if (fresh && my_d != my_d) {  // NaN: the reference's comparisons are all false; no ordered slot exists here
@@ -2036,7 +2246,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kFastWaves<D
       const bool probe = sslot < 0 && in_row && prow != INV;
       const typename VisitedLds<VT>::Hint pword = probe ? vis.probe(prow) : VisitedLds<VT>::unknown();
       const bool seen = probe && vis.home_match(prow, pword);
-      issue_list<D, E, P, ACCT>(X, vec, seen ? INV : prow, pad, c4, A.g);
+      issue_list<D, METRIC, E, P, ACCT>(X, vec, seen ? INV : prow, pad, c4, A.g);
 
       // ---- merge (:456-465 over the whole list at once) ----------------------------------------------------------
       PHASE(6)
@@ -2144,7 +2354,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kFastWaves<D
       if (c != pid) {  // mispredicted (ties / NaN keys): fetch the picked candidate's list and vectors
         EVENT(11)
         erow = c == nid ? nrow : load_row(c);
-        issue_list<D, E, P, ACCT>(X, vec, erow, pad, c4, A.g);
+        issue_list<D, METRIC, E, P, ACCT>(X, vec, erow, pad, c4, A.g);
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this rare path leaves nothing in flight behind the prefetch
       }
       nid = c2 != INV ? c2 : c;
