@@ -72,7 +72,10 @@ def run(name, a):
     kind, n, dim, metric, elem, M, efc, ef, batch, alpha = WORKLOADS[name]
     n = a.n or n
     base_t = D.generate_device(kind, n, seed=1, d=dim)
-    nq = batch * a.nbatches
+    # --per-slot: with slots > 1 every slot answers a whole batch per step (global batch = batch x slots), as bench.py's
+    # sharded leg does, instead of 1/slots of one batch (a GPU of a sharded node runs full launches)
+    bmul = max(int(x) for x in a.slots.split(",")) if a.per_slot else 1
+    nq = batch * bmul * a.nbatches
     q = queries(torch, D, kind, dim, nq, alpha)
     with Heartbeat(f"{name}: ground truth"):
         gt = D.ground_truth_device(base_t, q, a.k, metric)
@@ -102,7 +105,8 @@ def run(name, a):
             for k_, _, v_ in kv:
                 os.environ[k_] = v_
             for rep in range(a.repeat):  # --repeat: the same measurement again on the same handle (warm-state check)
-                for line in run_measure(torch, idx, name, a, q, gt, batch, slots, ef, kind, n, dim, metric, M, efc,
+                gbatch = batch * slots if a.per_slot else batch
+                for line in run_measure(torch, idx, name, a, q, gt, gbatch, slots, ef, kind, n, dim, metric, M, efc,
                                         placement, alpha, nq, elem, st):
                     line["repeat"] = rep
                     line["env"] = env
@@ -243,6 +247,7 @@ def main():
     p.add_argument("--repeat", type=int, default=1)
     p.add_argument("--envs", default="", help="';'-separated variants of comma-separated KEY=VALUE library hooks, "
                                               "measured one after the other on the same handle ('' = defaults)")
+    p.add_argument("--per-slot", action="store_true", help="slots > 1: a whole batch per slot per step")
     p.add_argument("--slots", default="1", help="GPU slots per layout, e.g. 1,8: the same graph as a replica and "
                                                 "as 8 sharded memory-node dumps on this device")
     p.add_argument("--batch-fraction", type=float, default=0.0)
