@@ -1666,13 +1666,16 @@ int knn_enqueue(shine_index* h, shine_request& C, const float* queries, const ui
   // 1,024: the bench's batch; 0 = never split).  Not while the dynamic cache logs a call (its replay orders admissions
   // by query within one launch) or a warmup counts reads: those run as one launch on the slot's own stream.
   const int64_t chunk_env = env_int("SHINE_HOST_CHUNK", kHostChunk);
-  const bool own_stream = C.access || C.dynamic;
   const uint32_t chunk = chunk_env <= 0 ? 0xFFFFFFFFu : static_cast<uint32_t>(std::min<int64_t>(chunk_env, 0x7FFFFFFF));
   for (uint32_t r = 0; r < G; ++r) {
     const uint32_t n = static_cast<uint32_t>(C.part[r].size());
     if (n == 0) continue;
     Replica& R = h->reps[r];
     HIP_TRY(hipSetDevice(R.device));
+    // A synchronous call's share of at most one chunk runs as one launch on the slot's own stream too: the slots' own
+    // streams were created together at open and take distinct hardware queues, where every slot's first host stream
+    // can land on the same one (eight slots of one GPU ran their shares back to back: 3.1 against 1.35 ms a call)
+    const bool own_stream = C.access || C.dynamic || (!C.rotate && n <= chunk);
     // chunks near `chunk` queries, and once there are at least as many as host streams, as many on every stream (the
     // call ends when its longest stream does: 10,000 queries as ten chunks of 1,024 left two of the four streams a
     // chunk behind); a call just past one chunk is not cut into launches too small to fill the GPU
@@ -1732,7 +1735,7 @@ int knn_enqueue(shine_index* h, shine_request& C, const float* queries, const ui
     // A synchronous call starts at stream 0, so that consecutive calls put their chunks on the same streams and each
     // stream's visited tables are learned from the calls before it (capi.cc learned_*_table: per stream); calls in
     // flight together start where the previous one stopped
-    const uint64_t first = C.rotate ? R.hnext : 0;
+    const uint64_t first = C.rotate ? R.hnext + R.slot : 0;  // (slots of one GPU start on different queues)
     if (C.rotate) R.hnext += n_chunks;
     for (uint32_t c = 0, off = 0; off < n; ++c, off += m_chunk) {
       const uint32_t m = std::min(m_chunk, n - off);
