@@ -14,7 +14,7 @@ for W in ${WHICH//,/ }; do
     sift1m_f32) export WORKLOAD=sift1m ROWS=f32; K="search_fast_kernel<128, 0, float, 2,"; T=150 ;;
     sift1m_u8) export WORKLOAD=sift1m ROWS=u8; K="search_fast_kernel<128, 0, unsigned char, 2,"; T=150 ;;
     cfg5_10m_f16) export WORKLOAD=cfg5_10m ROWS=f16; K="search_fast_kernel<200, 1, __half, 4,"; T=300 ;;
-    cfg5_50m_f16) export WORKLOAD=cfg5_10m N=50000000 ROWS=f16 REPS=4; K="search_fast_kernel<200, 1, __half, 4, 2, 0, 0,"; T=420 ;;
+    cfg5_50m_f16) export WORKLOAD=cfg5_10m N=50000000 ROWS=f16 REPS=4; K="search_fast_kernel<200, 1, __half, 4, 2, 0, 3,"; T=420 ;;
     *) echo "unknown workload $W"; exit 1 ;;
   esac
   i=0; mkdir -p $O/$W
