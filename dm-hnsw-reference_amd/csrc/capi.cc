@@ -1517,7 +1517,8 @@ int enqueue_update(shine_index* h, Replica& R) {
   std::memcpy(R.upd_host.p, R.upd_vec.data(), n * sizeof(uint32_t));
   HIP_TRY(hipMemcpyAsync(R.upd.p, R.upd_host.p, n * sizeof(uint32_t), hipMemcpyHostToDevice, R.stream));
   hipError_t e = launch_cache_apply(R.upd.p, R.upd_drop, R.upd_fill, R.upd_cool, R.cslot.p, R.cbits.p, R.cvec.p,
-                                    R.cool.p, R.rlogged.p, reinterpret_cast<const uint8_t*>(h->svec.view[R.slot].va),
+                                    R.cool.p, R.rlogged.p, R.slot_id.p,
+                                    reinterpret_cast<const uint8_t*>(h->svec.view[R.slot].va),
                                     row_bytes(h->dim, h->elem), R.stream);
   if (e != hipSuccess) return set_error(SHINE_ERR_HIP, std::string("cache update: ") + hipGetErrorString(e));
   R.upd_vec.clear();
@@ -2299,6 +2300,7 @@ int shine_set_cache_policy(shine_index_t h, int policy, double ratio_percent, ui
     int rc = 0;
     if ((rc = R.cslot.grow(h->id_space)) || (rc = R.cbits.grow((h->id_space + 31) / 32)) ||
         (rc = R.cvec.grow(entries * vrow)) || (rc = R.cool.grow(entries)) || (rc = R.rlogged.grow(entries)) ||
+        (rc = R.slot_id.grow(entries)) ||
         (rc = R.clog.grow(R.clog_cap)) || (rc = R.rlog.grow(R.rlog_cap)) || (rc = R.logn.grow(2))) {
       R.release_dynamic();
       return rc;
@@ -2307,6 +2309,7 @@ int shine_set_cache_policy(shine_index_t h, int policy, double ratio_percent, ui
     HIP_TRY(hipMemsetAsync(R.cbits.p, 0, (h->id_space + 31) / 32 * sizeof(uint32_t), R.stream));
     HIP_TRY(hipMemsetAsync(R.cool.p, 0, entries * sizeof(uint32_t), R.stream));
     HIP_TRY(hipMemsetAsync(R.rlogged.p, 0xFF, entries * sizeof(uint32_t), R.stream));
+    HIP_TRY(hipMemsetAsync(R.slot_id.p, 0xFF, entries * sizeof(uint32_t), R.stream));
     HIP_TRY(hipMemsetAsync(R.logn.p, 0, 2 * sizeof(uint32_t), R.stream));
     HIP_TRY(hipStreamSynchronize(R.stream));
     R.cache = RecordCache(static_cast<uint32_t>(entries), seed + R.slot, h->inv_size);  // keys: uids < inv_size

@@ -207,7 +207,7 @@ struct Replica {
   hipEvent_t hfork = nullptr;
   DevBuf<unsigned long long> prof;  // SHINE_PHASE_PROFILE diagnostics
   // dynamic record cache (SHINE_CACHE_DYNAMIC): this GPU's arena, lookup table, logs and the host policy engine
-  DevBuf<uint32_t> cslot, cbits, cool, rlog, rlogged, logn, upd;
+  DevBuf<uint32_t> cslot, cbits, cool, rlog, rlogged, slot_id, logn, upd;
   DevBuf<uint8_t> cvec;
   DevBuf<unsigned long long> clog;
   uint32_t clog_cap = 0, rlog_cap = 0, dyn_call = 0;
@@ -226,7 +226,7 @@ struct Replica {
   HostBuf<uint32_t> upd_host;
   bool dev_api_dirty = false;
   void release_dynamic() {
-    for (auto* b : {&cslot, &cbits, &cool, &rlog, &rlogged, &logn, &upd}) b->release();
+    for (auto* b : {&cslot, &cbits, &cool, &rlog, &rlogged, &slot_id, &logn, &upd}) b->release();
     cvec.release();
     clog.release();
     upd_host.release();

@@ -30,12 +30,13 @@ struct DevGraph {
   // offers a cooling entry its second chance (cache.hh:128-132: the device id goes to rlog), a miss reads over xGMI
   // and is offered for admission through clog (entry point and upper levels always, level-0 reads while the cache is
   // not full or when their coin passes, hnsw.hh:447-448).
-  const uint32_t* cslot;      // [id space]: arena slot of device id x, or 0xFFFFFFFF
+  const uint32_t* cslot;      // [id space]: arena slot of device id x with the entry's cooling flag in bit 31, or
+                              // 0xFFFFFFFF (the flag travels with the slot: one dependent read for both)
   const uint32_t* cbits;      // [id space / 32]: bit x set while x is cached — read before cslot, so that a miss
                               // (most off-stripe reads) costs one read of a bitmap 1/32 of cslot's size, which stays
                               // in the caches, instead of a cslot read from HBM ahead of its xGMI read
   const void* cvec;           // [arena slots][row]: cached vectors, device row layout
-  uint32_t* cool;             // [arena slots]: 1 while the entry is cooling
+  uint32_t* cool;             // [arena slots]: 1 while the entry is cooling (the host's copy; kernels read cslot's bit)
   unsigned long long* clog;   // admission candidates: (query << 32) | x | always << 31 | coin << 63
   uint32_t* clog_n;           // [0] candidates logged (may exceed clog_cap: the overflow is counted, not stored);
                               // [1] hits on cooling entries logged
@@ -265,8 +266,8 @@ hipError_t radix_sort_u32_pairs(void* temp, size_t* temp_bytes, const uint32_t* 
 // their arena slots and point cslot at them; set the cooling flags.  upd = [drop ids (n_drop) | (slot, id) pairs
 // (n_fill) | (slot, flag) pairs (n_cool)].
 hipError_t launch_cache_apply(const uint32_t* upd, uint32_t n_drop, uint32_t n_fill, uint32_t n_cool, uint32_t* cslot,
-                              uint32_t* cbits, uint8_t* cvec, uint32_t* cool, uint32_t* rlogged, const uint8_t* vec,
-                              uint64_t row_bytes, hipStream_t s);
+                              uint32_t* cbits, uint8_t* cvec, uint32_t* cool, uint32_t* rlogged, uint32_t* slot_id,
+                              const uint8_t* vec, uint64_t row_bytes, hipStream_t s);
 
 // Diagnostics: replay push / pop / push_k sequences through the device heap routines (one wavefront).
 hipError_t launch_heap_replay(int is_max, const int32_t* ops, const float* vals, const uint32_t* ids, uint32_t n_ops,

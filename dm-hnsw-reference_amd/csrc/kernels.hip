@@ -70,10 +70,11 @@ __global__ __launch_bounds__(256) void cache_drop_kernel(const uint32_t* ids, ui
   }
 }
 
-// one workgroup per admitted record: its row into the arena slot (4-byte words; rows are whole words), then cslot
+// one workgroup per admitted record: its row into the arena slot (4-byte words; rows are whole words), then cslot (the
+// slot, not cooling) and the slot's occupant
 __global__ __launch_bounds__(64) void cache_fill_kernel(const uint32_t* pairs, uint32_t* cslot, uint32_t* cbits,
-                                                        uint8_t* cvec, uint32_t* rlogged, const uint8_t* vec,
-                                                        uint64_t row_bytes) {
+                                                        uint8_t* cvec, uint32_t* rlogged, uint32_t* slot_id,
+                                                        const uint8_t* vec, uint64_t row_bytes) {
   const uint32_t slot = pairs[2 * blockIdx.x], id = pairs[2 * blockIdx.x + 1];
   const uint32_t* src = reinterpret_cast<const uint32_t*>(vec + static_cast<uint64_t>(id) * row_bytes);
   uint32_t* dst = reinterpret_cast<uint32_t*>(cvec + static_cast<uint64_t>(slot) * row_bytes);
@@ -82,28 +83,37 @@ __global__ __launch_bounds__(64) void cache_fill_kernel(const uint32_t* pairs, u
     cslot[id] = slot;
     atomicOr(&cbits[id >> 5], 1u << (id & 31));
     rlogged[slot] = 0xFFFFFFFFu;  // a new occupant: its first cooling hit of the epoch is logged
+    slot_id[slot] = id;
   }
 }
 
-__global__ __launch_bounds__(256) void cache_cool_kernel(const uint32_t* pairs, uint32_t n, uint32_t* cool) {
+// the cooling flags: the arena's flag array, and bit 31 of the occupant's cslot word (the search kernels read the flag
+// with the slot, kernels_impl.h kCool)
+__global__ __launch_bounds__(256) void cache_cool_kernel(const uint32_t* pairs, uint32_t n, uint32_t* cool,
+                                                         const uint32_t* slot_id, uint32_t* cslot) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  if (i < n) cool[pairs[2 * i]] = pairs[2 * i + 1];
+  if (i < n) {
+    const uint32_t slot = pairs[2 * i], flag = pairs[2 * i + 1];
+    cool[slot] = flag;
+    const uint32_t id = slot_id[slot];
+    if (id != 0xFFFFFFFFu && (cslot[id] & 0x7FFFFFFFu) == slot) cslot[id] = slot | (flag ? 0x80000000u : 0u);
+  }
 }
 
 }  // namespace
 
 hipError_t launch_cache_apply(const uint32_t* upd, uint32_t n_drop, uint32_t n_fill, uint32_t n_cool, uint32_t* cslot,
-                              uint32_t* cbits, uint8_t* cvec, uint32_t* cool, uint32_t* rlogged, const uint8_t* vec,
-                              uint64_t row_bytes, hipStream_t s) {
+                              uint32_t* cbits, uint8_t* cvec, uint32_t* cool, uint32_t* rlogged, uint32_t* slot_id,
+                              const uint8_t* vec, uint64_t row_bytes, hipStream_t s) {
   // drops before fills (a record may leave one slot and enter another in the same update: its bit ends set)
   if (n_drop)
     hipLaunchKernelGGL(cache_drop_kernel, dim3((n_drop + 255) / 256), dim3(256), 0, s, upd, n_drop, cslot, cbits);
   if (n_fill)
-    hipLaunchKernelGGL(cache_fill_kernel, dim3(n_fill), dim3(64), 0, s, upd + n_drop, cslot, cbits, cvec, rlogged, vec,
-                       row_bytes);
+    hipLaunchKernelGGL(cache_fill_kernel, dim3(n_fill), dim3(64), 0, s, upd + n_drop, cslot, cbits, cvec, rlogged, slot_id,
+                       vec, row_bytes);
   if (n_cool)
     hipLaunchKernelGGL(cache_cool_kernel, dim3((n_cool + 255) / 256), dim3(256), 0, s, upd + n_drop + 2 * n_fill,
-                       n_cool, cool);
+                       n_cool, cool, slot_id, cslot);
   return hipGetLastError();
 }
 

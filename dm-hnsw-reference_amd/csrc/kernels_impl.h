@@ -508,14 +508,25 @@ __device__ __forceinline__ void load_byte_row(NbrBuf<D, E, P>& B, int p, const E
 }
 
 // Off-stripe record x of a dynamic-cache view (DevGraph::cbits, cslot): its arena row when cached, else its xGMI row.
+// A cslot word is the arena slot with the entry's cooling flag in bit 31 (kCool), INV when x is not cached.
+constexpr u32 kCool = 0x80000000u;
 __device__ __forceinline__ u32 read_class(const DevGraph& g, u32 x, u32 cached);
 template <int D, typename E>
 __device__ __forceinline__ const E* cached_row(const DevGraph& g, const E* row, u32 x) {
   if (read_class(g, x, 0u) == 2u && ((g.cbits[x >> 5] >> (x & 31)) & 1u)) {
     const u32 c = g.cslot[x];
-    if (c != INV) return static_cast<const E*>(g.cvec) + static_cast<u64>(c) * kRowElems<D, E>;
+    if (c != INV) return static_cast<const E*>(g.cvec) + static_cast<u64>(c & ~kCool) * kRowElems<D, E>;
   }
   return row;
+}
+// The cache word of a level-0 list entry, looked up once where the list arrives (the fast kernel carries it from the
+// row request to the read accounting): INV for an empty slot, a record of this GPU's stripe, or one not cached.
+__device__ __forceinline__ u32 cache_word(const DevGraph& g, u32 x) {
+  return x != INV && read_class(g, x, 0u) == 2u ? g.cslot[x] : INV;
+}
+template <int D, typename E>
+__device__ __forceinline__ const E* word_row(const DevGraph& g, const E* row, u32 w) {
+  return w != INV ? static_cast<const E*>(g.cvec) + static_cast<u64>(w & ~kCool) * kRowElems<D, E> : row;
 }
 
 // Issue the loads of pass p: this lane's group evaluates node `id` (INV: nothing to load).  CACHE (the ACCT = 2 kernels
@@ -876,23 +887,26 @@ __device__ __forceinline__ bool admission_coin(unsigned long long seed, u32 call
 // vector reads of the lanes with `active` set (each reads record x; `always`: an entry-point or upper-level read,
 // admitted without the coin).  ACCT = 0 (replica, no warmup) compiles the accounting out of the search loop; ACCT = 2
 // adds the dynamic cache's lookups and logs (DevGraph::cslot).
+// (w: the entry's cache word when the caller looked it up already, kNoWord to look it up here)
+constexpr u32 kNoWord = 0xFFFFFFFEu;
 template <int ACCT>
 __device__ __forceinline__ void count_vec_reads(const SearchArgs& A, ReadCount& rc, bool active, u32 x, u32 qi = 0,
-                                                bool always = false) {
+                                                bool always = false, u32 w = kNoWord) {
   if constexpr (!ACCT) return;
   if (A.g.sharded) {
     u32 c = active ? read_class(A.g, x, A.g.cached_rows) : 0u;
     if constexpr (ACCT == 2) {
       if (c == 2u) {
-        const u32 slot = ((A.g.cbits[x >> 5] >> (x & 31)) & 1u) ? A.g.cslot[x] : INV;
-        if (slot != INV) {
+        const u32 word = w != kNoWord ? w : ((A.g.cbits[x >> 5] >> (x & 31)) & 1u) ? A.g.cslot[x] : INV;
+        if (word != INV) {
+          const u32 slot = word & ~kCool;
           c = 1u;
           // a hit on a cooling entry: its second chance (cache.hh:128-132) is the host's to give, so the hit is logged
           // by device id and the flag is left as the host engine set it: the flags on the device always equal the
           // engine's after its last update, which is what lets the updates trail the calls (capi.cc replay).  The
           // host takes each key once, so each slot logs once per log epoch (the plain read filters repeat hits
           // before the exchange that decides): the log holds at most one entry per arena slot and cannot overflow
-          if (A.g.cool[slot]) {
+          if (word & kCool) {
             const u32 ep = A.g.dyn_epoch;
             if (A.g.rlogged[slot] != ep && atomicExch(&A.g.rlogged[slot], ep) != ep) {
               const u32 i = atomicAdd(&A.g.clog_n[1], 1u);
@@ -1967,16 +1981,16 @@ __device__ __forceinline__ u32 quad_bcast(u32 x, int p) {  // lane 4g + p's valu
   }
 }
 
+// w: the dynamic cache's word of this lane's entry (ACCT = 2: cache_word, looked up when the list arrived)
 template <int D, int METRIC, typename E, int P, int ACCT>
-__device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restrict__ vec, u32 e, u32 pad, int c4,
+__device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restrict__ vec, u32 e, u32 w, u32 pad, int c4,
                                            const DevGraph& g) {
   if constexpr (kMfma<METRIC, E>) {
     // fp16 inner products (pass_dists_mfma): lane l reads chunk l >> 4 of slot 16p + (l & 15), whose entry sits in lane
     // 4 (l & 15) + p of the list (one ds_bpermute per pass for the id, or the dynamic cache's resolved row address)
     const int lane = static_cast<int>(threadIdx.x), src = 4 * (lane & 15), c = lane >> 4;
     if constexpr (ACCT == 2) {
-      const E* row = vec + static_cast<u64>(e == INV ? pad : e) * kRowElems<D, E>;
-      if (e != INV) row = cached_row<D, E>(g, row, e);
+      const E* row = word_row<D, E>(g, vec + static_cast<u64>(e == INV ? pad : e) * kRowElems<D, E>, e == INV ? INV : w);
       const u64 rp = reinterpret_cast<u64>(row);
 #pragma unroll
       for (int p = 0; p < P; ++p) {
@@ -1994,8 +2008,7 @@ __device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restri
     return;
   }
   if constexpr (ACCT == 2) {  // dynamic cache: each lane resolves its own list slot to a row, the groups share it
-    const E* row = vec + static_cast<u64>(e == INV ? pad : e) * kRowElems<D, E>;
-    if (e != INV) row = cached_row<D, E>(g, row, e);
+    const E* row = word_row<D, E>(g, vec + static_cast<u64>(e == INV ? pad : e) * kRowElems<D, E>, e == INV ? INV : w);
     const u64 rp = reinterpret_cast<u64>(row);
 #pragma unroll
     for (int p = 0; p < P; ++p) {
@@ -2089,7 +2102,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kFastWaves<D
     // prefetched list.  X is refilled for the next candidate as soon as the current distances have consumed it.
     NbrBuf<D, E, P> X;
     u32 e = load_row(status == 0 ? nn : pad);
-    issue_list<D, METRIC, E, P, ACCT>(X, vec, e, pad, c4, A.g);
+    // ACCT = 2: the cache words of list e's entries (cache_word), looked up once per list and carried from its rows'
+    // request to its read accounting; ncs: those of nrow, looked up after the distances, before the rows are requested
+    u32 ecs = ACCT == 2 ? cache_word(A.g, e) : INV;
+    u32 ncs = INV;
+    issue_list<D, METRIC, E, P, ACCT>(X, vec, e, ecs, pad, c4, A.g);
     u32 r_id = INV;
     float r_key = INF;
     u32 nid = nn;
@@ -2170,7 +2187,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kFastWaves<D
       }
       const u64 fm = __ballot(fresh);
       const int nf = __popcll(fm);
-      count_vec_reads<ACCT>(A, rc, fresh, e, qi);
+      count_vec_reads<ACCT>(A, rc, fresh, e, qi, false, ACCT == 2 ? ecs : kNoWord);
       nvis += nf;
       st_vl0 += nf;
       st_dist += nf;
@@ -2225,6 +2242,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kFastWaves<D
       // runner-up r; its vectors are requested here, one issue point for every path, into the buffer the
       // distances above have just consumed
       PHASE(4)
+      if constexpr (ACCT == 2) ncs = cache_word(A.g, nrow);  // (the runner-up's list: requested one expansion ago)
       u32 pid = r_id;
       if (acc) {
         const float fstar = wave_min(((acc >> lane) & 1ull) ? my_d : INF);
@@ -2246,7 +2264,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kFastWaves<D
       const bool probe = sslot < 0 && in_row && prow != INV;
       const typename VisitedLds<VT>::Hint pword = probe ? vis.probe(prow) : VisitedLds<VT>::unknown();
       const bool seen = probe && vis.home_match(prow, pword);
-      issue_list<D, METRIC, E, P, ACCT>(X, vec, seen ? INV : prow, pad, c4, A.g);
+      const u32 pcs = ACCT == 2 ? (pid == r_id ? ncs : cache_word(A.g, prow)) : INV;
+      issue_list<D, METRIC, E, P, ACCT>(X, vec, seen ? INV : prow, pcs, pad, c4, A.g);
 
       // ---- merge (:456-465 over the whole list at once) ----------------------------------------------------------
       PHASE(6)
@@ -2350,16 +2369,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kFastWaves<D
           k2 = r == r2 ? kr : k2;
         }
       }
-      u32 erow = prow;
+      u32 erow = prow, ecsn = pcs;
       if (c != pid) {  // mispredicted (ties / NaN keys): fetch the picked candidate's list and vectors
         EVENT(11)
         erow = c == nid ? nrow : load_row(c);
-        issue_list<D, METRIC, E, P, ACCT>(X, vec, erow, pad, c4, A.g);
+        if constexpr (ACCT == 2) ecsn = c == nid ? ncs : cache_word(A.g, erow);
+        issue_list<D, METRIC, E, P, ACCT>(X, vec, erow, ecsn, pad, c4, A.g);
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this rare path leaves nothing in flight behind the prefetch
       }
       nid = c2 != INV ? c2 : c;
       nrow = load_row(nid);  // unconditional: always the youngest load
       e = erow;
+      ecs = ecsn;
       ehint = c != pid ? VisitedLds<VT>::unknown() : pword;  // the probe read prow's home bucket, no insert since
       ehint_known = c == pid && sslot < 0;
       cur = c;
