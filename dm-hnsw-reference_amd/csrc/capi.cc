@@ -562,7 +562,8 @@ bool vt3_usable(const shine_index* h) {
 // per CU) 1.41 M QPS, 0.7 (5,952, 6) 1.81 M, 0.85 (4,928, 7) 1.82 M once no call hands queries on; exact 0.6 0.63 M, 0.7
 // 0.61 M (linear-probed u32 at 0.45: 1.42 M / 0.41 M).
 uint32_t vt3_load_permille(bool fast) {
-  return static_cast<uint32_t>(std::min<int64_t>(950, std::max<int64_t>(100, env_int("SHINE_VT3_LOAD", fast ? 700 : 600))));
+  const int64_t v = fast ? env_int("SHINE_VT3_LOAD", 700) : env_int("SHINE_VT3_EXACT_LOAD", env_int("SHINE_VT3_LOAD", 600));
+  return static_cast<uint32_t>(std::min<int64_t>(950, std::max<int64_t>(100, v)));
 }
 
 // Words per spill / fallback slot: the id-space bitmap, or at least the largest hash table; a multiple of 4 words, so
