@@ -210,7 +210,7 @@ def parse():
     p.add_argument("--mode", choices=["fast", "exact", "both"], default="both",
                    help="search mode(s); the first one measured gives `value` (fast, then exact with 'both')")
     p.add_argument("--cache", default=os.environ.get("SHINE_BENCH_CACHE", "/tmp/shine_bench"))
-    p.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r05" / "pmc" / "sift1m_f32_pmc.json"),
+    p.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r06" / "final" / "sift1m_f32_pmc.json"),
                    help="per-launch HBM bytes of the search kernel measured by rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                         "passes of this bench (tools/pmc.py; tools/gpu_round.sh)")
     p.add_argument("--no-host", action="store_true", help="skip the host-to-host and host-API legs")
