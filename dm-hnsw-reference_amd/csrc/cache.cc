@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <chrono>
 #include <new>
 
 namespace shine {
@@ -83,7 +84,7 @@ RecordCache::RecordCache(uint32_t entries, uint64_t seed, uint32_t key_space)
       cooling_(entries) {
   modB_ = FastMod(B_);
   modCT_ = FastMod(CT_);
-  for (uint32_t n = 1; n <= kInPlace; ++n) mod_n_[n] = FastMod(n);
+  mod60_ = FastMod(60);
   for (uint32_t i = 0; i < kAhead; ++i) push_draw(i);
   std::fill(key_of_.data(), key_of_.data() + entries, kInv);
   std::fill(dev_of_.data(), dev_of_.data() + entries, kInv);
@@ -104,16 +105,32 @@ uint64_t RecordCache::next_draw() {
 }
 
 void RecordCache::push_draw(uint32_t slot) {
-  ring_[slot] = next_draw();
-  if (C_) __builtin_prefetch(brec(static_cast<uint32_t>(modB_(ring_[slot]))));
+  Draw& d = ring_[slot];
+  d.v = next_draw();
+  d.b = static_cast<uint32_t>(modB_(d.v));
+  d.r60 = static_cast<uint32_t>(mod60_(d.v));
+  if (C_) __builtin_prefetch(brec(d.b));
 }
 
-uint64_t RecordCache::rand() {
-  const uint64_t v = ring_[head_];
+RecordCache::Draw RecordCache::rand() {
+  const Draw d = ring_[head_];
   push_draw(head_);
   head_ = head_ + 1 == kAhead ? 0u : head_ + 1;
-  return v;
+  return d;
 }
+
+namespace {
+struct Pick60 {
+  uint8_t t[60][6];
+  constexpr Pick60() : t() {
+    for (int r = 0; r < 60; ++r)
+      for (int n = 1; n < 6; ++n) t[r][n] = static_cast<uint8_t>(r % n);
+  }
+};
+constexpr Pick60 kPick60Table{};
+}  // namespace
+
+const uint8_t (&RecordCache::kPick60)[60][RecordCache::kInPlace + 1] = kPick60Table.t;
 
 uint32_t RecordCache::bucket_of(uint32_t key) const { return static_cast<uint32_t>(modB_(murmur64(key))); }
 uint32_t RecordCache::cool_of(uint32_t key) const { return static_cast<uint32_t>(modCT_(splitmix(key))); }
@@ -210,60 +227,72 @@ bool RecordCache::ct_remove(uint32_t key) {  // cooling_table.hh:52-75
   uint32_t i = 0;
   while (i < r[0] && r[1 + i] != key) ++i;
   if (i == r[0]) return false;
-  for (uint32_t j = i; j + 1 < r[0]; ++j) r[1 + j] = r[2 + j];
+  for (uint32_t j = i; j + 1 < r[0]; ++j) {
+    r[1 + j] = r[2 + j];
+    r[kCB + j] = r[kCB + 1 + j];
+  }
   --r[0];
   return true;
 }
 
-bool RecordCache::ct_insert(uint32_t key, uint32_t& victim) {  // cooling_table.hh:81-98
-  uint32_t* r = &ct_[static_cast<size_t>(cool_of(key)) * kCW];
+bool RecordCache::ct_insert(uint32_t key, uint32_t b, uint32_t c, uint32_t& victim, uint32_t& vbucket) {
+  uint32_t* r = &ct_[static_cast<size_t>(c) * kCW];  // cooling_table.hh:81-98
   bool pushed = false;
   if (r[0] == kCoolingBucketEntries) {  // the oldest (last) key leaves
     victim = r[kCoolingBucketEntries];
+    vbucket = r[kCB + kCoolingBucketEntries - 1];
     --r[0];
     pushed = true;
   }
-  for (uint32_t j = r[0]; j > 0; --j) r[1 + j] = r[j];  // newest first
+  for (uint32_t j = r[0]; j > 0; --j) {  // newest first
+    r[1 + j] = r[j];
+    r[kCB + j] = r[kCB + j - 1];
+  }
   r[1] = key;
+  r[kCB] = b;
   ++r[0];
   return pushed;
 }
 
 // The draw i ahead of the stream without taking it (1 <= i <= kAhead; prefetch hints only).
-uint64_t RecordCache::peek(uint32_t i) const { return ring_[(head_ + i - 1) % kAhead]; }
+const RecordCache::Draw& RecordCache::peek(uint32_t i) const { return ring_[(head_ + i - 1) % kAhead]; }
 
 // The next pick of the eviction scan, read ahead (its bucket's line was requested kAhead draws earlier): when the
-// step will start an entry cooling, its cooling-table bucket and — when that bucket is full — the hash bucket of the
-// key it would push out are requested now, so that the victim lookup, the scan's one dependent miss, overlaps this
-// step's.  A hint only: the step itself re-reads everything.
-void RecordCache::lookahead() const {
-  const uint32_t* r = brec(static_cast<uint32_t>(modB_(peek(1))));
+// step will start an entry cooling, its cooling-table bucket is computed now (kept for that step: cool_bucket) and —
+// when that bucket is full — the hash record of the key it would push out is requested, so that the victim lookup,
+// the scan's one dependent miss, overlaps this step's.  A hint only: the step itself re-reads everything.
+void RecordCache::lookahead() {
+  const Draw& d1 = peek(1);
+  const uint32_t* r = brec(d1.b);
   const uint32_t n = bcount(r);
   if (n == 0 || n > kInPlace) return;
-  const uint32_t i = static_cast<uint32_t>(mod_n_[n](peek(2)));
+  const uint32_t i = pick(peek(2), n);
   if ((r[0] >> (16 + i)) & 1u) return;  // already cooling: the step changes nothing
-  const uint32_t* c = &ct_[static_cast<size_t>(cool_of(r[1 + 3 * i])) * kCW];
-  if (c[0] == kCoolingBucketEntries) __builtin_prefetch(brec(bucket_of(c[kCoolingBucketEntries])));
+  memo_key_ = r[1 + 3 * i];
+  memo_cool_ = cool_of(memo_key_);
+  const uint32_t* c = &ct_[static_cast<size_t>(memo_cool_) * kCW];
+  if (c[0] == kCoolingBucketEntries) __builtin_prefetch(brec(c[kCB + kCoolingBucketEntries - 1]));
 }
 
 RecordCache::Victim RecordCache::evict() {  // cache.hh:232-311
   for (;;) {
-    const uint32_t b = static_cast<uint32_t>(modB_(rand()));  // (its bucket was requested kAhead draws ago)
+    ++scan_steps;
+    const uint32_t b = rand().b;  // (its record was requested kAhead draws ago)
     const uint32_t n = bcount(brec(b));
     if (n == 0) continue;
-    const uint32_t i = static_cast<uint32_t>(n <= kInPlace ? mod_n_[n](rand()) : rand() % n);
+    const uint32_t i = pick(rand(), n);
     const Ent e = bget(b, i);
+    const uint32_t cb = e.cool ? 0u : cool_bucket(e.key);  // (before the look-ahead overwrites its memo)
     lookahead();
-    uint32_t victim = kInv;
+    uint32_t victim = kInv, vb = 0;
     bool has_victim = false;
     if (!e.cool) {  // hot -> cooling; the table may push its oldest key out
-      has_victim = ct_insert(e.key, victim);
+      has_victim = ct_insert(e.key, b, cb, victim, vb);
       bset_cool(b, i, true);
       cooling_[e.slot] = 1;
       if (flagged_) flagged_->push_back(e.slot);
     }
     if (!has_victim) continue;
-    const uint32_t vb = bucket_of(victim);
     Ent v;
     const int vi = bfind(vb, victim, v);
     if (vi < 0 || !v.cool) continue;  // rescued meanwhile: no eviction
@@ -325,6 +354,10 @@ void sort_candidates(std::vector<CacheCandidate>& c) {
 void RecordCache::apply_call(std::vector<uint32_t> rescued_keys, std::vector<CacheCandidate> candidates,
                              std::vector<CacheUpdate>& updates, std::vector<uint32_t>& flagged) {
   if (C_ == 0) return;
+  using clk = std::chrono::steady_clock;
+  auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+  const clk::time_point t0 = clk::now();
+  scan_steps = 0;
   flagged_ = &flagged;
   if (!std::is_sorted(rescued_keys.begin(), rescued_keys.end())) std::sort(rescued_keys.begin(), rescued_keys.end());
   rescued_keys.erase(std::unique(rescued_keys.begin(), rescued_keys.end()), rescued_keys.end());
@@ -348,7 +381,9 @@ void RecordCache::apply_call(std::vector<uint32_t> rescued_keys, std::vector<Cac
       ++rescued;
     }
   }
+  const clk::time_point t1 = clk::now();
   sort_candidates(candidates);  // (query, key): a query offers a key once, so the order is total
+  const clk::time_point t2 = clk::now();
   const size_t nc = candidates.size();
   for (size_t i = 0; i < nc; ++i) {
     if (i + kLookAhead < nc && candidates[i + kLookAhead].key < key_space_)
@@ -358,6 +393,10 @@ void RecordCache::apply_call(std::vector<uint32_t> rescued_keys, std::vector<Cac
     if (c.always || !full() || c.coin) insert(c.key, c.dev_id, updates);
   }
   flagged_ = nullptr;
+  const clk::time_point t3 = clk::now();
+  ms_rescue = ms(t0, t1);
+  ms_sort = ms(t1, t2);
+  ms_admit = ms(t2, t3);
 }
 
 std::vector<uint32_t> RecordCache::keys() const {

@@ -101,20 +101,39 @@ class RecordCache {
   bool cooling(uint32_t slot) const { return slot < cooling_.size() && cooling_[slot] != 0; }
 
   uint64_t admitted = 0, evicted = 0, rescued = 0;
+  // diagnostics of the last apply_call (SHINE_DEBUG_CACHE_TIMING): eviction-scan steps, and the ms of its second
+  // chances, of the candidates' sort and of the admissions
+  uint64_t scan_steps = 0;
+  double ms_rescue = 0, ms_sort = 0, ms_admit = 0;
 
  private:
-  uint64_t rand();                    // the next draw of the stream
-  uint64_t peek(uint32_t i) const;    // the draw i ahead (1 <= i <= kAhead), not taken
+  // A draw of the stream with what the scan derives from it, computed when it enters the ring (kAhead draws before it
+  // is taken, off the scan's chain of dependent steps): the bucket it picks (v % B) and v % 60, which gives the pick of
+  // an entry in a bucket of n <= 5 entries as (v % 60) % n (every such n divides 60) by a table read.
+  struct Draw {
+    uint64_t v;
+    uint32_t b;
+    uint32_t r60;
+  };
+  Draw rand();                        // the next draw of the stream
+  const Draw& peek(uint32_t i) const; // the draw i ahead (1 <= i <= kAhead), not taken
   uint64_t next_draw();               // SplitMix64 step: the draw kAhead ahead of rand()'s
   void push_draw(uint32_t slot);      // ring slot <- the next draw, its bucket requested
+  uint32_t pick(const Draw& d, uint32_t n) const {  // d.v % n, the entry a draw picks in a bucket of n
+    return n <= kInPlace ? kPick60[d.r60][n] : static_cast<uint32_t>(d.v % n);
+  }
+  uint32_t cool_bucket(uint32_t key) {  // cool_of(key), from the look-ahead's memo when it computed it
+    return key == memo_key_ ? memo_cool_ : cool_of(key);
+  }
   struct Victim {
     uint32_t slot, dev;
   };
   Victim evict();  // cache.hh:232-311: frees one slot (and names the device id that leaves it)
-  void lookahead() const;
+  void lookahead();
   void insert(uint32_t key, uint32_t dev, std::vector<CacheUpdate>& updates);
   bool ct_remove(uint32_t key);
-  bool ct_insert(uint32_t key, uint32_t& victim);
+  // key (home bucket b, cooling bucket c) in; when the cooling bucket was full its oldest key leaves: victim, vbucket
+  bool ct_insert(uint32_t key, uint32_t b, uint32_t c, uint32_t& victim, uint32_t& vbucket);
 
   // Hash buckets as flat 64-byte records, one cache line each: [count | cooling bits << 16, (key, slot, device id) x 5]
   // in insertion order.  A lookup, the eviction scan's random pick with its cooling flag, and an erase with the
@@ -122,8 +141,11 @@ class RecordCache {
   // scan's path (the policy is a chain of dependent misses; each array read on it was one more).  A bucket holds 5
   // entries in place and the rare rest (Poisson(1) occupancy: ~6e-4 of the buckets) in `bover_` as (key, slot,
   // device, cooling) in order.  The slot arrays below are written on the way for the callers' per-slot reads.
-  // Cooling-table buckets: 8-word records [count, up to 6 keys newest first].
-  static constexpr uint32_t kBW = 16, kInPlace = 5, kCW = 8;
+  // Cooling-table buckets: 16-word records [count, up to 6 keys newest first, their hash buckets in the same order]:
+  // the key a full bucket pushes out comes with its hash bucket, so the scan reads the victim's record without hashing
+  // it first (and the look-ahead requests that record one step early).
+  static constexpr uint32_t kBW = 16, kInPlace = 5, kCW = 16, kCB = 7;
+  static const uint8_t (&kPick60)[60][kInPlace + 1];  // [v % 60][n] = v % n
   struct Ent {
     uint32_t key, slot, dev;
     bool cool;
@@ -140,13 +162,14 @@ class RecordCache {
   void berase(uint32_t b, uint32_t i);  // entry i out, the others in order (vector::erase in the reference's Bucket)
 
   uint32_t C_ = 0, B_ = 1, CT_ = 1, next_idx_ = 0, key_space_ = 0;
-  FastMod modB_, modCT_, mod_n_[kInPlace + 1];  // % B_, % CT_, % n for in-place bucket sizes n
+  FastMod modB_, modCT_, mod60_;  // % B_, % CT_, % 60
   uint64_t state_ = 0;
   // the next kAhead draws, computed once each with their hash bucket (a draw picks a bucket, or an entry of one): each
   // bucket is requested kAhead draws before the eviction scan may read it
   static constexpr uint32_t kAhead = 8;
-  uint64_t ring_[kAhead] = {};
+  Draw ring_[kAhead] = {};
   uint32_t head_ = 0;
+  uint32_t memo_key_ = 0xFFFFFFFFu, memo_cool_ = 0;  // the look-ahead's cool_of(memo_key_)
   HugeArray<uint32_t> bk_;  // [B_][kBW] (page-aligned: records on cache-line boundaries)
   std::unordered_map<uint32_t, std::vector<uint32_t>> bover_;  // bucket -> (key, slot, dev, cool) past kInPlace
   HugeArray<uint32_t> ct_;                                     // [CT_][kCW]

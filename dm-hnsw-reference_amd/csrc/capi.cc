@@ -62,7 +62,7 @@ DevGraph dev_graph(const shine_index* h, const Replica& r) {
     g.rlog_cap = r.rlog_cap;
     g.rlogged = r.rlogged.p;
     g.dyn_epoch = r.log_epoch;
-    g.dyn_full = r.cache.full() ? 1u : 0u;
+    g.dyn_full = r.dyn_full ? 1u : 0u;
     g.dyn_call = r.dyn_call;
     g.dyn_seed = h->cache_seed + r.slot;
   }
@@ -1391,16 +1391,16 @@ int fetch_logs(shine_index* h) {
 
 // Host only (no HIP call): safe on a thread per slot while the main thread waits.
 void replay(const shine_index* h, Replica& R, shine_stats* agg) {
-  if (R.pend_clog.empty() && R.pend_rlog.empty()) return;
+  if (R.rp_clog.empty() && R.rp_rlog.empty()) return;
   const auto t0 = std::chrono::steady_clock::now();
   // hits on cooling entries (by device id, every hit logged): each key once, deduplicated in an open-addressed set over
   // twice the log (a sort of the raw log was most of this step), then sorted by the engine
   std::vector<uint32_t> rescued_keys;
   {
     uint32_t rmask = 63;
-    while (rmask + 1 < 2 * R.pend_rlog.size()) rmask = 2 * rmask + 1;
+    while (rmask + 1 < 2 * R.rp_rlog.size()) rmask = 2 * rmask + 1;
     std::vector<uint32_t> seen(rmask + 1, kInvalid);
-    for (uint32_t x : R.pend_rlog) {
+    for (uint32_t x : R.rp_rlog) {
       if (x >= h->uid_of_dev.size()) continue;
       uint32_t q = (x * 0x9E3779B1u) & rmask;
       while (seen[q] != kInvalid && seen[q] != x) q = (q + 1) & rmask;
@@ -1409,9 +1409,9 @@ void replay(const shine_index* h, Replica& R, shine_stats* agg) {
       rescued_keys.push_back(h->uid_of_dev[x]);
     }
   }
-  std::vector<CacheCandidate> cand(R.pend_clog.size());
+  std::vector<CacheCandidate> cand(R.rp_clog.size());
   for (size_t i = 0; i < cand.size(); ++i) {
-    const unsigned long long e = R.pend_clog[i];
+    const unsigned long long e = R.rp_clog[i];
     CacheCandidate& c = cand[i];
     c.query = static_cast<uint32_t>(e >> 32) & 0x7FFFFFFFu;
     c.dev_id = static_cast<uint32_t>(e) & 0x7FFFFFFFu;
@@ -1484,18 +1484,19 @@ void replay(const shine_index* h, Replica& R, shine_stats* agg) {
   if (env_int("SHINE_DEBUG_CACHE_TIMING", 0) > 1) {  // diagnostics: the replay's parts on this slot
     auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     std::fprintf(stderr, "replay slot %u: %zu candidates, %zu rescued keys, %zu updates: logs %.3f policy %.3f "
-                 "updates %.3f ms\n", R.slot, n_cand, n_resc, ups.size(), ms(t0, t1), ms(t1, t2),
-                 ms(t2, std::chrono::steady_clock::now()));
+                 "(second chances %.3f, sort %.3f, admissions %.3f, %llu scan steps) updates %.3f ms\n", R.slot, n_cand,
+                 n_resc, ups.size(), ms(t0, t1), ms(t1, t2), R.cache.ms_rescue, R.cache.ms_sort, R.cache.ms_admit,
+                 static_cast<unsigned long long>(R.cache.scan_steps), ms(t2, std::chrono::steady_clock::now()));
   }
   if (agg) {
     agg->cache_admitted += R.cache.admitted - a0;
     agg->cache_evicted += R.cache.evicted - e0;
     agg->cache_rescued += R.cache.rescued - r0;
-    agg->cache_log_dropped += R.pend_lost;
+    agg->cache_log_dropped += R.rp_lost;
   }
-  R.pend_clog.clear();
-  R.pend_rlog.clear();
-  R.pend_lost = 0;
+  R.rp_clog.clear();
+  R.rp_rlog.clear();
+  R.rp_lost = 0;
 }
 
 // The replayed updates onto the slot's stream (from pinned host memory: the stream is synchronized before the next
@@ -1527,15 +1528,71 @@ int enqueue_update(shine_index* h, Replica& R) {
   return 0;
 }
 
+// The slots whose fetched logs await a replay, their logs handed to it (rp_*): the next call's logs can be fetched
+// into pend_* while it runs.
+std::vector<size_t> take_logs(shine_index* h) {
+  std::vector<size_t> todo;
+  for (size_t r = 0; r < h->reps.size(); ++r) {
+    Replica& R = h->reps[r];
+    if (R.pend_clog.empty() && R.pend_rlog.empty()) continue;
+    R.rp_clog.swap(R.pend_clog);
+    R.rp_rlog.swap(R.pend_rlog);
+    R.pend_clog.clear();
+    R.pend_rlog.clear();
+    R.rp_lost = R.pend_lost;
+    R.pend_lost = 0;
+    todo.push_back(r);
+  }
+  return todo;
+}
+
 // replay on every slot with pending logs, one thread each from the handle's pool (8 slots of a 10M-record index filling
-// their caches took ~0.3 s a call one after the other, profiles/r03/config_lines_cfg4_10m.jsonl)
+// their caches took ~0.3 s a call one after the other, profiles/r03/config_lines_cfg4_10m.jsonl).  The caller has
+// waited for a replay still running (wait_replay).
 void replay_all(shine_index* h, std::vector<shine_stats>& per) {
   const size_t G = h->reps.size();
   per.assign(G, shine_stats{});
-  std::vector<size_t> todo;
-  for (size_t r = 0; r < G; ++r)
-    if (!h->reps[r].pend_clog.empty() || !h->reps[r].pend_rlog.empty()) todo.push_back(r);
+  const std::vector<size_t> todo = take_logs(h);
   h->pool.run(todo.size(), [&](size_t i) { replay(h, h->reps[todo[i]], &per[todo[i]]); });
+  for (Replica& R : h->reps) R.dyn_full = R.cache.full();
+}
+
+// Pipelined policy: the replay of the logs fetched so far starts on the pool and runs past the host call's return —
+// through the call's searches, its collection and the caller's time until the next call — instead of holding the
+// call until it ends (a replay of 8 slots took 2.1-2.6 ms against 1.6-1.8 ms of searches in the skew cell,
+// profiles/r06/cache/skew8_replay_timing_inline.txt).  The next host call, and everything else that reads the engine or the
+// arena's state, waits for it first (wait_replay).
+void replay_launch(shine_index* h) {
+  const std::vector<size_t> todo = take_logs(h);
+  h->replay_per.assign(h->reps.size(), shine_stats{});
+  if (todo.empty()) return;
+  h->replay_busy = true;
+  h->pool.launch(todo.size(), [h, todo](size_t i) { replay(h, h->reps[todo[i]], &h->replay_per[todo[i]]); });
+}
+
+// A replay started by replay_launch joined: its updates onto each slot's stream (behind the searches enqueued there
+// so far, ahead of the next ones) and its statistics kept for the next call to report.  The host calls' order of
+// updates and searches on a slot's stream is the same as with the replay inside the call: call n's updates land
+// before call n + 2's searches.
+int wait_replay(shine_index* h) {
+  if (!h->replay_busy) return 0;
+  h->pool.wait();
+  h->replay_busy = false;
+  const size_t G = h->reps.size();
+  if (h->replay_unreported.size() != G) h->replay_unreported.assign(G, shine_stats{});
+  for (size_t r = 0; r < G; ++r) {
+    Replica& R = h->reps[r];
+    R.dyn_full = R.cache.full();
+    const shine_stats& p = h->replay_per[r];
+    shine_stats& u = h->replay_unreported[r];
+    u.cache_admitted += p.cache_admitted;
+    u.cache_evicted += p.cache_evicted;
+    u.cache_rescued += p.cache_rescued;
+    u.cache_log_dropped += p.cache_log_dropped;
+  }
+  for (size_t r = 0; r < G; ++r)
+    if (int rc = enqueue_update(h, h->reps[r])) return rc;
+  return 0;
 }
 
 // Queries per chunk of a large host-API call (the bench's batch) and the chunks in flight per slot: four, as the bench
@@ -1623,8 +1680,9 @@ struct shine_request {
   bool dynamic = false, lagged = false;
   bool rotate = false;                               // chunks start at the slot's next host stream (asynchronous
                                                      // calls in flight spread over the streams), else at stream 0
-  std::vector<shine_stats> per;                      // the lagged replay's statistics
+  std::vector<shine_stats> per;                      // statistics of replays finished since the last call's
   double replay_ms = 0;
+  std::chrono::steady_clock::time_point t_enq, t_launched;  // (SHINE_DEBUG_CACHE_TIMING)
   int rc = SHINE_OK;                                 // an error already met (collected calls drain first)
   bool collected = false;
   shine_stats stats{};
@@ -1652,8 +1710,20 @@ int knn_enqueue(shine_index* h, shine_request& C, const float* queries, const ui
   C.chunked.assign(G, 0);
   C.csize.assign(G, 0);
   C.nchunks.assign(G, 0);
+  C.t_enq = std::chrono::steady_clock::now();
   C.dynamic = h->cache_policy == SHINE_CACHE_DYNAMIC && !C.access;
   C.lagged = C.dynamic && cache_lagged();
+  // a replay still running from the previous call: joined, its updates enqueued ahead of this call's searches, its
+  // statistics reported by this call
+  {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (int rc = wait_replay(h)) return rc;
+    C.replay_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (C.dynamic) {
+      C.per = std::move(h->replay_unreported);
+      h->replay_unreported.clear();
+    }
+  }
   // on an error after the first enqueue, the slots already enqueued are drained before returning
   auto drain = [&](uint32_t upto, int rc) {
     for (uint32_t r = 0; r < upto; ++r) {
@@ -1751,14 +1821,15 @@ int knn_enqueue(shine_index* h, shine_request& C, const float* queries, const ui
     }
     C.chunked[r] = 1;
   }
-  // Dynamic cache, pipelined: the previous call's logs are replayed while this call's searches run, and the updates
-  // go onto each slot's stream behind them (they serve from the next call on)
+  // Dynamic cache, pipelined: the previous call's logs are replayed while this call's searches run and past its
+  // return; the next call enqueues the updates ahead of its searches (they serve from the call after this one on)
+  C.t_launched = std::chrono::steady_clock::now();
   if (C.lagged) {
-    const auto t0 = std::chrono::steady_clock::now();
-    replay_all(h, C.per);
-    C.replay_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    for (uint32_t r = 0; r < G; ++r)
-      if (int rc = enqueue_update(h, h->reps[r])) return drain(G, rc);
+    replay_launch(h);
+    // SHINE_CACHE_ASYNC=0: the replay joined inside the call, while its searches run (the round-5 pipeline; its
+    // updates then land behind this call's searches, its statistics are reported by the next call)
+    if (env_int("SHINE_CACHE_ASYNC", 1) == 0)
+      if (int rc = wait_replay(h)) return drain(G, rc);
   }
   return SHINE_OK;
 }
@@ -1849,6 +1920,7 @@ int knn_collect(shine_index* h, shine_request& C, shine_stats* stats) {
     // this call's logs to the host (device-API searches on other streams of a slot log into the same buffers: the
     // device drains first when one ran)
     const auto t0 = std::chrono::steady_clock::now();
+    const auto t_coll = C.t_launched;
     for (uint32_t r = 0; r < G; ++r) {
       Replica& R = h->reps[r];
       HIP_TRY(hipSetDevice(R.device));
@@ -1861,7 +1933,9 @@ int knn_collect(shine_index* h, shine_request& C, shine_stats* stats) {
     }
     if (int e2 = fetch_logs(h)) return e2;
     if (!C.lagged) {  // the updates before the call returns
-      replay_all(h, C.per);
+      std::vector<shine_stats> now;
+      replay_all(h, now);
+      C.per.insert(C.per.end(), now.begin(), now.end());
       for (uint32_t r = 0; r < G; ++r) {
         if (int e2 = enqueue_update(h, h->reps[r])) return e2;
         HIP_TRY(hipStreamSynchronize(h->reps[r].stream));
@@ -1875,8 +1949,10 @@ int knn_collect(shine_index* h, shine_request& C, shine_stats* stats) {
     }
     if (env_int("SHINE_DEBUG_CACHE_TIMING", 0)) {  // diagnostics: where the time between calls goes
       const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-      std::fprintf(stderr, "cache timing: kernel %.3f ms, replay during the searches %.3f ms, after them %.3f ms, "
-                   "admitted %llu (%s)\n", kernel_ms, C.replay_ms, ms, static_cast<unsigned long long>(agg.cache_admitted),
+      auto d = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+      std::fprintf(stderr, "cache timing: kernel %.3f ms, waited for the previous replay %.3f ms, enqueue %.3f ms, "
+                   "launch to results %.3f ms, after the searches %.3f ms, admitted %llu (%s)\n", kernel_ms, C.replay_ms,
+                   d(C.t_enq, C.t_launched), d(t_coll, t0), ms, static_cast<unsigned long long>(agg.cache_admitted),
                    C.lagged ? "pipelined" : "synchronous");
     }
   }
@@ -1993,7 +2069,10 @@ int shine_prepare(shine_index_t h, uint32_t nq, uint32_t k, uint32_t ef) {
     uint32_t call = 0;
   };
   std::vector<Stash> stash(h->reps.size());
+  std::vector<shine_stats> unreported;
   if (dynamic) {
+    if (int rc = wait_replay(h)) return rc;
+    unreported.swap(h->replay_unreported);
     for (size_t r = 0; r < h->reps.size(); ++r) {
       Replica& R = h->reps[r];
       stash[r].clog.swap(R.pend_clog);
@@ -2039,6 +2118,7 @@ int shine_prepare(shine_index_t h, uint32_t nq, uint32_t k, uint32_t ef) {
       R.pend_lost = stash[r].lost;
       R.dyn_call = stash[r].call;
     }
+    h->replay_unreported.swap(unreported);
   }
   return rc;
 }
@@ -2049,6 +2129,7 @@ int shine_cache_warmup(shine_index_t h, const float* queries, const uint32_t* qu
   if (nq == 0) return SHINE_OK;
   if (!queries) return set_error(SHINE_ERR_ARG, "NULL host pointer");
   std::lock_guard<std::mutex> lk(h->mu);
+  if (int rc = wait_replay(h)) return rc;
   const uint32_t G = static_cast<uint32_t>(h->reps.size());
   if (h->placement == SHINE_PLACE_REPLICA || G < 2 || (h->cached_rows == 0 && h->cached_list_rows == 0))
     return SHINE_OK;  // nothing is cached
@@ -2269,6 +2350,8 @@ int shine_selftest_heap(int is_max, const int32_t* ops, const float* vals, const
 int shine_set_cache_policy(shine_index_t h, int policy, double ratio_percent, uint64_t seed) {
   if (!h) return set_error(SHINE_ERR_ARG, "index handle is NULL");
   std::lock_guard<std::mutex> lk(h->mu);
+  if (int rc = wait_replay(h)) return rc;
+  h->replay_unreported.clear();
   if (policy == SHINE_CACHE_STATIC) {
     for (auto& R : h->reps) {
       HIP_TRY(hipSetDevice(R.device));
@@ -2314,6 +2397,7 @@ int shine_set_cache_policy(shine_index_t h, int policy, double ratio_percent, ui
     HIP_TRY(hipMemsetAsync(R.logn.p, 0, 2 * sizeof(uint32_t), R.stream));
     HIP_TRY(hipStreamSynchronize(R.stream));
     R.cache = RecordCache(static_cast<uint32_t>(entries), seed + R.slot, h->inv_size);  // keys: uids < inv_size
+    R.dyn_full = R.cache.full();
   }
   h->cache_policy = SHINE_CACHE_DYNAMIC;
   h->cache_seed = seed;
@@ -2325,6 +2409,7 @@ int shine_cache_update(shine_index_t h) {
   if (!h) return set_error(SHINE_ERR_ARG, "index handle is NULL");
   std::lock_guard<std::mutex> lk(h->mu);
   if (h->cache_policy != SHINE_CACHE_DYNAMIC) return SHINE_OK;
+  if (int rc = wait_replay(h)) return rc;
   for (auto& R : h->reps) {  // every stream of the slot may have searched: wait for the device
     HIP_TRY(hipSetDevice(R.device));
     HIP_TRY(hipDeviceSynchronize());
@@ -2341,10 +2426,17 @@ int shine_cache_update(shine_index_t h) {
   return SHINE_OK;
 }
 
+int shine_cache_wait(shine_index_t h) {
+  if (!h) return set_error(SHINE_ERR_ARG, "index handle is NULL");
+  std::lock_guard<std::mutex> lk(h->mu);
+  return wait_replay(h);
+}
+
 int shine_cache_keys(shine_index_t h, uint32_t slot, uint32_t* uids, uint64_t cap, uint64_t* n) {
   if (!h || !n) return set_error(SHINE_ERR_ARG, "NULL argument");
   std::lock_guard<std::mutex> lk(h->mu);
   if (slot >= h->reps.size()) return set_error(SHINE_ERR_ARG, "gpu_slot out of range");
+  if (int rc = wait_replay(h)) return rc;  // (the engine as the last call left it)
   const std::vector<uint32_t> keys = h->reps[slot].cache.keys();
   *n = keys.size();
   if (uids) std::copy(keys.begin(), keys.begin() + std::min<uint64_t>(cap, keys.size()), uids);
@@ -2389,6 +2481,10 @@ int shine_selftest_cache(uint32_t entries, uint64_t seed, uint32_t n_calls, cons
 
 int shine_close(shine_index_t h) {
   if (!h) return SHINE_OK;
+  {
+    std::lock_guard<std::mutex> lk(h->mu);
+    (void)wait_replay(h);  // (its updates are dropped with the arena)
+  }
   // requests never waited for: their staging goes back to the pools (freed, once the devices drain, with the rest)
   for (shine_request* q : h->requests) {
     for (uint32_t r = 0; r < q->stage.size() && r < h->reps.size(); ++r) give_stage(h->reps[r], q->stage[r]);

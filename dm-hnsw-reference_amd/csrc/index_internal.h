@@ -218,6 +218,11 @@ struct Replica {
   std::vector<unsigned long long> pend_clog;
   std::vector<uint32_t> pend_rlog;
   uint64_t pend_lost = 0;  // log entries past the device logs' capacity
+  // the logs a replay works on (moved out of pend_* as it starts: the next call's logs are fetched while it runs)
+  std::vector<unsigned long long> rp_clog;
+  std::vector<uint32_t> rp_rlog;
+  uint64_t rp_lost = 0;
+  bool dyn_full = false;  // the engine's full() after its last finished replay (read by launches while one runs)
   std::vector<uint32_t> upd_vec;
   uint32_t upd_drop = 0, upd_fill = 0, upd_cool = 0;
   HostBuf<uint32_t> logn_h, rlog_h;  // pinned landing of the log counts and logs (copies of all slots in flight at once)
@@ -239,6 +244,10 @@ struct Replica {
     pend_clog.clear();
     pend_rlog.clear();
     pend_lost = 0;
+    rp_clog.clear();
+    rp_rlog.clear();
+    rp_lost = 0;
+    dyn_full = false;
     upd_vec.clear();
     upd_drop = upd_fill = upd_cool = 0;
     dev_api_dirty = false;
@@ -301,6 +310,7 @@ class TaskPool {
   TaskPool(const TaskPool&) = delete;
   TaskPool& operator=(const TaskPool&) = delete;
   ~TaskPool() {
+    wait();
     {
       std::lock_guard<std::mutex> lk(m_);
       stop_ = true;
@@ -311,6 +321,7 @@ class TaskPool {
   // f(i) for every i < n, on up to n - 1 pool threads and the caller's; returns when all are done
   void run(size_t n, const std::function<void(size_t)>& f) {
     if (n == 0) return;
+    wait();  // (a launch still running)
     {
       std::lock_guard<std::mutex> lk(m_);
       // a new worker starts from the current generation, so it joins this run, not a finished one
@@ -323,6 +334,27 @@ class TaskPool {
     }
     go_.notify_all();
     for (size_t i; (i = next_.fetch_add(1)) < n;) f(i);
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [this] { return active_ == 0; });
+    f_ = nullptr;
+  }
+  // f(i) for every i < n on n pool threads, returning at once (the caller takes no share); wait() joins it
+  void launch(size_t n, std::function<void(size_t)> f) {
+    if (n == 0) return;
+    wait();
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      while (th_.size() < n) th_.emplace_back([this, g = gen_] { worker(g); });
+      own_ = std::move(f);
+      f_ = &own_;
+      n_ = n;
+      next_ = 0;
+      active_ = th_.size();
+      ++gen_;
+    }
+    go_.notify_all();
+  }
+  void wait() {
     std::unique_lock<std::mutex> lk(m_);
     done_.wait(lk, [this] { return active_ == 0; });
     f_ = nullptr;
@@ -347,6 +379,7 @@ class TaskPool {
   std::mutex m_;
   std::condition_variable go_, done_;
   const std::function<void(size_t)>* f_ = nullptr;
+  std::function<void(size_t)> own_;  // a launch's function
   size_t n_ = 0, active_ = 0;
   std::atomic<size_t> next_{0};
   uint64_t gen_ = 0;
@@ -358,6 +391,10 @@ class TaskPool {
 // The opaque handle of include/shine_gpu.h.
 struct shine_index : shine::IndexState {
   std::vector<shine_request*> requests;  // shine_knn_batch_async calls not waited for yet
+  // the dynamic cache's replay running on the pool past a host call's return (capi.cc replay_launch / wait_replay),
+  // its per-slot statistics, and those of finished replays no call has reported yet
+  bool replay_busy = false;
+  std::vector<shine_stats> replay_per, replay_unreported;
   std::mutex mu;
   shine::TaskPool pool;  // (declared last: its threads stop before the state they work on goes)
 };

@@ -161,6 +161,7 @@ PROTOTYPES = {
     "shine_release_stream": (I32, [P, P]),
     "shine_set_cache_policy": (I32, [P, I32, C.c_double, U64]),
     "shine_cache_update": (I32, [P]),
+    "shine_cache_wait": (I32, [P]),
     "shine_cache_keys": (I32, [P, U32, P, U64, C.POINTER(U64)]),
     "shine_device_ids": (I32, [P, P, U32, P]),
     "shine_selftest_cache": (I32, [U32, U64, U32, P, P, P, P, P, U64, C.POINTER(U64), P]),

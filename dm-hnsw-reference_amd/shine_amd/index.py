@@ -139,6 +139,10 @@ class Index:
     def cache_update(self) -> None:
         L.check(L.lib().shine_cache_update(self._h))
 
+    def cache_wait(self) -> None:
+        """Wait for the pipelined replay of the last call's logs (shine_cache_wait) and enqueue its updates."""
+        L.check(L.lib().shine_cache_wait(self._h))
+
     def cache_keys(self, slot: int) -> np.ndarray:
         """uids the dynamic cache of GPU slot `slot` holds, ascending."""
         n = C.c_uint64()

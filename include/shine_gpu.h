@@ -236,6 +236,13 @@ int shine_cache_warmup(shine_index_t h, const float* queries, const uint32_t* qu
 int shine_set_cache_policy(shine_index_t h, int policy, double ratio_percent, uint64_t seed);
 /* Apply the misses and rescues logged since the last update (shine_knn_batch does this itself after every call). */
 int shine_cache_update(shine_index_t h);
+/* Pipelined policy (the default; SHINE_CACHE_LAG=0 replays inside each call instead): shine_knn_batch starts the
+ * replay of the previous call's logs on the handle's worker threads and returns without waiting for it; the next call
+ * (or any cache function) waits for it and enqueues its updates ahead of its own searches, so call n's admissions
+ * serve from call n + 2 on either way.  This waits for such a replay and enqueues its updates now (a caller timing a
+ * stream of calls ends its clock here).  The replay's statistics (cache_admitted / evicted / rescued) are reported by
+ * the next shine_knn_batch. */
+int shine_cache_wait(shine_index_t h);
 /* Diagnostics: the uids GPU slot `slot`'s dynamic cache holds, ascending (*n = count; up to cap written), and the
  * device ids of uids (0xFFFFFFFF where a uid is not a record). */
 int shine_cache_keys(shine_index_t h, uint32_t slot, uint32_t* uids, uint64_t cap, uint64_t* n);
