@@ -2032,10 +2032,15 @@ __device__ __forceinline__ void issue_list(NbrBuf<D, E, P>& B, const E* __restri
 #ifndef SHINE_FAST_MIN_WAVES
 #define SHINE_FAST_MIN_WAVES 1
 #endif
-template <int D, int R, int VT>
-constexpr int kFastWaves = VT == 2 && D <= 128 && R <= 4 && SHINE_FAST_MIN_WAVES < 3 ? 3 : SHINE_FAST_MIN_WAVES;
+// fp16 rows past d = 128 in two passes a list (cfg 5's TTI shape: MFMA inner products) are held to 256 registers (2
+// per SIMD): unconstrained they took 236 VGPRs + 60 AGPRs, one wavefront per SIMD and 4 per CU whatever the visited
+// tables left, and fit 225 without spilling (f32 rows at d = 200 spill at 256).
+template <int D, int R, int VT, typename E = float, int P = 4>
+constexpr int kFastWaves = VT == 2 && D <= 128 && R <= 4 && SHINE_FAST_MIN_WAVES < 3 ? 3
+                           : std::is_same_v<E, __half> && D > 128 && P <= 2 && SHINE_FAST_MIN_WAVES < 2 ? 2
+                                                                                                    : SHINE_FAST_MIN_WAVES;
 template <int D, int METRIC, typename E, int R, int P, int ACCT, int VT, bool PROF = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kFastWaves<D, R, VT>))) void search_fast_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kFastWaves<D, R, VT, E, P>))) void search_fast_kernel(
     SearchArgs A) {
   PhaseClock<PROF> clk;
   clk.start();
@@ -2126,6 +2131,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kFastWaves<D
       ++st_ll0;  // read_neighborlist (:436-438)
       count_list_read<ACCT>(A, rc, cur, lane);
       PHASE(8)
+      // ACCT = 2: the runner-up's cache words requested as soon as its list is home (it was the youngest load, so this
+      // waits for e's vectors too, which the distances below need anyway): the lookup's round trip overlaps this
+      // expansion's visited test and distances instead of holding the next rows' request back (PHASE(4))
+      if constexpr (ACCT == 2) ncs = cache_word(A.g, nrow);
       bool cand = in_row && e != INV;
       if (!A.g.lists_unique) {  // first occurrence in list order wins (visited.insert order, :443)
 #pragma unroll 1
@@ -2242,7 +2251,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kFastWaves<D
       // runner-up r; its vectors are requested here, one issue point for every path, into the buffer the
       // distances above have just consumed
       PHASE(4)
-      if constexpr (ACCT == 2) ncs = cache_word(A.g, nrow);  // (the runner-up's list: requested one expansion ago)
       u32 pid = r_id;
       if (acc) {
         const float fstar = wave_min(((acc >> lane) & 1ull) ? my_d : INF);
