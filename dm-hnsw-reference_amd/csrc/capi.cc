@@ -810,12 +810,18 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
     // mean-sized table (below) its halved bytes put a seventh wavefront on each CU and make room for next_candidates:
     // 1.28 M against 1.14 M, and the hand-ons for next_candidates capacity drop from 6-13 to 0-1 per call
     // (profiles/r04/env_scan_cfg3_exact.jsonl).  SHINE_EXACT_TWO_CHOICE = 0 / 1 turns it off / on for both sizes.
+    // next_candidates' room in eighths of ef, reserved when wavefronts are counted (the leftover LDS goes to it in the
+    // end anyway): a query that outgrows it is handed on to the next pass (SHINE_EXACT_NEXT_EIGHTHS; 0 keeps the
+    // earlier 5·ef with u16 tables and 4·ef with u32)
+    const int64_t next8 = env_int("SHINE_EXACT_NEXT_EIGHTHS", 0);
+    const uint32_t next16 = next8 > 0 ? static_cast<uint32_t>((next8 * ef + 7) / 8) : 5 * ef;
+    const uint32_t next32 = next8 > 0 ? next16 : 4 * ef;
     auto fit = [&](uint32_t vis_cap, uint32_t& vis16, bool two_choice) {
       auto waves = [&](uint64_t need) {
         return std::max<uint32_t>(1, std::min<uint32_t>(want, static_cast<uint32_t>(lds / need)));
       };
-      const uint32_t w32 = waves(search_lds_bytes(ef, 4 * ef, vis_cap, 4));
-      const uint32_t w16 = waves(search_lds_bytes(ef, 5 * ef, vis_cap, 2));
+      const uint32_t w32 = waves(search_lds_bytes(ef, next32, vis_cap, 4));
+      const uint32_t w16 = waves(search_lds_bytes(ef, next16, vis_cap, 2));
       const int64_t tc = env_int("SHINE_EXACT_TWO_CHOICE", -1);
       const uint32_t kind = bits <= log2_ceil(vis_cap) + 10                                        ? 1u
                             : bits <= log2_ceil(vis_cap) + 12 && (tc == 1 || (tc < 0 && two_choice)) ? 2u
@@ -851,7 +857,7 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
     // Two-choice u32 buckets (vt3_usable) take the same rule at their higher load (SHINE_VT3_LOAD).
     const bool vt3 = vt3_usable(h);
     if (mean_visits && sh.vis16 == 0 && spill_enabled() && spill_hashed(h) && env_int("SHINE_EXACT_LOAD_RULE", 1)) {
-      const uint64_t fixed = top_bytes + align16(8ull * 5 * ef) + 512;
+      const uint64_t fixed = top_bytes + align16(8ull * (next8 > 0 ? next16 : 5 * ef)) + 512;
       auto waves = [&](uint64_t t) {
         return std::min<uint64_t>(want, lds / lds_alloc_bytes(fixed + align16(4ull * t)));
       };

@@ -84,7 +84,8 @@ typedef struct shine_stats {
    * cache.hit_rate = node_cache_hits / node_reads. */
   uint64_t node_reads;            /* node reads: the entry point, upper-level neighbours, fresh level-0 neighbours */
   uint64_t node_cache_hits;       /* ... served by this GPU's cache (static copies or the dynamic cache) */
-  uint64_t cache_admitted;        /* SHINE_CACHE_DYNAMIC, after this call: records admitted ... */
+  uint64_t cache_admitted;        /* SHINE_CACHE_DYNAMIC: by the replays of earlier calls' logs that finished since the
+                                     previous call reported (shine_cache_wait), records admitted ... */
   uint64_t cache_evicted;         /* ... evicted through the cooling table ... */
   uint64_t cache_rescued;         /* ... cooling entries given a second chance by a hit */
   uint64_t cache_log_dropped;     /* admission candidates past the log's capacity (not offered) */
