@@ -775,7 +775,7 @@ uint32_t bitmap_slot_cap(const shine_index* h) {
 // overflows exit at once, and a launch of thousands of them delays the stream's next batch (-7 % QPS at ef = 32).
 LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint32_t ef, int pass,
                        uint32_t handed = 0xFFFFFFFFu, uint32_t learned = 0, uint32_t learned_mean = 0,
-                       uint32_t mean_visits = 0) {
+                       uint32_t mean_visits = 0, uint32_t learned_next = 0) {
   LaunchShape sh{};
   const uint64_t top_bytes = align16(8ull * ef);
   const uint32_t cus = R.cus, lds = R.lds_per_cu;
@@ -810,12 +810,26 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
     // mean-sized table (below) its halved bytes put a seventh wavefront on each CU and make room for next_candidates:
     // 1.28 M against 1.14 M, and the hand-ons for next_candidates capacity drop from 6-13 to 0-1 per call
     // (profiles/r04/env_scan_cfg3_exact.jsonl).  SHINE_EXACT_TWO_CHOICE = 0 / 1 turns it off / on for both sizes.
-    // next_candidates' room in eighths of ef, reserved when wavefronts are counted (the leftover LDS goes to it in the
-    // end anyway): a query that outgrows it is handed on to the next pass (SHINE_EXACT_NEXT_EIGHTHS; 0 keeps the
-    // earlier 5·ef with u16 tables and 4·ef with u32)
+    // next_candidates' room, reserved when wavefronts are counted (the leftover LDS goes to it in the end anyway): a
+    // query that outgrows it is handed on to the next pass.  It was a fixed 5 ef with u16 tables and 4 ef with u32, but
+    // how large next_candidates grows depends on the data: the oracle's largest on a TTI-shaped index is 1.4 ef on
+    // average and 2.3 ef at most (ef = 128, 250), on a SIFT-shaped one 2.2 ef and 3.5 ef (ef = 128), 2.6 and 4.3 at
+    // ef = 64.  So the room is learned: 5/4 of the largest any query of the slot's recent calls held (a query past
+    // the capacity reports capacity + 1, so an undersized room grows back), at least ef plus two lists and at most
+    // the fixed sizes.  3 ef against the fixed sizes put a fourth wavefront on cfg 5's CUs and a fifth or sixth on
+    // cfg 3's and cfg 4's (exact 0.65-0.68 -> 0.74 M, 1.34 -> 1.69 M, 1.52 -> 1.92 M QPS), and cost the SIFT-shaped
+    // bench 37 % (its largest queries were handed on: 2.30 M against 3.62 M; profiles/r06/exact/).
+    // SHINE_EXACT_NEXT_EIGHTHS > 0: a fixed room in eighths of ef (tuning); < 0: the fixed sizes.
     const int64_t next8 = env_int("SHINE_EXACT_NEXT_EIGHTHS", 0);
-    const uint32_t next16 = next8 > 0 ? static_cast<uint32_t>((next8 * ef + 7) / 8) : 5 * ef;
-    const uint32_t next32 = next8 > 0 ? next16 : 4 * ef;
+    const uint32_t floor_next = ef + 2 * h->M0;
+    uint32_t next16 = 5 * ef, next32 = 4 * ef;
+    if (next8 > 0) {
+      next16 = next32 = std::max<uint32_t>(static_cast<uint32_t>((next8 * ef + 7) / 8), floor_next);
+    } else if (next8 == 0 && learned_next > 0) {
+      const uint32_t want_next = std::max<uint32_t>(floor_next, learned_next + learned_next / 4 + 8);
+      next16 = std::min(next16, want_next);
+      next32 = std::min(next32, want_next);
+    }
     auto fit = [&](uint32_t vis_cap, uint32_t& vis16, bool two_choice) {
       auto waves = [&](uint64_t need) {
         return std::max<uint32_t>(1, std::min<uint32_t>(want, static_cast<uint32_t>(lds / need)));
@@ -857,7 +871,7 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
     // Two-choice u32 buckets (vt3_usable) take the same rule at their higher load (SHINE_VT3_LOAD).
     const bool vt3 = vt3_usable(h);
     if (mean_visits && sh.vis16 == 0 && spill_enabled() && spill_hashed(h) && env_int("SHINE_EXACT_LOAD_RULE", 1)) {
-      const uint64_t fixed = top_bytes + align16(8ull * (next8 > 0 ? next16 : 5 * ef)) + 512;
+      const uint64_t fixed = top_bytes + align16(8ull * std::min<uint32_t>(next16, 5 * ef)) + 512;
       auto waves = [&](uint64_t t) {
         return std::min<uint64_t>(want, lds / lds_alloc_bytes(fixed + align16(4ull * t)));
       };
@@ -942,7 +956,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   if (S.ovf.n < 3ull * nq) HIP_TRY(hipStreamSynchronize(s));  // a reallocation must not pull the list from under
   if (int rc = S.ovf.grow(3ull * nq)) return rc;                // an earlier call on this stream
   if (!S.seen_dev) {
-    if (int rc = S.seen.grow(8, hipHostMallocMapped | hipHostMallocPortable)) return rc;
+    if (int rc = S.seen.grow(12, hipHostMallocMapped | hipHostMallocPortable)) return rc;
     void* dp = nullptr;
     HIP_TRY(hipHostGetDevicePointer(&dp, S.seen.p, 0));
     S.seen_dev = static_cast<uint32_t*>(dp);
@@ -971,10 +985,13 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
   if (ef != S.last_ef) S.table_floor = 0;
   if (ef != R.vmax_ef) {
     for (uint32_t& v : R.vmax_recent) v = 0;
+    for (uint32_t& v : R.nmax_recent) v = 0;
     R.vmax_ef = ef;
   }
-  if (ef == S.last_ef && S.seen.p && S.seen.p[3])  // the worst query of the stream's latest finished call
+  if (ef == S.last_ef && S.seen.p && S.seen.p[3]) {  // the worst query of the stream's latest finished call
+    R.nmax_recent[R.vmax_pos % 32] = S.seen.p[8];
     R.vmax_recent[R.vmax_pos++ % 32] = S.seen.p[4];
+  }
   // the fast pass sizes its table for the mean query when it can spill in place; the exact pass keeps the maximum
   // (its tables sized from the mean ran slower, profiles/r03/ab1_merge_spill_tables.jsonl)
   const uint32_t learned = ef != S.last_ef ? 0 : learned_exact_table(S, ef, R.recent_vmax());
@@ -1029,7 +1046,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
         pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu, h->id_space, learned_fast, handed > 0,
                                           elem_is_byte(h->elem), learned_vt3)
                           : pick_shape(h, R, nq, ef, pass, handed, learned, learned_mean,
-                                       i == 0 ? mean_v : 0u);
+                                       i == 0 ? mean_v : 0u, ef == S.last_ef && !fast_mode ? R.recent_nmax() : 0u);
     if (i == 0) {
       S.last_table = sh.vis_cap;
       S.last_fast = pass == PASS_FAST;
@@ -1090,6 +1107,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
     a.log_cap = kLogCap;
     a.counter = S.counter.p + i;
     a.vis_max = S.counter.p + 3;
+    a.next_max = S.counter.p + 10;
     a.vis_sum = i == 0 ? S.counter.p + 8 : nullptr;  // the main pass's queries only: a hand-on counts once
     a.spill_count = i == 0 ? S.counter.p + 9 : nullptr;
     a.fast = pass == PASS_FAST ? 1u : 0u;

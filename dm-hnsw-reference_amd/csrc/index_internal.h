@@ -185,10 +185,16 @@ struct Replica {
   // the worst query's visits of the latest finished call on a stream, as seen at the slot's last 32 enqueues at
   // `vmax_ef` on any of its streams: the learned tables size for the recent batches, not one stream's last
   uint32_t vmax_recent[32] = {};
+  uint32_t nmax_recent[32] = {};  // ... and its largest next_candidates (exact passes), at the same enqueues
   uint32_t vmax_pos = 0, vmax_ef = 0;
   uint32_t recent_vmax() const {
     uint32_t m = 0;
     for (uint32_t v : vmax_recent) m = v > m ? v : m;
+    return m;
+  }
+  uint32_t recent_nmax() const {
+    uint32_t m = 0;
+    for (uint32_t v : nmax_recent) m = v > m ? v : m;
     return m;
   }
   hipStream_t stream = nullptr;

@@ -50,7 +50,7 @@ struct DevGraph {
 };
 
 // Counter words of one call on a stream (SearchArgs::call_counters).
-constexpr uint32_t kCallWords = 10;
+constexpr uint32_t kCallWords = 11;
 
 // Per-query counter words (u32) written by the search kernels; include/shine_gpu.h SHINE_QS_*.
 constexpr uint32_t kQsWords = 12;
@@ -79,13 +79,17 @@ struct SearchArgs {
   uint32_t* access;          // cache warmup (nullable): per device id, reads of the record (vector or list)
   uint32_t* call_counters;   // last pass of a call (nullable): the call's kCallWords counter words; the last workgroup
   uint32_t* host_counts;     // to finish copies words 4..6 to host_counts[0..2] (host memory), sets host_counts[3] = 1,
-                             // copies words 3 and 8 to host_counts[4] and [5], the call's nq to [6], and zeroes the words for the next call
+                             // copies words 3 and 8 to host_counts[4] and [5], the call's nq to [6], words 9 and 10 to
+                             // [7] and [8], and zeroes the words for the next call
                              // on the stream (word 7 counts finished groups)
   uint32_t* call_out;        // last pass (nullable): call_out[0] = the queries the call's passes handed on (words 4..6
                              // summed), call_out[1] = 1 — a per-call copy (host_counts is the stream's, and a later call
                              // on the stream may overwrite it before the host reads it)
   uint32_t* vis_max;         // every pass (nullable): the call's counter word 3, the most nodes any query marked
                              // visited (atomicMax per query) — sizes the next call's visited tables
+  uint32_t* next_max;        // exact passes (nullable): the call's counter word 10, the most next_candidates entries
+                             // any query held (atomicMax per query; past the capacity: capacity + 1) — sizes the next
+                             // call's reservation for them (capi.cc pick_shape)
   uint32_t* vis_sum;         // every pass (nullable): the call's counter word 8, the nodes its queries marked visited
                              // (atomicAdd per query; copied to host_counts[5]) — the mean sizes spilling tables
   unsigned long long* prof; // diagnostics (nullable): per-phase shader-clock totals, PROF kernel variant only

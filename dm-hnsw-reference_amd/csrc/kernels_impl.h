@@ -1505,6 +1505,7 @@ __device__ __forceinline__ void finish_call(const SearchArgs& A, int lane) {
   host[5] = __atomic_load_n(&c[8], __ATOMIC_RELAXED);
   host[6] = A.nq;  // the call the sum belongs to (several calls may be in flight on the stream)
   host[7] = __atomic_load_n(&c[9], __ATOMIC_RELAXED);
+  host[8] = __atomic_load_n(&c[10], __ATOMIC_RELAXED);
   host[3] = 1u;
   if (A.call_out) {
     volatile u32* co = A.call_out;
@@ -1840,7 +1841,11 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
           pass &= pass - 1;
           const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_d), j));
           if (d < key(troot) || ntop < ef) {
-            if (nnext >= cap) { status = ST_OVERFLOW; break; }
+            if (nnext >= cap) {
+              status = ST_OVERFLOW;
+              st_maxnext = static_cast<u32>(cap) + 1u;  // (it needed more: the next call reserves more)
+              break;
+            }
             const u32 id = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(my_id), j));
             const u64 en = mk(d, id);
             // next_candidates.push (:462) and top_candidates.push_k (heap.hh:34-41) touch different heaps: the
@@ -1902,6 +1907,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs A) {
     }
     if (status == ST_OVERFLOW && A.out_list && lane == 0) A.out_list[atomicAdd(A.out_count, 1u)] = qi;
     if (A.vis_max && lane == 0) atomicMax(A.vis_max, nvis);
+    if (A.next_max && lane == 0) atomicMax(A.next_max, st_maxnext);
     // visited-table occupancy, for the next call's shape (capped at the largest table, so that the call's sum cannot
     // wrap below 2^18 queries)
     if (A.vis_sum && lane == 0) atomicAdd(A.vis_sum, nvis < 16384u ? nvis : 16384u);
