@@ -501,6 +501,7 @@ enum PassKind { PASS_LDS = 0, PASS_WHOLE_CU = 1, PASS_LIGHT = 2, PASS_GLOBAL = 3
 
 struct LaunchShape {
   uint32_t cap, grid, vis_cap, vis_limit;
+  uint32_t waves;            // wavefronts per CU the LDS shares allow
   uint32_t vis16, vis_bits;  // fast kernel: u16 quotient visited entries over a vis_bits-bit id space
 };
 
@@ -773,9 +774,10 @@ uint32_t bitmap_slot_cap(const shine_index* h) {
 // handed: queries the main pass handed on in an earlier call on this stream.  The light pass gets slots for twice
 // that (at least one per CU, at most what LDS shares and bitmap memory allow): its workgroups of a call with few
 // overflows exit at once, and a launch of thousands of them delays the stream's next batch (-7 % QPS at ef = 32).
-LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint32_t ef, int pass,
-                       uint32_t handed = 0xFFFFFFFFu, uint32_t learned = 0, uint32_t learned_mean = 0,
-                       uint32_t mean_visits = 0, uint32_t learned_next = 0) {
+// room8: next_candidates' room the exact pass reserves per wavefront, in eighths of ef (0: the fixed 5 ef with u16
+// tables and 4 ef with u32); see pick_shape below
+LaunchShape pick_shape_room(const shine_index* h, const Replica& R, uint32_t nq, uint32_t ef, int pass, uint32_t handed,
+                            uint32_t learned, uint32_t learned_mean, uint32_t mean_visits, int64_t room8) {
   LaunchShape sh{};
   const uint64_t top_bytes = align16(8ull * ef);
   const uint32_t cus = R.cus, lds = R.lds_per_cu;
@@ -810,26 +812,9 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
     // mean-sized table (below) its halved bytes put a seventh wavefront on each CU and make room for next_candidates:
     // 1.28 M against 1.14 M, and the hand-ons for next_candidates capacity drop from 6-13 to 0-1 per call
     // (profiles/r04/env_scan_cfg3_exact.jsonl).  SHINE_EXACT_TWO_CHOICE = 0 / 1 turns it off / on for both sizes.
-    // next_candidates' room, reserved when wavefronts are counted (the leftover LDS goes to it in the end anyway): a
-    // query that outgrows it is handed on to the next pass.  It was a fixed 5 ef with u16 tables and 4 ef with u32, but
-    // how large next_candidates grows depends on the data: the oracle's largest on a TTI-shaped index is 1.4 ef on
-    // average and 2.3 ef at most (ef = 128, 250), on a SIFT-shaped one 2.2 ef and 3.5 ef (ef = 128), 2.6 and 4.3 at
-    // ef = 64.  So the room is learned: 5/4 of the largest any query of the slot's recent calls held (a query past
-    // the capacity reports capacity + 1, so an undersized room grows back), at least ef plus two lists and at most
-    // the fixed sizes.  3 ef against the fixed sizes put a fourth wavefront on cfg 5's CUs and a fifth or sixth on
-    // cfg 3's and cfg 4's (exact 0.65-0.68 -> 0.74 M, 1.34 -> 1.69 M, 1.52 -> 1.92 M QPS), and cost the SIFT-shaped
-    // bench 37 % (its largest queries were handed on: 2.30 M against 3.62 M; profiles/r06/exact/).
-    // SHINE_EXACT_NEXT_EIGHTHS > 0: a fixed room in eighths of ef (tuning); < 0: the fixed sizes.
-    const int64_t next8 = env_int("SHINE_EXACT_NEXT_EIGHTHS", 0);
-    const uint32_t floor_next = ef + 2 * h->M0;
+    // next_candidates' room (pick_shape), reserved when wavefronts are counted; the leftover LDS goes to it in the end
     uint32_t next16 = 5 * ef, next32 = 4 * ef;
-    if (next8 > 0) {
-      next16 = next32 = std::max<uint32_t>(static_cast<uint32_t>((next8 * ef + 7) / 8), floor_next);
-    } else if (next8 == 0 && learned_next > 0) {
-      const uint32_t want_next = std::max<uint32_t>(floor_next, learned_next + learned_next / 4 + 8);
-      next16 = std::min(next16, want_next);
-      next32 = std::min(next32, want_next);
-    }
+    if (room8 > 0) next16 = next32 = std::max<uint32_t>(static_cast<uint32_t>((room8 * ef + 7) / 8), ef + 2 * h->M0);
     auto fit = [&](uint32_t vis_cap, uint32_t& vis16, bool two_choice) {
       auto waves = [&](uint64_t need) {
         return std::max<uint32_t>(1, std::min<uint32_t>(want, static_cast<uint32_t>(lds / need)));
@@ -911,6 +896,7 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
   // has no overflow exit (a 64-entry table, forced by the test hook at M0 = 16, filled up and probed forever)
   sh.vis_limit = std::min<uint32_t>(sh.vis_cap / 8 * 7, sh.vis_cap > h->M0 ? sh.vis_cap - h->M0 : 0u);
   sh.grid = std::max<uint32_t>(1, std::min<uint32_t>(nq, cus * wpc));
+  sh.waves = wpc;
   if (pass == PASS_LIGHT) {
     sh.grid = std::min(sh.grid, bitmap_slot_cap(h));
     // at least 64 slots: a call whose main pass hands on nothing launches few workgroups that exit at once (64
@@ -920,6 +906,27 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
     sh.grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(sh.grid, want)));
   }
   return sh;
+}
+
+// The exact pass's next_candidates room.  A query that outgrows the capacity is handed on to the next pass.  How
+// large next_candidates grows depends on the data: the oracle's largest on a TTI-shaped index is 1.4 ef on average
+// and 2.3 ef at most (ef = 128, 250), on a SIFT-shaped one 2.2 and 3.5 ef (ef = 128), 2.6 and 4.3 ef at ef = 64 — a
+// heavy tail, so the most any recent query held (reported in call word 10) would reserve for the outliers.  The fixed
+// 5 ef (u16 tables) / 4 ef (u32) stay where they leave more than 6 wavefronts per CU; below that, 3 ef puts another
+// wavefront or two on each CU and the few queries past it are handed on: exact cfg 5 (50M) 0.65-0.68 -> 0.74 M, cfg 3
+// (10M) 1.34 -> 1.69 M, cfg 4 (100M) 1.52 -> 1.92 M QPS.  At the SIFT-shaped bench (11 wavefronts per CU) 3 ef cost
+// 37 % (2.30 M against 3.62 M: its launches are short, and the hand-on pass after each one is not; profiles/r06/exact/).
+// SHINE_EXACT_NEXT_EIGHTHS > 0: that room everywhere, < 0: the fixed sizes everywhere (tuning).
+LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint32_t ef, int pass,
+                       uint32_t handed = 0xFFFFFFFFu, uint32_t learned = 0, uint32_t learned_mean = 0,
+                       uint32_t mean_visits = 0) {
+  const int64_t room8 = env_int("SHINE_EXACT_NEXT_EIGHTHS", 0);
+  if (pass != PASS_LDS || room8 != 0)
+    return pick_shape_room(h, R, nq, ef, pass, handed, learned, learned_mean, mean_visits, std::max<int64_t>(room8, 0));
+  const LaunchShape fixed = pick_shape_room(h, R, nq, ef, pass, handed, learned, learned_mean, mean_visits, 0);
+  if (fixed.waves > 6) return fixed;
+  const LaunchShape tight = pick_shape_room(h, R, nq, ef, pass, handed, learned, learned_mean, mean_visits, 24);
+  return tight.waves > fixed.waves ? tight : fixed;
 }
 
 Scratch& scratch_for(Replica& R, hipStream_t s) {
@@ -1046,7 +1053,7 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
         pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu, h->id_space, learned_fast, handed > 0,
                                           elem_is_byte(h->elem), learned_vt3)
                           : pick_shape(h, R, nq, ef, pass, handed, learned, learned_mean,
-                                       i == 0 ? mean_v : 0u, ef == S.last_ef && !fast_mode ? R.recent_nmax() : 0u);
+                                       i == 0 ? mean_v : 0u);
     if (i == 0) {
       S.last_table = sh.vis_cap;
       S.last_fast = pass == PASS_FAST;
@@ -1054,10 +1061,11 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
       S.last_learned = (learned_fast != 0 && sh.vis_cap == learned_fast) || (learned_vt3 != 0 && sh.vis16 == 3) ||
                        (pass != PASS_FAST && learned != 0 && sh.vis_cap == learned);
       if (env_int("SHINE_DEBUG_SHAPE", 0))  // diagnostics: the main pass's shape and what it was learned from
-        std::fprintf(stderr, "shape: pass %d nq %u ef %u table %u vis16 %u grid %u learned %u vmax %u handed %u floor %u "
-                     "spill_hash %u learned_fast %u\n",
-                     pass, nq, ef, sh.vis_cap, sh.vis16, sh.grid, learned, S.seen.p[3] ? S.seen.p[4] : 0u, handed,
-                     S.table_floor, spill_hashed(h) ? spill_hash_entries(sh.vis_cap) : 0u, learned_fast);
+        std::fprintf(stderr, "shape: pass %d nq %u ef %u table %u vis16 %u grid %u waves %u cap %u learned %u vmax %u "
+                     "next_max %u handed %u floor %u spill_hash %u learned_fast %u\n",
+                     pass, nq, ef, sh.vis_cap, sh.vis16, sh.grid, sh.waves, sh.cap, learned,
+                     S.seen.p[3] ? S.seen.p[4] : 0u, R.recent_nmax(), handed, S.table_floor,
+                     spill_hashed(h) ? spill_hash_entries(sh.vis_cap) : 0u, learned_fast);
     }
     SearchArgs a{};
     a.g = dev_graph(h, R);
