@@ -912,10 +912,12 @@ LaunchShape pick_shape_room(const shine_index* h, const Replica& R, uint32_t nq,
 // large next_candidates grows depends on the data: the oracle's largest on a TTI-shaped index is 1.4 ef on average
 // and 2.3 ef at most (ef = 128, 250), on a SIFT-shaped one 2.2 and 3.5 ef (ef = 128), 2.6 and 4.3 ef at ef = 64 — a
 // heavy tail, so the most any recent query held (reported in call word 10) would reserve for the outliers.  The fixed
-// 5 ef (u16 tables) / 4 ef (u32) stay where they leave more than 6 wavefronts per CU; below that, 3 ef puts another
-// wavefront or two on each CU and the few queries past it are handed on: exact cfg 5 (50M) 0.65-0.68 -> 0.74 M, cfg 3
-// (10M) 1.34 -> 1.69 M, cfg 4 (100M) 1.52 -> 1.92 M QPS.  At the SIFT-shaped bench (11 wavefronts per CU) 3 ef cost
-// 37 % (2.30 M against 3.62 M: its launches are short, and the hand-on pass after each one is not; profiles/r06/exact/).
+// 5 ef (u16 tables) / 4 ef (u32) stay where they leave more than 8 wavefronts per CU; at 8 or fewer 3 ef is taken
+// unless it leaves fewer: another wavefront or two on each CU (cfg 3: 7 -> 9) or a larger table at the same count (cfg
+// 5: 4 per CU, 7,104 -> ~7,900 two-choice u32 entries), the few queries past it handed on: exact cfg 5 (50M) 0.65-0.68
+// -> 0.74 M, cfg 3 (10M) 1.34 -> 1.69 M, cfg 4 (100M) 1.52 -> 1.92 M QPS.  At the SIFT-shaped bench (11 wavefronts per
+// CU) 3 ef cost 37 % (2.30 M against 3.62 M: its launches are short, and the hand-on pass after each one is not;
+// profiles/r06/exact/).
 // SHINE_EXACT_NEXT_EIGHTHS > 0: that room everywhere, < 0: the fixed sizes everywhere (tuning).
 LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint32_t ef, int pass,
                        uint32_t handed = 0xFFFFFFFFu, uint32_t learned = 0, uint32_t learned_mean = 0,
@@ -924,9 +926,9 @@ LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint
   if (pass != PASS_LDS || room8 != 0)
     return pick_shape_room(h, R, nq, ef, pass, handed, learned, learned_mean, mean_visits, std::max<int64_t>(room8, 0));
   const LaunchShape fixed = pick_shape_room(h, R, nq, ef, pass, handed, learned, learned_mean, mean_visits, 0);
-  if (fixed.waves > 6) return fixed;
+  if (fixed.waves > 8) return fixed;
   const LaunchShape tight = pick_shape_room(h, R, nq, ef, pass, handed, learned, learned_mean, mean_visits, 24);
-  return tight.waves > fixed.waves ? tight : fixed;
+  return tight.waves >= fixed.waves ? tight : fixed;
 }
 
 Scratch& scratch_for(Replica& R, hipStream_t s) {
