@@ -105,6 +105,27 @@ def test_overflow_rerun_path(gpu_available, monkeypatch):
     _check_same(r, *ref)
 
 
+def test_tight_next_room_hands_on_and_matches(gpu_available, capfd, monkeypatch):
+    """ef = 400 and 2,048 queries: the fixed next_candidates room (5 ef) leaves 5 wavefronts per CU, so the exact pass
+    reserves 3 ef (capi.cc pick_shape, 7 per CU) and its capacity is what that LDS share leaves; queries that outgrow it
+    are handed on to the next pass.  The shape line shows the pick; every query must still equal the oracle bit for
+    bit."""
+    monkeypatch.setenv("SHINE_DEBUG_SHAPE", "1")
+    base = D.sift_like(3000, seed=51)
+    q = D.sift_like(2048, seed=52)
+    dumps, _, _ = O.build(base, 16, 100, 0, 1, seed=7)
+    ref = O.OracleIndex(dumps, 128, 16, 0).knn(q, 10, 400)
+    with shine_amd.Index.from_buffers(dumps, 128, 16, 0, gpus=[0]) as idx:
+        for _ in range(2):  # (the second call's table is learned from the first)
+            r = idx.knn(q, 10, 400)
+            _check_same(r, *ref)
+    shapes = [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith("shape: pass 0")]
+    assert shapes
+    f = shapes[-1].split()
+    waves, cap = int(f[f.index("waves") + 1]), int(f[f.index("cap") + 1])
+    assert 5 < waves <= 16 and cap < 5 * 400  # the 3 ef room was taken: more wavefronts, a capacity below 5 ef
+
+
 def test_repeated_batches_keep_visited_clean(gpu_available):
     """The visited bitmaps are cleared per query from the visited log: re-running must not change anything."""
     base = D.sift_like(5000, seed=21)
