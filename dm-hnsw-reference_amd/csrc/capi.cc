@@ -502,6 +502,7 @@ enum PassKind { PASS_LDS = 0, PASS_WHOLE_CU = 1, PASS_LIGHT = 2, PASS_GLOBAL = 3
 struct LaunchShape {
   uint32_t cap, grid, vis_cap, vis_limit;
   uint32_t waves;            // wavefronts per CU the LDS shares allow
+  uint32_t tight;            // exact pass: 1 = the tight next_candidates room was taken (pick_shape)
   uint32_t vis16, vis_bits;  // fast kernel: u16 quotient visited entries over a vis_bits-bit id space
 };
 
@@ -919,15 +920,24 @@ LaunchShape pick_shape_room(const shine_index* h, const Replica& R, uint32_t nq,
 // CU) 3 ef cost 37 % (2.30 M against 3.62 M: its launches are short, and the hand-on pass after each one is not;
 // profiles/r06/exact/).
 // SHINE_EXACT_NEXT_EIGHTHS > 0: that room everywhere, < 0: the fixed sizes everywhere (tuning).
+// The room is a cliff: at cfg 4, 3 ef hands on 3-4 % of a call's queries and runs at 1.90 M, 2.5 ef at 1.03 M and
+// 2 ef at 0.51 M (profiles/r06/exact/scale_cfg4_100m_room_scan.jsonl).  So a stream whose call handed on more than 1/12
+// of its queries with the tight room keeps the fixed room at that ef from then on (allow_tight, Scratch::tight_off_ef).
 LaunchShape pick_shape(const shine_index* h, const Replica& R, uint32_t nq, uint32_t ef, int pass,
                        uint32_t handed = 0xFFFFFFFFu, uint32_t learned = 0, uint32_t learned_mean = 0,
-                       uint32_t mean_visits = 0) {
+                       uint32_t mean_visits = 0, bool allow_tight = true) {
   const int64_t room8 = env_int("SHINE_EXACT_NEXT_EIGHTHS", 0);
-  if (pass != PASS_LDS || room8 != 0)
-    return pick_shape_room(h, R, nq, ef, pass, handed, learned, learned_mean, mean_visits, std::max<int64_t>(room8, 0));
-  const LaunchShape fixed = pick_shape_room(h, R, nq, ef, pass, handed, learned, learned_mean, mean_visits, 0);
-  if (fixed.waves > 8) return fixed;
-  const LaunchShape tight = pick_shape_room(h, R, nq, ef, pass, handed, learned, learned_mean, mean_visits, 24);
+  if (pass != PASS_LDS || room8 != 0) {
+    LaunchShape sh =
+        pick_shape_room(h, R, nq, ef, pass, handed, learned, learned_mean, mean_visits, std::max<int64_t>(room8, 0));
+    sh.tight = pass == PASS_LDS && room8 > 0 ? 1u : 0u;
+    return sh;
+  }
+  LaunchShape fixed = pick_shape_room(h, R, nq, ef, pass, handed, learned, learned_mean, mean_visits, 0);
+  fixed.tight = 0;
+  if (fixed.waves > 8 || !allow_tight) return fixed;
+  LaunchShape tight = pick_shape_room(h, R, nq, ef, pass, handed, learned, learned_mean, mean_visits, 24);
+  tight.tight = 1;
   return tight.waves >= fixed.waves ? tight : fixed;
 }
 
@@ -992,6 +1002,8 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
       S.table_floor = std::max(S.table_floor, pow2_at_least(2 * S.last_table));
   }
   if (ef != S.last_ef) S.table_floor = 0;
+  // the tight next_candidates room handed on too many of the last call's queries: the fixed room at this ef from now
+  if (S.last_tight && ef == S.last_ef && S.seen.p[3] && handed * 12 > S.seen.p[6]) S.tight_off_ef = ef;
   if (ef != R.vmax_ef) {
     for (uint32_t& v : R.vmax_recent) v = 0;
     for (uint32_t& v : R.nmax_recent) v = 0;
@@ -1055,10 +1067,11 @@ int enqueue_search(shine_index* h, Replica& R, const float* d_q, uint32_t nq, ui
         pass == PASS_FAST ? pick_fast_shape(nq, ef, R.cus, R.lds_per_cu, h->id_space, learned_fast, handed > 0,
                                           elem_is_byte(h->elem), learned_vt3)
                           : pick_shape(h, R, nq, ef, pass, handed, learned, learned_mean,
-                                       i == 0 ? mean_v : 0u);
+                                       i == 0 ? mean_v : 0u, S.tight_off_ef != ef);
     if (i == 0) {
       S.last_table = sh.vis_cap;
       S.last_fast = pass == PASS_FAST;
+      S.last_tight = pass == PASS_LDS && sh.tight;
       // the table came from learning, not the fixed rule
       S.last_learned = (learned_fast != 0 && sh.vis_cap == learned_fast) || (learned_vt3 != 0 && sh.vis16 == 3) ||
                        (pass != PASS_FAST && learned != 0 && sh.vis_cap == learned);

@@ -144,6 +144,8 @@ struct Scratch {
   uint32_t last_ef = 0;          // ef of the last call: what it visited says nothing about another ef
   uint32_t last_nq = 0;          // queries of the last call (seen[5] / last_nq: the mean a query marked visited)
   bool last_fast = false;        // the last call's main pass was the fast kernel
+  bool last_tight = false;       // the last call's exact pass reserved the tight next_candidates room (capi.cc pick_shape)
+  uint32_t tight_off_ef = 0;     // ... and handed on more than 1/12 of its queries for it: not again at this ef
   void release() {
     for (auto* b : {&visited, &vlog, &counter, &ovf, &qs, &spill_flags}) b->release();
     heaps.release();
