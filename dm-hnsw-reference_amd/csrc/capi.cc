@@ -861,10 +861,27 @@ LaunchShape pick_shape_room(const shine_index* h, const Replica& R, uint32_t nq,
       auto waves = [&](uint64_t t) {
         return std::min<uint64_t>(want, lds / lds_alloc_bytes(fixed + align16(4ull * t)));
       };
-      const uint64_t t0 = (static_cast<uint64_t>(mean_visits) * 1000 / (vt3 ? vt3_load_permille(false) : 450) + 63) / 64 * 64;
-      const uint64_t w = std::max<uint64_t>(1, waves(t0));
-      const uint64_t per = lds / w / 1024 * 1024;
-      const uint64_t t = per > fixed + 4096 ? std::min<uint64_t>(16384, (per - fixed) / 4 / 64 * 64) : 0;
+      // (t0: the table at the load; w: the wavefronts it leaves; t: the largest table at w)
+      auto rule = [&](uint32_t load_permille, uint64_t& t0, uint64_t& w, uint64_t& t) {
+        t0 = (static_cast<uint64_t>(mean_visits) * 1000 / load_permille + 63) / 64 * 64;
+        w = std::max<uint64_t>(1, waves(t0));
+        const uint64_t per = lds / w / 1024 * 1024;
+        t = per > fixed + 4096 ? std::min<uint64_t>(16384, (per - fixed) / 4 / 64 * 64) : 0;
+      };
+      uint64_t t0 = 0, w = 0, t = 0;
+      rule(vt3 ? vt3_load_permille(false) : 450, t0, w, t);
+      // two-choice tables where the load leaves 4 wavefronts per CU or fewer: a fuller table (0.72) for one more
+      // wavefront — cfg 5 50M exact 0.75 -> 0.79 M; at cfg 4's 7 per CU 0.72 lost (1.81 against 1.90 M,
+      // profiles/r06/exact/scale_cfg*_vt3_exact_load_scan.jsonl).  SHINE_VT3_EXACT_LOAD sets the load outright.
+      if (vt3 && w <= 4 && !std::getenv("SHINE_VT3_EXACT_LOAD") && !std::getenv("SHINE_VT3_LOAD")) {
+        uint64_t t0b = 0, wb = 0, tb = 0;
+        rule(720, t0b, wb, tb);
+        if (wb > w && tb >= t0b && tb >= 1024) {
+          t0 = t0b;
+          w = wb;
+          t = tb;
+        }
+      }
       if (t >= t0 && t >= 1024 && w > wpc) {
         sh.vis_cap = static_cast<uint32_t>(t);
         sh.vis16 = vt3 ? 3u : 0u;
